@@ -1,0 +1,166 @@
+"""ctypes binding of include/cfd2_amd.h (the C ABI of the native library).
+
+The library is built in-tree by ``__graft_entry__.build()`` into
+``cfd2_amd/_lib/libcfd2_amd.so``.  There is no fallback: if the library is
+missing, importing the solver raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libcfd2_amd.so")
+
+u32p = C.POINTER(C.c_uint32)
+f64p = C.POINTER(C.c_double)
+
+
+class MeshView(C.Structure):
+    _fields_ = [
+        ("num_cells", C.c_uint32),
+        ("num_faces", C.c_uint32),
+        ("face_owner", u32p),
+        ("face_neighbor", u32p),
+        ("face_boundary", u32p),
+        ("face_area", f64p),
+        ("face_nx", f64p),
+        ("face_ny", f64p),
+        ("face_cx", f64p),
+        ("face_cy", f64p),
+        ("cell_cx", f64p),
+        ("cell_cy", f64p),
+        ("cell_vol", f64p),
+        ("cell_face_offsets", u32p),
+        ("cell_faces", u32p),
+    ]
+
+
+class Geometry(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("p", C.c_double * 8)]
+
+
+class Constants(C.Structure):
+    _fields_ = [
+        ("dt", C.c_float),
+        ("dt_old", C.c_float),
+        ("time", C.c_float),
+        ("viscosity", C.c_float),
+        ("density", C.c_float),
+        ("component", C.c_uint32),
+        ("alpha_p", C.c_float),
+        ("scheme", C.c_uint32),
+        ("alpha_u", C.c_float),
+        ("stride_x", C.c_uint32),
+        ("time_scheme", C.c_uint32),
+        ("inlet_velocity", C.c_float),
+        ("ramp_time", C.c_float),
+        ("precond_type", C.c_uint32),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_outer_correctors", C.c_int32),
+        ("convergence_lag", C.c_int32),
+        ("fixed_outer", C.c_int32),
+        ("fixed_inner", C.c_int32),
+        ("max_restart", C.c_int32),
+        ("max_outer_restarts", C.c_int32),
+        ("fgmres_rtol", C.c_float),
+        ("fgmres_atol", C.c_float),
+        ("log_level", C.c_int32),
+        ("use_graphs", C.c_int32),
+    ]
+
+
+class LinearStats(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_uint32),
+        ("residual", C.c_float),
+        ("converged", C.c_int32),
+        ("diverged", C.c_int32),
+        ("time_s", C.c_double),
+    ]
+
+
+class StepInfo(C.Structure):
+    _fields_ = [
+        ("should_stop", C.c_int32),
+        ("degenerate_count", C.c_uint32),
+        ("steady_state_count", C.c_uint32),
+        ("outer_residual_u", C.c_float),
+        ("outer_residual_p", C.c_float),
+        ("outer_iterations", C.c_uint32),
+        ("stats_p", LinearStats),
+        ("total_linear_iterations", C.c_uint32),
+    ]
+
+
+def default_config(**overrides) -> Config:
+    cfg = Config(
+        n_outer_correctors=20,
+        convergence_lag=1,
+        fixed_outer=0,
+        fixed_inner=0,
+        max_restart=50,
+        max_outer_restarts=20,
+        fgmres_rtol=1e-5,
+        fgmres_atol=1e-7,
+        log_level=0,
+        use_graphs=0,
+    )
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+# Every symbol include/cfd2_amd.h declares (checked by tests/test_capi.py).
+EXPORTED = [
+    "cfd_last_error",
+    "cfd_mesh_generate_cut_cell", "cfd_mesh_smooth", "cfd_mesh_max_skewness", "cfd_mesh_get_view",
+    "cfd_mesh_get_vertices", "cfd_mesh_save", "cfd_mesh_load", "cfd_mesh_destroy",
+    "cfd_config_default", "cfd_solver_create", "cfd_solver_destroy", "cfd_set_u", "cfd_set_p",
+    "cfd_get_constants", "cfd_set_constants", "cfd_set_dt", "cfd_set_viscosity", "cfd_set_alpha_p",
+    "cfd_set_alpha_u", "cfd_set_density", "cfd_set_scheme", "cfd_set_time_scheme",
+    "cfd_set_inlet_velocity", "cfd_set_ramp_time", "cfd_set_precond_type", "cfd_update_constants",
+    "cfd_initialize_history", "cfd_step", "cfd_get_u", "cfd_get_p", "cfd_get_d_p",
+    "cfd_get_step_info", "cfd_num_cells", "cfd_num_faces", "cfd_profile_enable", "cfd_profile_reset",
+    "cfd_profile_smoother", "cfd_amg_levels", "cfd_step_algorithmic_bytes", "cfd_debug_buffer",
+    "cfd_debug_buffer_len", "cfd_debug_prepare_assemble",
+]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the native library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"native library not built: {LIB_PATH} (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.cfd_last_error.restype = C.c_char_p
+    L.cfd_mesh_generate_cut_cell.argtypes = [C.POINTER(Geometry), C.c_double, C.c_double, C.c_double,
+                                             C.c_double, C.c_double, C.POINTER(vp)]
+    L.cfd_mesh_smooth.argtypes = [vp, C.POINTER(Geometry), C.c_double, C.c_int32, C.POINTER(C.c_int32)]
+    L.cfd_mesh_max_skewness.argtypes = [vp]
+    L.cfd_mesh_max_skewness.restype = C.c_double
+    L.cfd_mesh_get_view.argtypes = [vp, C.POINTER(MeshView)]
+    L.cfd_mesh_get_vertices.argtypes = [vp, C.POINTER(C.c_uint32), C.POINTER(f64p), C.POINTER(f64p),
+                                        C.POINTER(C.POINTER(C.c_uint8))]
+    L.cfd_mesh_save.argtypes = [vp, C.c_char_p]
+    L.cfd_mesh_load.argtypes = [C.c_char_p, C.POINTER(vp)]
+    L.cfd_mesh_destroy.argtypes = [vp]
+    L.cfd_mesh_destroy.restype = None
+    _lib = L
+    return L
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().cfd_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")

@@ -1,0 +1,177 @@
+"""Mesh input of the hot path: mirror of ``cfd2::solver::mesh``.
+
+``generate_cut_cell_mesh`` / ``Mesh.smooth`` run the native C++ restatement of
+src/solver/mesh/cut_cell.rs:10-510 and structs.rs:159-292 (deterministic, f64).
+Arrays are exposed as zero-copy numpy views of the native mesh.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi
+
+
+@dataclass
+class BackwardsStep:  # geometry.rs:121-126
+    length: float
+    height_inlet: float
+    height_outlet: float
+    step_x: float
+
+    def _geo(self) -> _ffi.Geometry:
+        g = _ffi.Geometry(kind=0)
+        g.p[:4] = [self.length, self.height_inlet, self.height_outlet, self.step_x]
+        return g
+
+
+@dataclass
+class ChannelWithObstacle:  # geometry.rs:32-37
+    length: float
+    height: float
+    obstacle_center: tuple
+    obstacle_radius: float
+
+    def _geo(self) -> _ffi.Geometry:
+        g = _ffi.Geometry(kind=1)
+        g.p[:5] = [self.length, self.height, self.obstacle_center[0], self.obstacle_center[1],
+                   self.obstacle_radius]
+        return g
+
+
+@dataclass
+class RectangularChannel:  # geometry.rs:216-219
+    length: float
+    height: float
+
+    def _geo(self) -> _ffi.Geometry:
+        g = _ffi.Geometry(kind=2)
+        g.p[:2] = [self.length, self.height]
+        return g
+
+
+@dataclass
+class CircleObstacle:  # src/solver/mesh/tests.rs:4-10
+    center: tuple
+    radius: float
+    domain_min: tuple
+    domain_max: tuple
+
+    def _geo(self) -> _ffi.Geometry:
+        g = _ffi.Geometry(kind=3)
+        g.p[:7] = [self.center[0], self.center[1], self.radius, self.domain_min[0],
+                   self.domain_min[1], self.domain_max[0], self.domain_max[1]]
+        return g
+
+
+def _np(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).view(dtype)
+
+
+class Mesh:
+    """Owned native mesh (``cfd2::solver::mesh::Mesh``)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _ffi.lib().cfd_mesh_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def view(self) -> _ffi.MeshView:
+        v = _ffi.MeshView()
+        _ffi.check(_ffi.lib().cfd_mesh_get_view(self._h, C.byref(v)), "cfd_mesh_get_view")
+        return v
+
+    def num_cells(self) -> int:
+        return int(self.view().num_cells)
+
+    def num_faces(self) -> int:
+        return int(self.view().num_faces)
+
+    def arrays(self) -> dict:
+        v = self.view()
+        n, f = v.num_cells, v.num_faces
+        offs = _np(v.cell_face_offsets, n + 1, np.uint32)
+        s = int(offs[-1]) if n else 0
+        return dict(
+            face_owner=_np(v.face_owner, f, np.uint32),
+            face_neighbor=_np(v.face_neighbor, f, np.uint32),
+            face_boundary=_np(v.face_boundary, f, np.uint32),
+            face_area=_np(v.face_area, f, np.float64),
+            face_nx=_np(v.face_nx, f, np.float64),
+            face_ny=_np(v.face_ny, f, np.float64),
+            face_cx=_np(v.face_cx, f, np.float64),
+            face_cy=_np(v.face_cy, f, np.float64),
+            cell_cx=_np(v.cell_cx, n, np.float64),
+            cell_cy=_np(v.cell_cy, n, np.float64),
+            cell_vol=_np(v.cell_vol, n, np.float64),
+            cell_face_offsets=offs,
+            cell_faces=_np(v.cell_faces, s, np.uint32),
+        )
+
+    def vertices(self):
+        nv = C.c_uint32()
+        vx, vy = _ffi.f64p(), _ffi.f64p()
+        vf = C.POINTER(C.c_uint8)()
+        _ffi.check(_ffi.lib().cfd_mesh_get_vertices(self._h, C.byref(nv), C.byref(vx), C.byref(vy),
+                                                      C.byref(vf)), "cfd_mesh_get_vertices")
+        n = nv.value
+        return _np(vx, n, np.float64), _np(vy, n, np.float64), _np(vf, n, np.uint8).astype(bool)
+
+    def smooth(self, geo, target_skew: float, max_iterations: int) -> int:
+        it = C.c_int32()
+        g = geo._geo()
+        _ffi.check(_ffi.lib().cfd_mesh_smooth(self._h, C.byref(g), target_skew, max_iterations,
+                                              C.byref(it)), "cfd_mesh_smooth")
+        return it.value
+
+    def calculate_max_skewness(self) -> float:
+        return float(_ffi.lib().cfd_mesh_max_skewness(self._h))
+
+    def save(self, path: str) -> None:
+        _ffi.check(_ffi.lib().cfd_mesh_save(self._h, path.encode()), "cfd_mesh_save")
+
+    @staticmethod
+    def load(path: str) -> "Mesh":
+        h = C.c_void_p()
+        _ffi.check(_ffi.lib().cfd_mesh_load(path.encode(), C.byref(h)), "cfd_mesh_load")
+        return Mesh(h.value)
+
+
+def generate_cut_cell_mesh(geo, min_cell_size: float, max_cell_size: float, growth_rate: float,
+                           domain_size) -> Mesh:
+    """cut_cell.rs:10-16."""
+    h = C.c_void_p()
+    g = geo._geo()
+    _ffi.check(_ffi.lib().cfd_mesh_generate_cut_cell(C.byref(g), min_cell_size, max_cell_size,
+                                                     growth_rate, float(domain_size[0]),
+                                                     float(domain_size[1]), C.byref(h)),
+               "cfd_mesh_generate_cut_cell")
+    return Mesh(h.value)
+
+
+def channel_obstacle_h(target_cells: float) -> float:
+    """Cell size h for a ~target_cells channel+obstacle mesh (N ≈ 2.9686/h²)."""
+    return float(np.sqrt(2.9686 / target_cells))
+
+
+def bench_channel(h: float, smooth_iters: int = 100) -> Mesh:
+    """SURVEY §8(d) synthetic input: ChannelWithObstacle{3x1, (1.0,0.51), r 0.1},
+    cut-cell with min=max=h, growth 1.2, then smooth(0.3, 100)."""
+    geo = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.51),
+                              obstacle_radius=0.1)
+    m = generate_cut_cell_mesh(geo, h, h, 1.2, (3.0, 1.0))
+    if smooth_iters > 0:
+        m.smooth(geo, 0.3, smooth_iters)
+    return m

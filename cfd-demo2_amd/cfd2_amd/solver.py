@@ -1,0 +1,190 @@
+"""``GpuSolver`` — Python mirror of the reference's ``cfd2::solver::gpu::GpuSolver``
+(src/solver/gpu/structs.rs, solver.rs) over the C ABI.  Every method is one
+C call into libcfd2_amd.so; the HIP kernels run on the library's own stream.
+There is no CPU fallback: constructing a solver without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _ffi
+
+_vp = C.c_void_p
+_bound = False
+
+
+def _bind():
+    global _bound
+    if _bound:
+        return _ffi.lib()
+    L = _ffi.lib()
+    dp = C.POINTER(C.c_double)
+    L.cfd_config_default.argtypes = [C.POINTER(_ffi.Config)]
+    L.cfd_config_default.restype = None
+    L.cfd_solver_create.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
+                                    C.POINTER(_vp)]
+    L.cfd_solver_destroy.argtypes = [_vp]
+    L.cfd_solver_destroy.restype = None
+    for n in ("cfd_set_u", "cfd_set_p", "cfd_get_u", "cfd_get_p", "cfd_get_d_p"):
+        getattr(L, n).argtypes = [_vp, dp]
+    L.cfd_get_constants.argtypes = [_vp, C.POINTER(_ffi.Constants)]
+    L.cfd_set_constants.argtypes = [_vp, C.POINTER(_ffi.Constants)]
+    for n in ("cfd_set_dt", "cfd_set_viscosity", "cfd_set_alpha_p", "cfd_set_alpha_u",
+              "cfd_set_density", "cfd_set_inlet_velocity", "cfd_set_ramp_time"):
+        getattr(L, n).argtypes = [_vp, C.c_float]
+    for n in ("cfd_set_scheme", "cfd_set_time_scheme", "cfd_set_precond_type"):
+        getattr(L, n).argtypes = [_vp, C.c_uint32]
+    for n in ("cfd_update_constants", "cfd_initialize_history", "cfd_step"):
+        getattr(L, n).argtypes = [_vp]
+    L.cfd_get_step_info.argtypes = [_vp, C.POINTER(_ffi.StepInfo)]
+    L.cfd_num_cells.argtypes = [_vp]
+    L.cfd_num_cells.restype = C.c_uint32
+    L.cfd_num_faces.argtypes = [_vp]
+    L.cfd_num_faces.restype = C.c_uint32
+    L.cfd_profile_enable.argtypes = [_vp, C.c_int32]
+    L.cfd_profile_reset.argtypes = [_vp]
+    L.cfd_profile_smoother.argtypes = [_vp, dp, C.POINTER(C.c_uint64), dp]
+    L.cfd_amg_levels.argtypes = [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint64)]
+    L.cfd_step_algorithmic_bytes.argtypes = [_vp]
+    L.cfd_step_algorithmic_bytes.restype = C.c_double
+    L.cfd_debug_buffer_len.argtypes = [_vp, C.c_int32]
+    L.cfd_debug_buffer_len.restype = C.c_size_t
+    L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
+    L.cfd_debug_prepare_assemble.argtypes = [_vp, C.c_int32]
+    _bound = True
+    return L
+
+
+class GpuSolver:
+    """Drop-in for ``GpuSolver`` (init/mod.rs:15).  ``mesh`` is a cfd2_amd.Mesh."""
+
+    JACOBI = 0
+    AMG = 1
+
+    def __init__(self, mesh, config: _ffi.Config | None = None, device: int = 0, **cfg_overrides):
+        L = _bind()
+        self._mesh = mesh
+        cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
+        self._cfg = cfg
+        view = mesh.view()
+        h = _vp()
+        _ffi.check(L.cfd_solver_create(C.byref(view), C.byref(cfg), int(device), C.byref(h)),
+                   "cfd_solver_create")
+        self._h = h
+        self.num_cells = int(L.cfd_num_cells(h))
+        self.num_faces = int(L.cfd_num_faces(h))
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _ffi.lib().cfd_solver_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- constants (public `constants` field + setters, solver.rs:36-95) --------
+    @property
+    def constants(self) -> _ffi.Constants:
+        c = _ffi.Constants()
+        _ffi.check(_ffi.lib().cfd_get_constants(self._h, C.byref(c)), "cfd_get_constants")
+        return c
+
+    @constants.setter
+    def constants(self, c: _ffi.Constants) -> None:
+        _ffi.check(_ffi.lib().cfd_set_constants(self._h, C.byref(c)), "cfd_set_constants")
+
+    def _call(self, name, *args):
+        _ffi.check(getattr(_ffi.lib(), name)(self._h, *args), name)
+
+    def set_dt(self, dt): self._call("cfd_set_dt", float(dt))
+    def set_viscosity(self, v): self._call("cfd_set_viscosity", float(v))
+    def set_alpha_p(self, v): self._call("cfd_set_alpha_p", float(v))
+    def set_alpha_u(self, v): self._call("cfd_set_alpha_u", float(v))
+    def set_density(self, v): self._call("cfd_set_density", float(v))
+    def set_scheme(self, v): self._call("cfd_set_scheme", int(v))
+    def set_time_scheme(self, v): self._call("cfd_set_time_scheme", int(v))
+    def set_inlet_velocity(self, v): self._call("cfd_set_inlet_velocity", float(v))
+    def set_ramp_time(self, v): self._call("cfd_set_ramp_time", float(v))
+    def set_precond_type(self, v): self._call("cfd_set_precond_type", int(v))
+    def update_constants(self): self._call("cfd_update_constants")
+
+    # -- state ------------------------------------------------------------------
+    def set_u(self, u):
+        a = np.ascontiguousarray(np.asarray(u, dtype=np.float64).reshape(-1))
+        if a.size != 2 * self.num_cells:
+            raise ValueError("set_u expects num_cells (u, v) pairs")
+        self._call("cfd_set_u", a.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def set_p(self, p):
+        a = np.ascontiguousarray(np.asarray(p, dtype=np.float64).reshape(-1))
+        if a.size != self.num_cells:
+            raise ValueError("set_p expects num_cells values")
+        self._call("cfd_set_p", a.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def initialize_history(self): self._call("cfd_initialize_history")
+    def step(self): self._call("cfd_step")
+
+    def get_u(self) -> np.ndarray:
+        a = np.zeros(2 * self.num_cells)
+        self._call("cfd_get_u", a.ctypes.data_as(C.POINTER(C.c_double)))
+        return a.reshape(-1, 2)
+
+    def get_p(self) -> np.ndarray:
+        a = np.zeros(self.num_cells)
+        self._call("cfd_get_p", a.ctypes.data_as(C.POINTER(C.c_double)))
+        return a
+
+    def get_d_p(self) -> np.ndarray:
+        a = np.zeros(self.num_cells)
+        self._call("cfd_get_d_p", a.ctypes.data_as(C.POINTER(C.c_double)))
+        return a
+
+    # -- public status fields of the reference struct -------------------------
+    def step_info(self) -> _ffi.StepInfo:
+        i = _ffi.StepInfo()
+        self._call("cfd_get_step_info", C.byref(i))
+        return i
+
+    @property
+    def should_stop(self) -> bool: return bool(self.step_info().should_stop)
+    @property
+    def degenerate_count(self) -> int: return int(self.step_info().degenerate_count)
+    @property
+    def steady_state_count(self) -> int: return int(self.step_info().steady_state_count)
+    @property
+    def outer_iterations(self) -> int: return int(self.step_info().outer_iterations)
+
+    # -- instrumentation --------------------------------------------------------
+    def profile_enable(self, on=True): self._call("cfd_profile_enable", 1 if on else 0)
+    def profile_reset(self): self._call("cfd_profile_reset")
+
+    def profile_smoother(self):
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_double()
+        self._call("cfd_profile_smoother", C.byref(ms), C.byref(n), C.byref(b))
+        return ms.value, n.value, b.value
+
+    def amg_levels(self):
+        nl = C.c_int32()
+        rows = (C.c_uint32 * 20)()
+        nnz = (C.c_uint64 * 20)()
+        self._call("cfd_amg_levels", C.byref(nl), rows, nnz)
+        return [(int(rows[i]), int(nnz[i])) for i in range(nl.value)]
+
+    def step_algorithmic_bytes(self) -> float:
+        return float(_ffi.lib().cfd_step_algorithmic_bytes(self._h))
+
+    def debug_buffer(self, bid: int) -> np.ndarray:
+        n = _ffi.lib().cfd_debug_buffer_len(self._h, bid)
+        a = np.zeros(n, dtype=np.float32)
+        self._call("cfd_debug_buffer", int(bid), a.ctypes.data_as(C.POINTER(C.c_float)), n)
+        return a
+
+    def debug_prepare_assemble(self, assemble=True):
+        self._call("cfd_debug_prepare_assemble", 1 if assemble else 0)

@@ -1,0 +1,943 @@
+// gfx950 (MI355X / CDNA4) kernels of the coupled FV step.
+//
+// Every kernel is HBM-bandwidth bound (<= 0.25 flop/B): face sweeps, SpMV on
+// compressed 3x3 blocks, BLAS-1 with wavefront reductions, Jacobi smoothing,
+// restriction and prolongation.  No MFMA: nothing here is a dense contraction.
+// Arithmetic follows the reference WGSL operation-for-operation (file:line in
+// each kernel) and is compiled with -ffp-contract=off, so results are
+// bit-identical to the CPU oracle; reductions follow the canonical order of
+// kernels.hpp (256 threads x 4 cells per chunk, halving tree).
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace cfd2 {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float wdistance(float ax, float ay, float bx, float by) {
+  const float dx = ax - bx, dy = ay - by;
+  return sqrtf(dx * dx + dy * dy);
+}
+__device__ __forceinline__ float wsmoothstep(float lo, float hi, float x) {
+  const float t = fminf(fmaxf((x - lo) / (hi - lo), 0.0f), 1.0f);
+  return t * t * (3.0f - 2.0f * t);
+}
+__device__ __forceinline__ float wmix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+__device__ __forceinline__ float safe_inverse(float v) {
+  return fabsf(v) > 1e-14f ? 1.0f / v : 0.0f;
+}
+
+inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// Halving tree over 256 per-thread values (canonical order): levels 128 and 64
+// through LDS, levels 32..1 by wavefront shuffles in wave 0.  Result valid in
+// thread 0.  `lds` must hold 256 floats; caller syncs before reusing it.
+__device__ __forceinline__ float block_tree(float v, float* lds) {
+  const int t = threadIdx.x;
+  lds[t] = v;
+  __syncthreads();
+  if (t < 128) lds[t] = lds[t] + lds[t + 128];
+  __syncthreads();
+  float x = 0.0f;
+  if (t < 64) {
+    x = lds[t] + lds[t + 64];
+    x = x + __shfl_down(x, 32);
+    x = x + __shfl_down(x, 16);
+    x = x + __shfl_down(x, 8);
+    x = x + __shfl_down(x, 4);
+    x = x + __shfl_down(x, 2);
+    x = x + __shfl_down(x, 1);
+  }
+  return x;
+}
+
+// Canonical stage 2 over `np` partials by one 256-thread block.
+__device__ __forceinline__ float block_final(const float* partial, uint32_t np, float* lds) {
+  float acc = 0.0f;
+  for (uint32_t q = threadIdx.x; q < np; q += kBlock) acc += partial[q];
+  return block_tree(acc, lds);
+}
+
+// ---------------------------------------------------------------------------
+// prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
+// Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
+__global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t N = a.N;
+  if (i >= N) return;
+  const cfd_constants c = a.c;
+  const FaceSlots fs = a.fs;
+  const float vol = a.vol[i];
+  float diag_coeff = 0.0f;
+  float time_coeff = vol * c.density / c.dt;
+  if (c.time_scheme == 1u) {
+    const float r = c.dt / c.dt_old;
+    time_coeff = vol * c.density / c.dt * (1.0f + 2.0f * r) / (1.0f + r);
+  }
+  diag_coeff += time_coeff;
+  const float2 uc = a.st.u[i];
+  const float pc = a.st.p[i];
+  const float dpc = a.st.dp[i];
+  const float2 gpc = a.st.gp[i];
+  float gpx = 0.0f, gpy = 0.0f, gux = 0.0f, guy = 0.0f, gvx = 0.0f, gvy = 0.0f;
+  const uint32_t nf = fs.nface[i];
+  for (uint32_t k = 0; k < nf; ++k) {
+    const size_t e = (size_t)k * N + i;
+    const uint32_t meta = fs.meta[e];
+    const int32_t other = fs.other[e];
+    const uint32_t bt = meta & kMetaBtypeMask;
+    const bool own = (meta & kMetaOwner) != 0;
+    const float area = fs.area[e];
+    const float nx = fs.nx[e], ny = fs.ny[e];  // oriented out of this cell
+    // stored face normal, then prepare's geometric re-orientation (wgsl:122-130)
+    const float Nx = own ? nx : -nx, Ny = own ? ny : -ny;
+    const bool flip = (meta & kMetaFluxFlip) != 0;
+    const float nfx = flip ? -Nx : Nx, nfy = flip ? -Ny : Ny;
+    float flux = 0.0f;
+    float po_other = 0.0f;
+    float2 uo = make_float2(0.0f, 0.0f);
+    if (other >= 0) {
+      const float2 u_oth = a.st.u[other];
+      const float p_oth = a.st.p[other];
+      const float dp_oth = a.st.dp[other];
+      const float2 gp_oth = a.st.gp[other];
+      uo = u_oth;
+      po_other = p_oth;
+      const float2 uow = own ? uc : u_oth, ung = own ? u_oth : uc;
+      const float pow_ = own ? pc : p_oth, png = own ? p_oth : pc;
+      const float dpow = own ? dpc : dp_oth, dpng = own ? dp_oth : dpc;
+      const float2 gpow = own ? gpc : gp_oth, gpng = own ? gp_oth : gpc;
+      const float lambda = fs.lam_f[e];
+      const float ufx = lambda * uow.x + (1.0f - lambda) * ung.x;
+      const float ufy = lambda * uow.y + (1.0f - lambda) * ung.y;
+      const float dp_face = lambda * dpow + (1.0f - lambda) * dpng;
+      const float gfx = lambda * gpow.x + (1.0f - lambda) * gpng.x;
+      const float gfy = lambda * gpow.y + (1.0f - lambda) * gpng.y;
+      const float dist = fs.dist_a[e];
+      const float grad_p_n = gfx * nfx + gfy * nfy;
+      const float p_grad_f = (png - pow_) / dist;
+      const float rc_term = dp_face * area * (grad_p_n - p_grad_f);
+      const float u_n = ufx * nfx + ufy * nfy;
+      flux = c.density * (u_n * area + rc_term);
+    } else if (bt == 1u) {
+      const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+      const float ubx = c.inlet_velocity * ramp, uby = 0.0f;
+      flux = c.density * (ubx * nfx + uby * nfy) * area;
+    } else if (bt == 2u) {
+      const float u_n = uc.x * nfx + uc.y * nfy;  // boundary faces are owned by this cell
+      const float raw = c.density * u_n * area;
+      flux = fmaxf(0.0f, raw);
+    }
+    const float flux_out = own ? flux : -flux;
+    a.flux_s[e] = flux_out;
+    const float diff_coeff = c.viscosity * area / fs.dist_e[e];
+    const float conv_diag = flux_out > 0.0f ? flux_out : 0.0f;
+    if (other >= 0) {
+      diag_coeff += diff_coeff + conv_diag;
+    } else if (bt == 1u || bt == 3u) {
+      diag_coeff += diff_coeff;
+      if (flux_out > 0.0f) diag_coeff += flux_out;
+    } else if (bt == 2u) {
+      if (flux_out > 0.0f) diag_coeff += flux_out;
+    }
+    float vfp, vfu, vfv;
+    if (other >= 0) {
+      const float lp = fs.lam_s[e];
+      vfp = lp * pc + (1.0f - lp) * po_other;
+      if ((meta & kMetaDegen) == 0) {
+        vfu = lp * uc.x + (1.0f - lp) * uo.x;
+        vfv = lp * uc.y + (1.0f - lp) * uo.y;
+      } else {
+        vfu = 0.5f * (uc.x + uo.x);
+        vfv = 0.5f * (uc.y + uo.y);
+      }
+    } else {
+      vfp = (bt == 2u) ? 0.0f : pc;
+      if (bt == 1u) {
+        const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+        vfu = c.inlet_velocity * ramp;
+        vfv = 0.0f;
+      } else if (bt == 3u) {
+        vfu = 0.0f;
+        vfv = 0.0f;
+      } else {
+        vfu = uc.x;
+        vfv = uc.y;
+      }
+    }
+    gpx += vfp * nx * area;
+    gpy += vfp * ny * area;
+    gux += vfu * nx * area;
+    guy += vfu * ny * area;
+    gvx += vfv * nx * area;
+    gvy += vfv * ny * area;
+  }
+  a.dp_out[i] = (fabsf(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
+  a.gp_out[i] = make_float2(gpx / vol, gpy / vol);
+  a.grad_u[i] = make_float2(gux / vol, guy / vol);
+  a.grad_v[i] = make_float2(gvx / vol, gvy / vol);
+}
+
+// coupled_assembly_merged.wgsl:70-463
+__global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t N = a.N;
+  if (i >= N) return;
+  const cfd_constants c = a.c;
+  const FaceSlots fs = a.fs;
+  const float vol = a.vol[i];
+  float diag_uv = 0.0f;  // diag_u == diag_v (identical update sequence)
+  float sdup = 0.0f, sdvp = 0.0f, sdpu = 0.0f, sdpv = 0.0f, sdpp = 0.0f;
+  float rhs_u = 0.0f, rhs_v = 0.0f, rhs_p = 0.0f, sdiag = 0.0f;
+  const float2 un = a.u_old[i];
+  float coeff_time = vol * c.density / c.dt;
+  float rtu = coeff_time * un.x, rtv = coeff_time * un.y;
+  if (c.time_scheme == 1u) {
+    const float dt = c.dt, dt_old = c.dt_old;
+    const float r = dt / dt_old;
+    const float2 unm1 = a.u_old_old[i];
+    coeff_time = vol * c.density / dt * (1.0f + 2.0f * r) / (1.0f + r);
+    const float fn = (1.0f + r);
+    const float fnm1 = (r * r) / (1.0f + r);
+    rtu = (vol * c.density / dt) * (fn * un.x - fnm1 * unm1.x);
+    rtv = (vol * c.density / dt) * (fn * un.y - fnm1 * unm1.y);
+  }
+  diag_uv += coeff_time;
+  rhs_u += rtu;
+  rhs_v += rtv;
+  const float dpc = a.st.dp[i];
+  const float2 uc = a.st.u[i];
+  const uint32_t nf = fs.nface[i];
+  for (uint32_t k = 0; k < nf; ++k) {
+    const size_t e = (size_t)k * N + i;
+    const uint32_t meta = fs.meta[e];
+    const int32_t other = fs.other[e];
+    const uint32_t bt = meta & kMetaBtypeMask;
+    const float area = fs.area[e];
+    const float nx = fs.nx[e], ny = fs.ny[e];
+    const float flux = a.flux_s[e];
+    const float dist = fs.dist_a[e];
+    const float diff_coeff = c.viscosity * area / dist;
+    const float conv_diag = flux > 0.0f ? flux : 0.0f;
+    const float conv_off = flux > 0.0f ? 0.0f : flux;
+    if (other >= 0) {
+      const uint32_t rank = (meta >> kMetaRankShift) & 0xFFu;
+      const float dp_other = a.st.dp[other];
+      const float coeff = -diff_coeff + conv_off;
+      diag_uv += diff_coeff + conv_diag;
+      if (c.scheme != 0u) {
+        const float2 uo = a.st.u[other];
+        float pu_u = uc.x, pu_v = uc.y;
+        if (flux < 0.0f) {
+          pu_u = uo.x;
+          pu_v = uo.y;
+        }
+        float ph_u = pu_u, ph_v = pu_v;
+        if (c.scheme == 1u) {
+          if (flux > 0.0f) {
+            const float2 gu = a.grad_u[i], gv = a.grad_v[i];
+            const float rx = fs.rx[e], ry = fs.ry[e];
+            ph_u = uc.x + (gu.x * rx + gu.y * ry);
+            ph_v = uc.y + (gv.x * rx + gv.y * ry);
+          } else {
+            const float2 gu = a.grad_u[other], gv = a.grad_v[other];
+            const float rx = fs.rox[e], ry = fs.roy[e];
+            ph_u = uo.x + (gu.x * rx + gu.y * ry);
+            ph_v = uo.y + (gv.x * rx + gv.y * ry);
+          }
+        } else if (c.scheme == 2u) {
+          if (flux > 0.0f) {
+            const float2 gu = a.grad_u[i], gv = a.grad_v[i];
+            const float dx = fs.dvx[e], dy = fs.dvy[e];
+            const float gtu = gu.x * dx + gu.y * dy, gtv = gv.x * dx + gv.y * dy;
+            ph_u = 0.625f * uc.x + 0.375f * uo.x + 0.125f * gtu;
+            ph_v = 0.625f * uc.y + 0.375f * uo.y + 0.125f * gtv;
+          } else {
+            const float2 gu = a.grad_u[other], gv = a.grad_v[other];
+            const float dx = -fs.dvx[e], dy = -fs.dvy[e];  // center - other_center
+            const float gtu = gu.x * dx + gu.y * dy, gtv = gv.x * dx + gv.y * dy;
+            ph_u = 0.625f * uo.x + 0.375f * uc.x + 0.125f * gtu;
+            ph_v = 0.625f * uo.y + 0.375f * uc.y + 0.125f * gtv;
+          }
+        }
+        rhs_u -= flux * (ph_u - pu_u);
+        rhs_v -= flux * (ph_v - pu_v);
+      }
+      const float lambda = fs.lam_s[e];
+      const float oml = 1.0f - lambda;
+      const float pgx = area * nx, pgy = area * ny;
+      sdup += lambda * pgx;
+      sdvp += lambda * pgy;
+      const float dcx = nx * area, dcy = ny * area;
+      sdpu += lambda * dcx;
+      sdpv += lambda * dcy;
+      const float dp_f = lambda * dpc + (1.0f - lambda) * dp_other;
+      const float lapl = dp_f * area / dist;
+      sdpp += lapl;
+      const float scoeff = c.density * dp_f * area / dist;
+      sdiag += scoeff;
+      const size_t slot = (size_t)rank * N + i;
+      a.cval[slot] = make_float4(coeff, oml * pgx, oml * pgy, -lapl);
+      a.sval[slot] = -scoeff;
+    } else if (bt == 1u) {
+      const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+      const float ubx = c.inlet_velocity * ramp, uby = 0.0f;
+      diag_uv += diff_coeff;
+      rhs_u += diff_coeff * ubx;
+      rhs_v += diff_coeff * uby;
+      if (flux > 0.0f) {
+        diag_uv += flux;
+      } else {
+        rhs_u -= flux * ubx;
+        rhs_v -= flux * uby;
+      }
+      sdup += area * nx;
+      sdvp += area * ny;
+      const float flux_bc = (ubx * nx + uby * ny) * area;
+      rhs_p -= flux_bc;
+    } else if (bt == 3u) {
+      diag_uv += diff_coeff;
+      sdup += area * nx;
+      sdvp += area * ny;
+    } else if (bt == 2u) {
+      if (flux > 0.0f) diag_uv += flux;
+      sdpu += nx * area;
+      sdpv += ny * area;
+      const float lapl = dpc * area / dist;
+      sdpp += lapl;
+      const float scoeff = c.density * dpc * area / dist;
+      sdiag += scoeff;
+    }
+  }
+  const uint32_t dr = a.srank_diag[i];
+  const size_t dslot = (size_t)dr * N + i;
+  a.cval[dslot] = make_float4(diag_uv, sdup, sdvp, 0.0f + sdpp);
+  a.cdiag2[i] = make_float2(sdpu, sdpv);
+  a.sval[dslot] = sdiag;
+  a.rhs[3 * (size_t)i + 0] = rhs_u;
+  a.rhs[3 * (size_t)i + 1] = rhs_v;
+  a.rhs[3 * (size_t)i + 2] = rhs_p;
+  a.dinv_uv[i] = safe_inverse(diag_uv);
+  a.dinv_p[i] = safe_inverse(sdiag);
+}
+
+// update_fields_from_coupled.wgsl:45-98; per-wave max of the f32 bit patterns
+// then one atomicMax per wave (max is order-independent: deterministic).
+__global__ void __launch_bounds__(kBlock) k_update_fields(uint32_t N, float alpha_u, float alpha_p,
+                                                          const float* __restrict__ x, float2* u,
+                                                          float* p, uint32_t* maxbits) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t bu = 0, bp = 0;
+  if (i < N) {
+    const float un = x[3 * (size_t)i], vn = x[3 * (size_t)i + 1], pn = x[3 * (size_t)i + 2];
+    const float2 uo = u[i];
+    const float po = p[i];
+    const float ux = uo.x + alpha_u * (un - uo.x);
+    const float uy = uo.y + alpha_u * (vn - uo.y);
+    const float pu = po + alpha_p * (pn - po);
+    u[i] = make_float2(ux, uy);
+    p[i] = pu;
+    const float du = fmaxf(fabsf(ux - uo.x), fabsf(uy - uo.y));
+    const float dp = fabsf(pu - po);
+    bu = __float_as_uint(du);
+    bp = __float_as_uint(dp);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    bu = max(bu, (uint32_t)__shfl_xor((int)bu, o));
+    bp = max(bp, (uint32_t)__shfl_xor((int)bp, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&maxbits[0], bu);
+    atomicMax(&maxbits[1], bp);
+  }
+}
+
+// canonical chunk partial of dot(x, y) over 3-component cells
+__global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
+                                                        const float* __restrict__ y, uint32_t N,
+                                                        float* partial) {
+  __shared__ float lds[kBlock];
+  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < kRedCellsPerThread; ++q) {
+    const size_t c = base + (size_t)kBlock * q;
+    if (c < N) {
+      const float x0 = x[3 * c], x1 = x[3 * c + 1], x2 = x[3 * c + 2];
+      const float y0 = y[3 * c], y1 = y[3 * c + 1], y2 = y[3 * c + 2];
+      acc += x0 * y0;
+      acc += x1 * y1;
+      acc += x2 * y2;
+    }
+  }
+  const float s = block_tree(acc, lds);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(kBlock) k_reduce_final(const float* __restrict__ partial,
+                                                         uint32_t np, int mode, float* out,
+                                                         float* H, int hidx) {
+  __shared__ float lds[kBlock];
+  const float s = block_final(partial, np, lds);
+  if (threadIdx.x == 0) {
+    if (mode == 0) {
+      out[0] = s;
+    } else {
+      const float nrm = sqrtf(s);
+      out[0] = nrm;
+      if (mode == 2) out[1] = 1.0f / nrm;
+      if (mode == 3) {
+        H[hidx] = nrm;
+        out[1] = nrm > 1e-20f ? 1.0f / nrm : 0.0f;
+      }
+    }
+  }
+}
+
+// axpby (gmres_ops.wgsl:108-117) with alpha = 1, beta = -1: V0 = b - A x
+__global__ void __launch_bounds__(kBlock) k_residual_axpby(const float* __restrict__ b,
+                                                           const float* __restrict__ w,
+                                                           float* v0, size_t n) {
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e < n) v0[e] = 1.0f * b[e] + -1.0f * w[e];
+}
+
+// scale (gmres_ops.wgsl:120-129): y = alpha * x, alpha from device scalar
+__global__ void __launch_bounds__(kBlock) k_scale(const float* __restrict__ x, float* y,
+                                                  const float* alpha, size_t n) {
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e < n) y[e] = alpha[0] * x[e];
+}
+
+struct BlockCoeffs {
+  float uu, up, vp, pu, pv, pp;
+};
+__device__ __forceinline__ BlockCoeffs load_block(const CoupledMatrix& A, uint32_t r, uint32_t dr,
+                                                  size_t slot, float2 d2) {
+  const float4 b = A.cval[slot];
+  BlockCoeffs k;
+  k.uu = b.x;
+  k.up = b.y;
+  k.vp = b.z;
+  k.pp = b.w;
+  k.pu = (r == dr) ? d2.x : b.y;
+  k.pv = (r == dr) ? d2.y : b.z;
+  return k;
+}
+
+// spmv (gmres_ops.wgsl:63-81) on compressed blocks: one thread per cell, three
+// rows; per-row term order identical to the CSR row (neighbour-major, u,v,p).
+__global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
+                                                 float* __restrict__ y) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t N = A.N;
+  if (i >= N) return;
+  const uint32_t len = A.len[i], dr = A.drank[i];
+  const float2 d2 = A.cdiag2[i];
+  float su = 0.0f, sv = 0.0f, sp = 0.0f;
+  for (uint32_t r = 0; r < len; ++r) {
+    const size_t slot = (size_t)r * N + i;
+    const uint32_t j = A.col[slot];
+    const BlockCoeffs k = load_block(A, r, dr, slot, d2);
+    const float xu = x[3 * (size_t)j], xv = x[3 * (size_t)j + 1], xp = x[3 * (size_t)j + 2];
+    su += k.uu * xu;
+    su += 0.0f * xv;
+    su += k.up * xp;
+    sv += 0.0f * xu;
+    sv += k.uu * xv;
+    sv += k.vp * xp;
+    sp += k.pu * xu;
+    sp += k.pv * xv;
+    sp += k.pp * xp;
+  }
+  y[3 * (size_t)i] = su;
+  y[3 * (size_t)i + 1] = sv;
+  y[3 * (size_t)i + 2] = sp;
+}
+
+// calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j
+__global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
+                                                     const float* __restrict__ basis,
+                                                     size_t stride, int j, uint32_t N,
+                                                     float* partial, uint32_t np) {
+  __shared__ float lds[kBlock];
+  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
+  float wv[kRedCellsPerThread][3];
+  bool ok[kRedCellsPerThread];
+#pragma unroll
+  for (int q = 0; q < kRedCellsPerThread; ++q) {
+    const size_t c = base + (size_t)kBlock * q;
+    ok[q] = c < N;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) wv[q][s] = ok[q] ? w[3 * c + s] : 0.0f;
+  }
+  for (int ii = 0; ii <= j; ++ii) {
+    const float* v = basis + (size_t)ii * stride;
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kRedCellsPerThread; ++q) {
+      const size_t c = base + (size_t)kBlock * q;
+      if (ok[q]) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) acc += wv[q][s] * v[3 * c + s];
+      }
+    }
+    const float r = block_tree(acc, lds);
+    if (threadIdx.x == 0) partial[(size_t)ii * np + blockIdx.x] = r;
+    __syncthreads();
+  }
+}
+
+// reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
+__global__ void __launch_bounds__(kBlock) k_cgs_reduce(const float* __restrict__ partial,
+                                                       uint32_t np, int j, float* H, int m1) {
+  __shared__ float lds[kBlock];
+  const int ii = blockIdx.x;
+  const float s = block_final(partial + (size_t)ii * np, np, lds);
+  if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
+}
+
+// update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 chunk partial
+__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w,
+                                                            const float* __restrict__ basis,
+                                                            size_t stride, int j,
+                                                            const float* __restrict__ H, int m1,
+                                                            uint32_t N, float* partial) {
+  __shared__ float lds[kBlock];
+  __shared__ float hcol[64];
+  if (threadIdx.x <= (unsigned)j) hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
+  float corr[kRedCellsPerThread][3];
+#pragma unroll
+  for (int q = 0; q < kRedCellsPerThread; ++q)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) corr[q][s] = 0.0f;
+  for (int ii = 0; ii <= j; ++ii) {
+    const float h = hcol[ii];
+    const float* v = basis + (size_t)ii * stride;
+#pragma unroll
+    for (int q = 0; q < kRedCellsPerThread; ++q) {
+      const size_t c = base + (size_t)kBlock * q;
+      if (c < N) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) corr[q][s] += h * v[3 * c + s];
+      }
+    }
+  }
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < kRedCellsPerThread; ++q) {
+    const size_t c = base + (size_t)kBlock * q;
+    if (c < N) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const float wn = w[3 * c + s] - corr[q][s];
+        w[3 * c + s] = wn;
+        acc += wn * wn;
+      }
+    }
+  }
+  const float r = block_tree(acc, lds);
+  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
+// reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
+// (gmres_logic.wgsl:24-76).  scal[3] = ||w||, scal[4] = 1/||w||, scal[5] = |g[j+1]|.
+__global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict__ partial,
+                                                        uint32_t np, int j, float* H, int m1,
+                                                        float* givens, float* g, float* scal,
+                                                        float* resid_hist) {
+  __shared__ float lds[kBlock];
+  const float s = block_final(partial, np, lds);
+  if (threadIdx.x != 0) return;
+  const float norm = sqrtf(s);
+  H[(size_t)j * m1 + j + 1] = norm;
+  scal[3] = norm;
+  scal[4] = norm > 1e-20f ? 1.0f / norm : 0.0f;
+  float* Hc = H + (size_t)j * m1;
+  for (int ii = 0; ii < j; ++ii) {
+    const float hij = Hc[ii], hi1j = Hc[ii + 1];
+    const float cc = givens[2 * ii], ss = givens[2 * ii + 1];
+    Hc[ii] = cc * hij + ss * hi1j;
+    Hc[ii + 1] = -ss * hij + cc * hi1j;
+  }
+  const float hjj = Hc[j], hj1j = Hc[j + 1];
+  float cc = 1.0f, ss = 0.0f;
+  const float rho = sqrtf(hjj * hjj + hj1j * hj1j);
+  if (fabsf(rho) > 1e-20f) {
+    cc = hjj / rho;
+    ss = hj1j / rho;
+  }
+  givens[2 * j] = cc;
+  givens[2 * j + 1] = ss;
+  Hc[j] = rho;
+  Hc[j + 1] = 0.0f;
+  const float gj = g[j], gj1 = g[j + 1];
+  g[j] = cc * gj + ss * gj1;
+  g[j + 1] = -ss * gj + cc * gj1;
+  const float res = fabsf(g[j + 1]);
+  scal[5] = res;
+  resid_hist[j] = res;
+}
+
+// predict_and_form_schur (schur_precond.wgsl:142-188)
+__global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
+                                                            const float* __restrict__ r_in,
+                                                            const float* __restrict__ dinv_uv,
+                                                            const float* __restrict__ dinv_p,
+                                                            float* z, float* temp_p, float* p_sol,
+                                                            float* p_prev) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t N = A.N;
+  if (i >= N) return;
+  const float du = dinv_uv[i];
+  z[3 * (size_t)i] = du * r_in[3 * (size_t)i];
+  z[3 * (size_t)i + 1] = du * r_in[3 * (size_t)i + 1];
+  z[3 * (size_t)i + 2] = 0.0f;
+  float rhs_p = r_in[3 * (size_t)i + 2];
+  const uint32_t len = A.len[i], dr = A.drank[i];
+  const float2 d2 = A.cdiag2[i];
+  for (uint32_t r = 0; r < len; ++r) {
+    const size_t slot = (size_t)r * N + i;
+    const uint32_t j = A.col[slot];
+    const BlockCoeffs k = load_block(A, r, dr, slot, d2);
+    const float dj = dinv_uv[j];
+    const float zu = r_in[3 * (size_t)j] * dj;
+    const float zv = r_in[3 * (size_t)j + 1] * dj;
+    rhs_p -= k.pu * zu;
+    rhs_p -= k.pv * zv;
+    rhs_p -= k.pp * 0.0f;
+  }
+  temp_p[i] = rhs_p;
+  p_sol[i] = dinv_p[i] * rhs_p;
+  if (p_prev) p_prev[i] = 0.0f;
+}
+
+// relax_pressure (schur_precond.wgsl:52-90), omega = 1.2, live scalar matrix
+__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const uint32_t* __restrict__ col,
+                                                           const uint32_t* __restrict__ len,
+                                                           const float* __restrict__ sval,
+                                                           const float* __restrict__ dinv_p,
+                                                           const float* __restrict__ temp_p,
+                                                           const float* __restrict__ p_sol,
+                                                           float* p_prev) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= N) return;
+  float sigma = 0.0f;
+  const uint32_t l = len[i];
+  for (uint32_t r = 0; r < l; ++r) {
+    const size_t slot = (size_t)r * N + i;
+    const uint32_t cc = col[slot];
+    if (cc != i) sigma += sval[slot] * p_sol[cc];
+  }
+  const float hat_x = dinv_p[i] * (temp_p[i] - sigma);
+  p_prev[i] = wmix(p_prev[i], hat_x, 1.2f);
+}
+
+// correct_velocity (schur_precond.wgsl:93-139)
+__global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
+                                                            const float* __restrict__ p_sol,
+                                                            const float* __restrict__ dinv_uv,
+                                                            float* z) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t N = A.N;
+  if (i >= N) return;
+  const uint32_t len = A.len[i];
+  float cu = 0.0f, cv = 0.0f;
+  for (uint32_t r = 0; r < len; ++r) {
+    const size_t slot = (size_t)r * N + i;
+    const uint32_t j = A.col[slot];
+    const float4 b = A.cval[slot];
+    const float pj = p_sol[j];
+    cu += b.y * pj;
+    cv += b.z * pj;
+  }
+  const float du = dinv_uv[i];
+  z[3 * (size_t)i] = z[3 * (size_t)i] - du * cu;
+  z[3 * (size_t)i + 1] = z[3 * (size_t)i + 1] - du * cv;
+  z[3 * (size_t)i + 2] = p_sol[i];
+}
+
+// solve_triangular (gmres_logic.wgsl:78-104), single lane
+__global__ void k_solve_triangular(const float* H, const float* g, float* y, int k, int m1) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int li = 0; li < k; ++li) {
+    const int i = k - 1 - li;
+    float sum = g[i];
+    for (int jj = i + 1; jj < k; ++jj) sum -= H[(size_t)jj * m1 + i] * y[jj];
+    const float diag = H[(size_t)i * m1 + i];
+    y[i] = (fabsf(diag) > 1e-12f) ? sum / diag : 0.0f;
+  }
+}
+
+// basis_size x axpy_from_y (gmres_ops.wgsl:96-105) fused: x = y_i * z_i + x, i ascending
+__global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __restrict__ z,
+                                                     size_t stride, const float* __restrict__ y,
+                                                     int k, size_t n) {
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  float xv = x[e];
+  for (int ii = 0; ii < k; ++ii) xv = y[ii] * z[(size_t)ii * stride + e] + xv;
+  x[e] = xv;
+}
+
+// ------------------------------- AMG ---------------------------------------
+// smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
+__global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
+                                                       const float* __restrict__ b,
+                                                       float* __restrict__ x_out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n = L.n;
+  if (i >= n) return;
+  const uint32_t len = L.len[i];
+  float sigma = 0.0f;
+  for (uint32_t r = 0; r < len; ++r) {
+    const size_t slot = (size_t)r * n + i;
+    sigma += L.val[slot] * x[L.col[slot]];
+  }
+  const float x_new = (b[i] - sigma) / L.de[i];
+  x_out[i] = wmix(x[i], x_new, 0.8f);
+}
+
+// residual part of restrict_residual (amg.wgsl:80-111): r = b - A x (full row, column order)
+__global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ r) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t n = L.n;
+  if (i >= n) return;
+  const uint32_t len = L.len[i], dr = L.drank[i];
+  const float dv = L.dv[i];
+  const float xi = x[i];
+  float ax = 0.0f;
+  for (uint32_t k = 0; k < len; ++k) {
+    if (k == dr) ax += dv * xi;
+    const size_t slot = (size_t)k * n + i;
+    ax += L.val[slot] * x[L.col[slot]];
+  }
+  if (dr == len) ax += dv * xi;
+  r[i] = b[i] - ax;
+}
+
+// restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f]
+__global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
+                                                         float* __restrict__ cb) {
+  const uint32_t I = blockIdx.x * kBlock + threadIdx.x;
+  if (I >= L.nc) return;
+  float sum = 0.0f;
+  for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
+  cb[I] = sum;
+}
+
+// prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg])
+__global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* x,
+                                                        const float* __restrict__ xc) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= L.n) return;
+  float corr = 0.0f;
+  corr += 1.0f * xc[L.agg[i]];
+  x[i] += corr;
+}
+
+__global__ void __launch_bounds__(kBlock) k_fill(float* x, float v, size_t n) {
+  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e < n) x[e] = v;
+}
+
+// ---------------------- check_evolution statistics --------------------------
+// AoS view of the reference FluidState (coupled_solver.rs:504 reads the 32-byte
+// records as a flat f32 array): record r = {u.x, u.y, p, d_p, gp.x, gp.y, 0, 0}.
+__device__ __forceinline__ double block_tree_d(double v, double* lds) {
+  const int t = threadIdx.x;
+  lds[t] = v;
+  __syncthreads();
+  if (t < 128) lds[t] = lds[t] + lds[t + 128];
+  __syncthreads();
+  double x = 0.0;
+  if (t < 64) {
+    x = lds[t] + lds[t + 64];
+    x = x + __shfl_down(x, 32);
+    x = x + __shfl_down(x, 16);
+    x = x + __shfl_down(x, 8);
+    x = x + __shfl_down(x, 4);
+    x = x + __shfl_down(x, 2);
+    x = x + __shfl_down(x, 1);
+  }
+  __syncthreads();
+  return x;
+}
+
+__device__ __forceinline__ void view_pair(const StateView& v, uint32_t rec, int pair, float* a,
+                                          float* b) {
+  if (pair == 0) {
+    const float2 u = v.u[rec];
+    *a = u.x;
+    *b = u.y;
+  } else if (pair == 1) {
+    *a = v.p[rec];
+    *b = v.dp[rec];
+  } else if (pair == 2) {
+    const float2 gp = v.gp[rec];
+    *a = gp.x;
+    *b = gp.y;
+  } else {
+    *a = 0.0f;
+    *b = 0.0f;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, StateView prev,
+                                                              int have_prev, uint32_t N,
+                                                              double* partial) {
+  __shared__ double lds[kBlock];
+  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
+  double evo = 0.0, su = 0.0, sv = 0.0, squ = 0.0, sqv = 0.0;
+  for (int q = 0; q < kRedCellsPerThread; ++q) {
+    const size_t c = base + (size_t)kBlock * q;
+    if (c >= N) continue;
+    if (have_prev) {
+      for (int pr = 0; pr < 4; ++pr) {
+        float a0, b0, a1, b1;
+        view_pair(cur, (uint32_t)c, pr, &a0, &b0);
+        view_pair(prev, (uint32_t)c, pr, &a1, &b1);
+        const float da = a0 - a1, db = b0 - b1;
+        evo += (double)(da * da);
+        evo += (double)(db * db);
+      }
+    }
+    float a, b;
+    view_pair(cur, (uint32_t)(c >> 2), (int)(c & 3), &a, &b);
+    const double ad = (double)a, bd = (double)b;
+    su += ad;
+    sv += bd;
+    squ += ad * ad;
+    sqv += bd * bd;
+  }
+  const double r0 = block_tree_d(evo, lds);
+  const double r1 = block_tree_d(su, lds);
+  const double r2 = block_tree_d(sv, lds);
+  const double r3 = block_tree_d(squ, lds);
+  const double r4 = block_tree_d(sqv, lds);
+  if (threadIdx.x == 0) {
+    double* o = partial + 5 * (size_t)blockIdx.x;
+    o[0] = r0;
+    o[1] = r1;
+    o[2] = r2;
+    o[3] = r3;
+    o[4] = r4;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_evolution_final(const double* __restrict__ partial,
+                                                            uint32_t np, double* out5) {
+  __shared__ double lds[kBlock];
+  for (int f = 0; f < 5; ++f) {
+    double acc = 0.0;
+    for (uint32_t q = threadIdx.x; q < np; q += kBlock) acc += partial[5 * (size_t)q + f];
+    const double r = block_tree_d(acc, lds);
+    if (threadIdx.x == 0) out5[f] = r;
+  }
+}
+
+}  // namespace
+
+// ------------------------------- launchers ----------------------------------
+void launch_prepare(const PrepareArgs& a, hipStream_t s) {
+  if (a.N) hipLaunchKernelGGL(k_prepare, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
+}
+void launch_assemble(const AssembleArgs& a, hipStream_t s) {
+  if (a.N) hipLaunchKernelGGL(k_assemble, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
+}
+void launch_update_fields(uint32_t N, float au, float ap, const float* x, float2* u, float* p,
+                          uint32_t* maxbits, hipStream_t s) {
+  if (N) hipLaunchKernelGGL(k_update_fields, dim3(grid_for(N)), dim3(kBlock), 0, s, N, au, ap, x, u, p, maxbits);
+}
+void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s) {
+  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
+  if (nb) hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, x, y, N, partial);
+}
+void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* H, int hidx,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, partial, np, mode, out, H, hidx);
+}
+void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
+}
+void launch_scale(const float* x, float* y, const float* alpha, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(kBlock), 0, s, x, y, alpha, n);
+}
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
+  if (A.N) hipLaunchKernelGGL(k_spmv, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, x, y);
+}
+void launch_cgs_dots(const float* w, const float* basis, size_t stride, int j, uint32_t N,
+                     float* partial, uint32_t np, hipStream_t s) {
+  if (np) hipLaunchKernelGGL(k_cgs_dots, dim3(np), dim3(kBlock), 0, s, w, basis, stride, j, N, partial, np);
+}
+void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s) {
+  hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kBlock), 0, s, partial, np, j, H, m1);
+}
+void launch_cgs_update_norm(float* w, const float* basis, size_t stride, int j, const float* H, int m1,
+                            uint32_t N, float* partial, hipStream_t s) {
+  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
+  if (nb) hipLaunchKernelGGL(k_cgs_update_norm, dim3(nb), dim3(kBlock), 0, s, w, basis, stride, j, H, m1, N, partial);
+}
+void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
+                        float* g, float* scal, float* resid_hist, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kBlock), 0, s, partial, np, j, H, m1, givens, g, scal,
+                     resid_hist);
+}
+void launch_precond_predict(const CoupledMatrix& A, const float* r_in, const float* dinv_uv,
+                            const float* dinv_p, float* z, float* temp_p, float* p_sol, float* p_prev,
+                            hipStream_t s) {
+  if (A.N)
+    hipLaunchKernelGGL(k_precond_predict, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, r_in, dinv_uv,
+                       dinv_p, z, temp_p, p_sol, p_prev);
+}
+void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len, const float* sval,
+                           const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
+                           hipStream_t s) {
+  (void)ws;
+  if (N)
+    hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, col, len, sval, dinv_p,
+                       temp_p, p_sol, p_prev);
+}
+void launch_precond_correct(const CoupledMatrix& A, const float* p_sol, const float* dinv_uv, float* z,
+                            hipStream_t s) {
+  if (A.N) hipLaunchKernelGGL(k_precond_correct, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, p_sol, dinv_uv, z);
+}
+void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
+  hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(64), 0, s, H, g, y, k, m1);
+}
+void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
+                     hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for(n)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
+}
+void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s) {
+  if (L.n) hipLaunchKernelGGL(k_amg_smooth, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, b, x_out);
+}
+void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
+  if (L.n) hipLaunchKernelGGL(k_amg_residual, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, b, r);
+}
+void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, hipStream_t s) {
+  if (L.nc) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(L.nc)), dim3(kBlock), 0, s, L, r, cb);
+}
+void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
+  if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, xc);
+}
+void launch_fill(float* x, float v, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);
+}
+void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, double* partial,
+                              hipStream_t s) {
+  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
+  if (nb) hipLaunchKernelGGL(k_evolution_partial, dim3(nb), dim3(kBlock), 0, s, cur, prev, have_prev, N, partial);
+}
+void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s) {
+  hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kBlock), 0, s, partial, np, out5);
+}
+
+}  // namespace cfd2

@@ -1,0 +1,165 @@
+// Kernel argument blocks + launch wrappers for the gfx950 HIP kernels.
+//
+// Data layout in HBM:
+//  * per-cell arrays are SoA (float / float2) indexed by cell;
+//  * per-(cell, face-slot) static geometry and per-(cell, neighbour-slot)
+//    matrix blocks are ELL "slot-major": element (slot k, cell i) at k*N + i,
+//    so lane-i accesses of one slot are fully coalesced across a wavefront;
+//  * the coupled 3N x 3N matrix is stored as compressed 3x3 blocks: the
+//    reference CSR (init/linear_solver/mod.rs:180-216) always holds
+//    A_uu == A_vv, A_uv == A_vu == 0, A_up == A_pu, A_vp == A_pv per
+//    off-diagonal block (coupled_assembly_merged.wgsl:221-333), so one float4
+//    {c, gx, gy, pp} per block reproduces every CSR entry bit-for-bit.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "../../../include/cfd2_amd.h"
+
+namespace cfd2 {
+
+// meta bits of a face slot
+constexpr uint32_t kMetaBtypeMask = 0x3u;      // 0 internal, 1 inlet, 2 outlet, 3 wall
+constexpr uint32_t kMetaOwner = 1u << 2;       // face_owner == this cell
+constexpr uint32_t kMetaDegen = 1u << 3;       // d_c + d_o <= 1e-6 (lambda fallback 0.5)
+constexpr uint32_t kMetaFluxFlip = 1u << 4;    // normal_flux = -stored normal
+constexpr uint32_t kMetaRankShift = 8;         // scalar-row rank of the neighbour (0xFF boundary)
+
+// Canonical reduction contract (mirrors oracle/oracle.cpp): 256 threads x 4 cells
+constexpr int kRedThreads = 256;
+constexpr int kRedCellsPerThread = 4;
+constexpr int kRedChunkCells = kRedThreads * kRedCellsPerThread;
+
+struct FaceSlots {  // ELL [k*N + i], k < wf
+  const int32_t* other;
+  const uint32_t* meta;
+  const float* area;
+  const float* nx;  // normal oriented out of this cell
+  const float* ny;
+  const float* lam_s;   // lambda from this cell's side (d_o / (d_c + d_o))
+  const float* lam_f;   // lambda from the owner's side (flux interpolation)
+  const float* dist_a;  // max(|d . n|, 1e-6)
+  const float* dist_e;  // |other_center - center|
+  const float* dvx;     // other_center - center
+  const float* dvy;
+  const float* rx;      // f_center - center
+  const float* ry;
+  const float* rox;     // f_center - other_center
+  const float* roy;
+  const uint32_t* nface;  // [N]
+  int wf;
+};
+
+struct StateView {
+  float2* u;
+  float* p;
+  float* dp;
+  float2* gp;
+};
+
+struct PrepareArgs {
+  uint32_t N;
+  cfd_constants c;
+  FaceSlots fs;
+  const float* vol;
+  StateView st;       // read (snapshot)
+  float* dp_out;      // new d_p
+  float2* gp_out;     // new grad_p
+  float* flux_s;      // [k*N + i] oriented flux
+  float2* grad_u;
+  float2* grad_v;
+};
+
+struct AssembleArgs {
+  uint32_t N;
+  cfd_constants c;
+  FaceSlots fs;
+  const float* vol;
+  StateView st;            // current iterate (d_p already refreshed)
+  const float2* u_old;     // state_old.u
+  const float2* u_old_old; // state_old_old.u
+  const float* flux_s;
+  const float2* grad_u;
+  const float2* grad_v;
+  const uint32_t* srank_diag;  // [N] diagonal rank in the scalar row
+  float4* cval;   // [r*N + i] compressed coupled blocks
+  float2* cdiag2; // [N] {s_pu, s_pv}
+  float* sval;    // [r*N + i] scalar pressure matrix
+  float* rhs;     // [3N]
+  float* dinv_uv; // [N]
+  float* dinv_p;  // [N]
+};
+
+struct CoupledMatrix {
+  uint32_t N;
+  int ws;
+  const uint32_t* col;  // [r*N + i]
+  const uint32_t* len;  // [N]
+  const uint32_t* drank;  // [N]
+  const float4* cval;
+  const float2* cdiag2;
+};
+
+struct AmgLevelDev {
+  uint32_t n;
+  int w;              // ELL width (off-diagonals only)
+  const uint32_t* col;  // [r*n + i]
+  const float* val;
+  const uint32_t* len;   // off-diagonal count per row
+  const uint32_t* drank; // position of the diagonal among the row's entries
+  const float* dv;       // raw diagonal (0 if absent)
+  const float* de;       // effective smoother diagonal
+  // coarsening operators (only when has_op)
+  uint32_t nc;
+  const uint32_t* agg;     // [n] P: fine -> coarse
+  const uint32_t* r_row;   // [nc+1] R = P^T rows (fine indices ascending)
+  const uint32_t* r_col;
+};
+
+// ---------------- launch wrappers (kernels.hip) ----------------
+void launch_prepare(const PrepareArgs& a, hipStream_t s);
+void launch_assemble(const AssembleArgs& a, hipStream_t s);
+void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
+                          float* p, uint32_t* maxbits, hipStream_t s);
+void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s);
+// mode 0: out[0] = sum; 1: out[0] = sqrt(sum); 2: out[0] = sqrt, out[1] = 1/sqrt (host-style
+// 1.0f/norm); 3: w-norm: out[0]=sqrt, H[hidx]=sqrt, out[1] = norm>1e-20 ? 1/norm : 0
+void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* H,
+                         int hidx, hipStream_t s);
+void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
+void launch_scale(const float* x, float* y, const float* alpha, size_t n, hipStream_t s);
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
+void launch_cgs_dots(const float* w, const float* basis, size_t stride, int j, uint32_t N,
+                     float* partial, uint32_t np, hipStream_t s);
+void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s);
+void launch_cgs_update_norm(float* w, const float* basis, size_t stride, int j, const float* H,
+                            int m1, uint32_t N, float* partial, hipStream_t s);
+// ||w|| final + Givens update of column j; resid -> out_resid (device)
+void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
+                        float* g, float* scal, float* resid_hist, hipStream_t s);
+void launch_precond_predict(const CoupledMatrix& A, const float* r_in, const float* dinv_uv,
+                            const float* dinv_p, float* z, float* temp_p, float* p_sol,
+                            float* p_prev, hipStream_t s);
+void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len,
+                           const float* sval, const float* dinv_p, const float* temp_p,
+                           const float* p_sol, float* p_prev, hipStream_t s);
+void launch_precond_correct(const CoupledMatrix& A, const float* p_sol, const float* dinv_uv,
+                            float* z, hipStream_t s);
+void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,
+                             hipStream_t s);
+void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
+                     hipStream_t s);
+void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
+                       hipStream_t s);
+void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,
+                         hipStream_t s);
+void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, hipStream_t s);
+void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
+void launch_fill(float* x, float v, size_t n, hipStream_t s);
+// check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
+// partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
+void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N,
+                              double* partial, hipStream_t s);
+void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s);
+
+}  // namespace cfd2

@@ -1,0 +1,224 @@
+// C ABI of the solver (include/cfd2_amd.h).  Each entry replaces one method of
+// the reference's `impl GpuSolver` (src/solver/gpu/solver.rs, init/mod.rs);
+// exceptions become status codes (the reference panics).
+#include <cstring>
+#include <exception>
+#include <new>
+
+#include "error.hpp"
+#include "solver_impl.hpp"
+
+struct cfd_solver {
+  cfd2::Solver* s;
+};
+
+using cfd2::set_error;
+
+namespace {
+
+template <class F>
+cfd_status guard(F&& f) {
+  try {
+    f();
+    return CFD_OK;
+  } catch (const cfd2::HipError& e) {
+    return set_error(CFD_ERR_HIP, e.what());
+  } catch (const std::domain_error& e) {
+    return set_error(CFD_ERR_DIVERGED, e.what());
+  } catch (const std::invalid_argument& e) {
+    const std::string m = e.what();
+    return set_error(m.find("Diagonal not found") != std::string::npos ? CFD_ERR_DIAGONAL : CFD_ERR_INVALID, m);
+  } catch (const std::bad_alloc&) {
+    return set_error(CFD_ERR_HIP, "out of host memory");
+  } catch (const std::exception& e) {
+    return set_error(CFD_ERR_INTERNAL, e.what());
+  }
+}
+
+#define CHECK_S(h)                                       \
+  if (!(h) || !(h)->s) return set_error(CFD_ERR_INVALID, "null solver handle")
+
+template <class F>
+cfd_status set_const(cfd_solver* s, F&& f) {  // setters write + update_constants
+  CHECK_S(s);
+  f(s->s->constants);
+  return CFD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void cfd_config_default(cfd_config* c) {
+  if (!c) return;
+  c->n_outer_correctors = 20;
+  c->convergence_lag = 1;
+  c->fixed_outer = 0;
+  c->fixed_inner = 0;
+  c->max_restart = 50;
+  c->max_outer_restarts = 20;
+  c->fgmres_rtol = 1e-5f;
+  c->fgmres_atol = 1e-7f;
+  c->log_level = 0;
+  c->use_graphs = 0;
+}
+
+cfd_status cfd_solver_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
+                             cfd_solver** out) {
+  if (!mesh || !out) return set_error(CFD_ERR_INVALID, "null argument");
+  cfd_config c;
+  if (cfg)
+    c = *cfg;
+  else
+    cfd_config_default(&c);
+  cfd2::Solver* sp = nullptr;
+  const cfd_status st = guard([&] { sp = new cfd2::Solver(*mesh, c, hip_device); });
+  if (st != CFD_OK) return st;
+  *out = new cfd_solver{sp};
+  return CFD_OK;
+}
+
+void cfd_solver_destroy(cfd_solver* s) {
+  if (!s) return;
+  delete s->s;
+  delete s;
+}
+
+cfd_status cfd_set_u(cfd_solver* s, const double* uv) {
+  CHECK_S(s);
+  if (!uv) return set_error(CFD_ERR_INVALID, "null u");
+  return guard([&] { s->s->set_u(uv); });
+}
+cfd_status cfd_set_p(cfd_solver* s, const double* p) {
+  CHECK_S(s);
+  if (!p) return set_error(CFD_ERR_INVALID, "null p");
+  return guard([&] { s->s->set_p(p); });
+}
+cfd_status cfd_get_constants(const cfd_solver* s, cfd_constants* out) {
+  CHECK_S(s);
+  if (!out) return set_error(CFD_ERR_INVALID, "null out");
+  *out = s->s->constants;
+  return CFD_OK;
+}
+cfd_status cfd_set_constants(cfd_solver* s, const cfd_constants* c) {
+  CHECK_S(s);
+  if (!c) return set_error(CFD_ERR_INVALID, "null constants");
+  s->s->constants = *c;
+  return CFD_OK;
+}
+cfd_status cfd_set_dt(cfd_solver* s, float dt) {  // solver.rs:36-44
+  return set_const(s, [&](cfd_constants& c) {
+    c.dt_old = (c.dt > 0.0f) ? c.dt : dt;
+    c.dt = dt;
+  });
+}
+cfd_status cfd_set_viscosity(cfd_solver* s, float v) { return set_const(s, [&](cfd_constants& c) { c.viscosity = v; }); }
+cfd_status cfd_set_alpha_p(cfd_solver* s, float v) { return set_const(s, [&](cfd_constants& c) { c.alpha_p = v; }); }
+cfd_status cfd_set_alpha_u(cfd_solver* s, float v) { return set_const(s, [&](cfd_constants& c) { c.alpha_u = v; }); }
+cfd_status cfd_set_density(cfd_solver* s, float v) { return set_const(s, [&](cfd_constants& c) { c.density = v; }); }
+cfd_status cfd_set_scheme(cfd_solver* s, uint32_t v) { return set_const(s, [&](cfd_constants& c) { c.scheme = v; }); }
+cfd_status cfd_set_time_scheme(cfd_solver* s, uint32_t v) {
+  return set_const(s, [&](cfd_constants& c) { c.time_scheme = v; });
+}
+cfd_status cfd_set_inlet_velocity(cfd_solver* s, float v) {
+  return set_const(s, [&](cfd_constants& c) { c.inlet_velocity = v; });
+}
+cfd_status cfd_set_ramp_time(cfd_solver* s, float v) { return set_const(s, [&](cfd_constants& c) { c.ramp_time = v; }); }
+cfd_status cfd_set_precond_type(cfd_solver* s, uint32_t v) {
+  return set_const(s, [&](cfd_constants& c) { c.precond_type = v; });
+}
+// Kernels take the constants by value at launch, so the host copy *is* the
+// uploaded uniform: update_constants (solver.rs:91-95) has nothing left to do.
+cfd_status cfd_update_constants(cfd_solver* s) {
+  CHECK_S(s);
+  return CFD_OK;
+}
+cfd_status cfd_initialize_history(cfd_solver* s) {
+  CHECK_S(s);
+  return guard([&] { s->s->initialize_history(); });
+}
+cfd_status cfd_step(cfd_solver* s) {
+  CHECK_S(s);
+  return guard([&] { s->s->step(); });
+}
+cfd_status cfd_get_u(cfd_solver* s, double* uv) {
+  CHECK_S(s);
+  if (!uv) return set_error(CFD_ERR_INVALID, "null out");
+  return guard([&] { s->s->get_u(uv); });
+}
+cfd_status cfd_get_p(cfd_solver* s, double* p) {
+  CHECK_S(s);
+  if (!p) return set_error(CFD_ERR_INVALID, "null out");
+  return guard([&] { s->s->get_p(p); });
+}
+cfd_status cfd_get_d_p(cfd_solver* s, double* dp) {
+  CHECK_S(s);
+  if (!dp) return set_error(CFD_ERR_INVALID, "null out");
+  return guard([&] { s->s->get_d_p(dp); });
+}
+cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out) {
+  CHECK_S(s);
+  if (!out) return set_error(CFD_ERR_INVALID, "null out");
+  *out = s->s->info;
+  return CFD_OK;
+}
+uint32_t cfd_num_cells(const cfd_solver* s) { return (s && s->s) ? s->s->N : 0; }
+uint32_t cfd_num_faces(const cfd_solver* s) { return (s && s->s) ? s->s->F : 0; }
+
+cfd_status cfd_profile_enable(cfd_solver* s, int32_t enable) {
+  CHECK_S(s);
+  s->s->prof = enable != 0;
+  return CFD_OK;
+}
+cfd_status cfd_profile_reset(cfd_solver* s) {
+  CHECK_S(s);
+  return guard([&] {
+    CFD_HIP(hipStreamSynchronize(s->s->stream));
+    s->s->prof_used = 0;
+    s->s->prof_ms = 0.0;
+    s->s->prof_launches = 0;
+  });
+}
+cfd_status cfd_profile_smoother(const cfd_solver* cs, double* total_ms, uint64_t* launches,
+                                double* bytes_per_launch) {
+  CHECK_S(cs);
+  cfd2::Solver* s = cs->s;
+  return guard([&] {
+    CFD_HIP(hipStreamSynchronize(s->stream));
+    for (size_t k = 0; k + 1 < s->prof_used; k += 2) {
+      float ms = 0.0f;
+      CFD_HIP(hipEventElapsedTime(&ms, s->prof_ev[k], s->prof_ev[k + 1]));
+      s->prof_ms += ms;
+    }
+    s->prof_used = 0;
+    if (total_ms) *total_ms = s->prof_ms;
+    if (launches) *launches = s->prof_launches;
+    if (bytes_per_launch) *bytes_per_launch = s->smoother_bytes();
+  });
+}
+cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* rows, uint64_t* nnz) {
+  CHECK_S(s);
+  const auto& L = s->s->levels;
+  if (num_levels) *num_levels = (int32_t)L.size();
+  for (size_t i = 0; i < L.size() && i < 20; ++i) {
+    if (rows) rows[i] = L[i].dev.n;
+    if (nnz) nnz[i] = L[i].nnz;
+  }
+  return CFD_OK;
+}
+double cfd_step_algorithmic_bytes(const cfd_solver* s) {
+  return (s && s->s) ? s->s->algorithmic_step_bytes() : 0.0;
+}
+size_t cfd_debug_buffer_len(const cfd_solver* s, int32_t id) { return (s && s->s) ? s->s->debug_len(id) : 0; }
+cfd_status cfd_debug_buffer(cfd_solver* s, int32_t id, float* out, size_t count) {
+  CHECK_S(s);
+  const size_t len = s->s->debug_len(id);
+  if (!out || len == 0 || count < len) return set_error(CFD_ERR_INVALID, "bad debug buffer request");
+  return guard([&] { s->s->debug_buffer(id, out); });
+}
+cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble) {
+  CHECK_S(s);
+  return guard([&] { s->s->debug_prepare_assemble(assemble != 0); });
+}
+
+}  // extern "C"

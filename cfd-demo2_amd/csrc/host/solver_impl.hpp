@@ -1,0 +1,217 @@
+// Host-side driver state of the HIP solver (one instance per GPU handle).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/cfd2_amd.h"
+#include "../hip/kernels.hpp"
+
+namespace cfd2 {
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define CFD_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw ::cfd2::HipError(std::string(#expr) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+// Device allocation arena: every buffer is freed with the solver.
+class DeviceArena {
+ public:
+  ~DeviceArena() { release(); }
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    const size_t bytes = (n ? n : 1) * sizeof(T);
+    CFD_HIP(hipMalloc(&p, bytes));
+    ptrs_.push_back(p);
+    bytes_ += bytes;
+    return static_cast<T*>(p);
+  }
+  template <class T>
+  T* upload(const std::vector<T>& v, hipStream_t s) {
+    T* p = alloc<T>(v.size());
+    if (!v.empty()) CFD_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return p;
+  }
+  void release() {
+    for (void* p : ptrs_) (void)hipFree(p);
+    ptrs_.clear();
+    bytes_ = 0;
+  }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  std::vector<void*> ptrs_;
+  size_t bytes_ = 0;
+};
+
+struct HostCsr {
+  std::vector<uint32_t> row, col;
+  std::vector<float> val;
+  size_t rows = 0, cols = 0;
+};
+
+// Mesh-derived static topology/geometry (init/mesh.rs + the per-slot geometric
+// factors every face sweep needs), computed once on the host in f32 with the
+// exact operation order of the WGSL expressions they replace.
+struct Topology {
+  uint32_t N = 0, F = 0;
+  int wf = 0;  // max faces per cell
+  int ws = 0;  // max scalar row length (incl. diagonal)
+  std::vector<float> vol;
+  std::vector<uint32_t> nface;
+  // face slots, [k*N + i]
+  std::vector<int32_t> fs_other;
+  std::vector<uint32_t> fs_meta;
+  std::vector<uint32_t> fs_face;  // host only: face index of each slot
+  std::vector<float> fs_area, fs_nx, fs_ny, fs_lam_s, fs_lam_f, fs_dist_a, fs_dist_e, fs_dvx,
+      fs_dvy, fs_rx, fs_ry, fs_rox, fs_roy;
+  // scalar CSR (init/mesh.rs:27-53) and its ELL image [r*N + i]
+  std::vector<uint32_t> srow, scol;
+  std::vector<uint32_t> ell_col, ell_len, ell_drank;
+};
+
+// Throws std::invalid_argument on inconsistent meshes.
+void build_topology(const cfd_mesh_view& m, Topology& t);
+
+// AMG hierarchy (linear_solver/amg.rs:84-235, 374-595) built on the host.
+struct AmgHostLevel {
+  HostCsr A;
+  std::vector<uint32_t> agg;         // P (fine -> coarse), when has_op
+  std::vector<uint32_t> r_row, r_col;  // R = P^T
+  uint32_t nc = 0;
+  bool has_op = false;
+};
+std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels);
+
+struct AmgGpuLevel {
+  AmgLevelDev dev{};
+  float* x = nullptr;   // level solution (level 0: external p_sol)
+  float* xt = nullptr;  // ping-pong partner for the out-of-place smoother
+  float* b = nullptr;   // level rhs (level 0: external temp_p)
+  float* r = nullptr;   // residual scratch
+  uint64_t nnz = 0;     // including diagonal
+};
+
+struct LagReader {  // async_buffer.rs restated as a deterministic lag model
+  bool has_last = false;
+  float last = 0.0f;
+  int pending = -1;
+};
+
+struct Solver {
+  cfd_config cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DeviceArena arena;
+  Topology topo;
+  uint32_t N = 0, F = 0;
+  int m = 50, m1 = 51;
+  uint32_t nchunks = 0;
+
+  // static device data
+  FaceSlots fs{};
+  float* d_vol = nullptr;
+  uint32_t* d_scol = nullptr;
+  uint32_t* d_slen = nullptr;
+  uint32_t* d_sdrank = nullptr;
+  // ring of 3 FluidState slots (SoA) + prepare's d_p / grad_p scratch
+  StateView ring[3]{};
+  float* dp_scratch = nullptr;
+  float2* gp_scratch = nullptr;
+  int step_index = 0, i_state = 0, i_old = 1, i_old_old = 2;
+  // prev view for check_evolution
+  StateView prev{};
+  bool have_prev = false;
+  // face-slot fluxes, gradients, matrices
+  float* flux_s = nullptr;
+  float2* grad_u = nullptr;
+  float2* grad_v = nullptr;
+  float4* cval = nullptr;
+  float2* cdiag2 = nullptr;
+  float* sval = nullptr;
+  float* rhs = nullptr;
+  float* x = nullptr;
+  float* dinv_uv = nullptr;
+  float* dinv_p = nullptr;
+  // FGMRES
+  bool fgmres_ready = false;
+  float* basis = nullptr;
+  size_t stride = 0;
+  float* zvec = nullptr;
+  float* w = nullptr;
+  float* temp = nullptr;
+  float* temp_p = nullptr;
+  float* p_sol = nullptr;
+  float* partial = nullptr;      // [(m+1) * nchunks]
+  float* partial_n = nullptr;    // [nchunks]
+  double* partial_d = nullptr;   // [5 * nchunks] check_evolution
+  float* dsc = nullptr;          // device scalars
+  float* H = nullptr;
+  float* givens = nullptr;
+  float* g = nullptr;
+  float* y = nullptr;
+  float* resid_hist = nullptr;
+  uint32_t* maxbits = nullptr;
+  float* h_pin = nullptr;        // pinned host scalars
+  std::vector<hipEvent_t> ev_iter;
+  hipEvent_t ev_outer[2]{};
+  LagReader inner;
+  // AMG
+  bool amg_built = false;
+  std::vector<AmgGpuLevel> levels;
+  // host-side state
+  cfd_constants constants{};
+  cfd_step_info info{};
+  std::vector<std::pair<double, double>> variance_history;
+  // profiling of the level-0 smoother
+  bool prof = false;
+  std::vector<hipEvent_t> prof_ev;
+  size_t prof_used = 0;
+  double prof_ms = 0.0;
+  uint64_t prof_launches = 0;
+
+  Solver(const cfd_mesh_view& mesh, const cfd_config& cfg, int device);
+  ~Solver();
+  StateView& S() { return ring[i_state]; }
+
+  void set_u(const double* uv);
+  void set_p(const double* p);
+  void initialize_history();
+  void step();
+  void get_u(double* uv);
+  void get_p(double* p);
+  void get_d_p(double* dp);
+  void debug_prepare_assemble(bool assemble);
+  size_t debug_len(int id) const;
+  void debug_buffer(int id, float* out);
+  double algorithmic_step_bytes() const;
+  double smoother_bytes() const;
+
+ private:
+  void rotate();
+  void prepare();
+  void assemble();
+  cfd_linear_stats solve();
+  void ensure_fgmres();
+  void ensure_amg();
+  void precondition(const float* v, float* z);
+  void v_cycle();
+  void amg_smooth(size_t li, float*& x, const float* b);
+  float norm_blocking(const float* v, int mode, int slot);
+  float residual_into_v0_blocking();
+  void check_evolution();
+  void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
+  CoupledMatrix cmat() const;
+};
+
+}  // namespace cfd2

@@ -1,0 +1,189 @@
+// Mesh -> device-ready static topology and per-face-slot geometric factors.
+//
+// Restates init/mesh.rs:24-212 (f64 -> f32 upload, scalar CSR, face -> matrix
+// slot, diagonal indices) and hoists every purely geometric sub-expression of
+// prepare_coupled.wgsl / coupled_assembly_merged.wgsl out of the per-step
+// kernels.  Each factor is computed in f32 with the same operations, in the
+// same order, as the WGSL expression it replaces (compiled -ffp-contract=off),
+// so the kernels reading it produce identical bits.
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+#include "solver_impl.hpp"
+
+namespace cfd2 {
+
+namespace {
+inline float wdistance(float ax, float ay, float bx, float by) {
+  const float dx = ax - bx, dy = ay - by;
+  return std::sqrt(dx * dx + dy * dy);
+}
+}  // namespace
+
+void build_topology(const cfd_mesh_view& m, Topology& t) {
+  const uint32_t N = m.num_cells, F = m.num_faces;
+  if (N == 0) throw std::invalid_argument("mesh has no cells");
+  t.N = N;
+  t.F = F;
+  const uint32_t NONE = 0xFFFFFFFFu;
+
+  // f32 geometry (init/mesh.rs:93-155)
+  std::vector<float> cx(N), cy(N);
+  t.vol.resize(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    cx[i] = (float)m.cell_cx[i];
+    cy[i] = (float)m.cell_cy[i];
+    t.vol[i] = (float)m.cell_vol[i];
+  }
+
+  // scalar CSR (init/mesh.rs:27-53): neighbours + diagonal, sorted, deduplicated
+  std::vector<uint32_t> deg(N + 1, 1);
+  for (uint32_t f = 0; f < F; ++f) {
+    const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
+    if (o >= N) throw std::invalid_argument("face_owner out of range");
+    if (n != NONE) {
+      if (n >= N) throw std::invalid_argument("face_neighbor out of range");
+      deg[o]++;
+      deg[n]++;
+    }
+  }
+  std::vector<uint32_t> aoff(N + 1, 0);
+  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] = aoff[i] + deg[i];
+  std::vector<uint32_t> adj(aoff[N]);
+  {
+    std::vector<uint32_t> pos(aoff.begin(), aoff.end() - 1);
+    for (uint32_t i = 0; i < N; ++i) adj[pos[i]++] = i;
+    for (uint32_t f = 0; f < F; ++f) {
+      const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
+      if (n != NONE) {
+        adj[pos[o]++] = n;
+        adj[pos[n]++] = o;
+      }
+    }
+  }
+  t.srow.assign(N + 1, 0);
+  t.scol.clear();
+  t.scol.reserve(aoff[N]);
+  int ws = 0;
+  for (uint32_t i = 0; i < N; ++i) {
+    auto b = adj.begin() + aoff[i], e = adj.begin() + aoff[i + 1];
+    std::sort(b, e);
+    e = std::unique(b, e);
+    t.srow[i] = (uint32_t)t.scol.size();
+    t.scol.insert(t.scol.end(), b, e);
+    ws = std::max(ws, (int)(e - b));
+  }
+  t.srow[N] = (uint32_t)t.scol.size();
+  t.ws = ws;
+  if (ws > 255) throw std::invalid_argument("cell with more than 255 neighbours");
+
+  // scalar-row ELL image + diagonal rank (init/mesh.rs:201-212)
+  t.ell_col.assign((size_t)ws * N, 0);
+  t.ell_len.resize(N);
+  t.ell_drank.resize(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    const uint32_t a = t.srow[i], b = t.srow[i + 1];
+    t.ell_len[i] = b - a;
+    bool found = false;
+    for (uint32_t k = a; k < b; ++k) {
+      const uint32_t r = k - a;
+      t.ell_col[(size_t)r * N + i] = t.scol[k];
+      if (t.scol[k] == i) {
+        t.ell_drank[i] = r;
+        found = true;
+      }
+    }
+    if (!found) throw std::invalid_argument("Diagonal not found in CSR cols");
+  }
+  // pad unused ELL slots with the row's own index (never read)
+  for (uint32_t i = 0; i < N; ++i)
+    for (uint32_t r = t.ell_len[i]; r < (uint32_t)ws; ++r) t.ell_col[(size_t)r * N + i] = i;
+
+  // face slots
+  int wf = 0;
+  t.nface.resize(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    const uint32_t nfc = m.cell_face_offsets[i + 1] - m.cell_face_offsets[i];
+    t.nface[i] = nfc;
+    wf = std::max(wf, (int)nfc);
+  }
+  t.wf = wf;
+  const size_t S = (size_t)wf * N;
+  t.fs_other.assign(S, -1);
+  t.fs_meta.assign(S, 0);
+  t.fs_face.assign(S, NONE);
+  for (auto* v : {&t.fs_area, &t.fs_nx, &t.fs_ny, &t.fs_lam_s, &t.fs_lam_f, &t.fs_dist_a,
+                  &t.fs_dist_e, &t.fs_dvx, &t.fs_dvy, &t.fs_rx, &t.fs_ry, &t.fs_rox, &t.fs_roy})
+    v->assign(S, 0.0f);
+  for (uint32_t i = 0; i < N; ++i) {
+    const float ci_x = cx[i], ci_y = cy[i];
+    for (uint32_t k = 0; k < t.nface[i]; ++k) {
+      const uint32_t f = m.cell_faces[m.cell_face_offsets[i] + k];
+      if (f >= F) throw std::invalid_argument("cell_faces out of range");
+      const uint32_t o = m.face_owner[f], nb = m.face_neighbor[f];
+      const bool own = (o == i);
+      const bool internal = (nb != NONE);
+      if (!internal && !own) throw std::invalid_argument("boundary face listed by a non-owner cell");
+      if (internal && !own && nb != i)
+        throw std::invalid_argument("cell lists a face it does not own or neighbour");
+      const uint32_t bt = internal ? 0u : (m.face_boundary[f] & 3u);
+      const float Nx = (float)m.face_nx[f], Ny = (float)m.face_ny[f];
+      const float area = (float)m.face_area[f];
+      const float fcx = (float)m.face_cx[f], fcy = (float)m.face_cy[f];
+      const float nx = own ? Nx : -Nx, ny = own ? Ny : -Ny;
+      // prepare_coupled.wgsl:124-130 geometric flip of the flux normal
+      const float cox = cx[o], coy = cy[o];
+      const float dxv = fcx - cox, dyv = fcy - coy;
+      const bool flip = (dxv * Nx + dyv * Ny < 0.0f);
+      const uint32_t other = internal ? (own ? nb : o) : NONE;
+      const float ocx = internal ? cx[other] : fcx, ocy = internal ? cy[other] : fcy;
+      const float dvx = ocx - ci_x, dvy = ocy - ci_y;
+      const float dist_e = std::sqrt(dvx * dvx + dvy * dvy);            // prepare :224-226
+      const float dist_a = std::fmax(std::fabs(dvx * nx + dvy * ny), 1e-6f);  // assembly :176-179
+      uint32_t meta = bt | (own ? kMetaOwner : 0u) | (flip ? kMetaFluxFlip : 0u);
+      float lam_s = 0.5f, lam_f = 0.5f;
+      uint32_t rank = 0xFFu;
+      if (internal) {
+        const float d_c = wdistance(ci_x, ci_y, fcx, fcy);
+        const float d_o = wdistance(ocx, ocy, fcx, fcy);
+        const float tot = d_c + d_o;
+        if (tot > 1e-6f)
+          lam_s = d_o / tot;
+        else
+          meta |= kMetaDegen;
+        const float cnx = cx[nb], cny = cy[nb];
+        const float d_own = wdistance(cox, coy, fcx, fcy);
+        const float d_ngh = wdistance(cnx, cny, fcx, fcy);
+        const float total = d_own + d_ngh;
+        if (total > 1e-6f) lam_f = d_ngh / total;
+        // cell_face_matrix_indices (init/mesh.rs:157-193) as a row rank
+        const uint32_t* b = t.scol.data() + t.srow[i];
+        const uint32_t* e = t.scol.data() + t.srow[i + 1];
+        const uint32_t* it = std::lower_bound(b, e, other);
+        if (it == e || *it != other) throw std::invalid_argument("neighbour missing from CSR row");
+        rank = (uint32_t)(it - b);
+      }
+      meta |= rank << kMetaRankShift;
+      const size_t e = (size_t)k * N + i;
+      t.fs_other[e] = internal ? (int32_t)other : -1;
+      t.fs_meta[e] = meta;
+      t.fs_face[e] = f;
+      t.fs_area[e] = area;
+      t.fs_nx[e] = nx;
+      t.fs_ny[e] = ny;
+      t.fs_lam_s[e] = lam_s;
+      t.fs_lam_f[e] = lam_f;
+      t.fs_dist_a[e] = dist_a;
+      t.fs_dist_e[e] = dist_e;
+      t.fs_dvx[e] = dvx;
+      t.fs_dvy[e] = dvy;
+      t.fs_rx[e] = fcx - ci_x;
+      t.fs_ry[e] = fcy - ci_y;
+      t.fs_rox[e] = fcx - ocx;
+      t.fs_roy[e] = fcy - ocy;
+    }
+  }
+}
+
+}  // namespace cfd2

@@ -1,0 +1,209 @@
+/*
+ * cfd2_amd.h — C ABI of the MI355X-native coupled incompressible-flow step.
+ *
+ * Drop-in boundary for the reference crate `cfd2` (TSultanov/cfd-demo2).
+ * Every solver entry point replaces one method of the reference's
+ * `impl GpuSolver` (Rust, src/solver/gpu/solver.rs / init/mod.rs); the Rust
+ * extern "C" shim that binds them is in INTEGRATION.md.  Plain pointers and
+ * sizes only; no torch types.  Calls are blocking and single-threaded per
+ * handle, as in the reference (GpuSolver holds RefCells; GUI wraps it in a
+ * Mutex).  Errors are returned as cfd_status (the reference panics instead);
+ * cfd_last_error() gives a thread-local message.
+ */
+#ifndef CFD2_AMD_H
+#define CFD2_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum cfd_status {
+  CFD_OK = 0,
+  CFD_ERR_INVALID = 1,    /* bad argument / inconsistent mesh                    */
+  CFD_ERR_HIP = 2,        /* HIP runtime failure (no device, OOM, launch error)  */
+  CFD_ERR_DIVERGED = 3,   /* NaN residual: coupled_solver.rs:344-346, 421-426    */
+  CFD_ERR_DIAGONAL = 4,   /* "Diagonal not found in CSR cols": init/mesh.rs:210   */
+  CFD_ERR_RCCL = 5,       /* collective failure (distributed solver)            */
+  CFD_ERR_INTERNAL = 6
+} cfd_status;
+
+const char* cfd_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* Mesh (input format).  Mirrors `Mesh` SoA, src/solver/mesh/structs.rs:12-42.
+ * face_neighbor == UINT32_MAX marks a boundary face (Option<usize>::None,
+ * init/mesh.rs:63-70); face_boundary: 0 none, 1 inlet, 2 outlet, 3 wall
+ * (init/mesh.rs:76-84).  Geometry is f64 and is rounded to f32 on upload
+ * exactly like init/mesh.rs:93-155.                                          */
+typedef struct cfd_mesh_view {
+  uint32_t num_cells;
+  uint32_t num_faces;
+  const uint32_t* face_owner;        /* [num_faces]     */
+  const uint32_t* face_neighbor;     /* [num_faces]     */
+  const uint32_t* face_boundary;     /* [num_faces]     */
+  const double* face_area;           /* [num_faces]     */
+  const double* face_nx;             /* [num_faces]     */
+  const double* face_ny;             /* [num_faces]     */
+  const double* face_cx;             /* [num_faces]     */
+  const double* face_cy;             /* [num_faces]     */
+  const double* cell_cx;             /* [num_cells]     */
+  const double* cell_cy;             /* [num_cells]     */
+  const double* cell_vol;            /* [num_cells]     */
+  const uint32_t* cell_face_offsets; /* [num_cells + 1] */
+  const uint32_t* cell_faces;        /* [cell_face_offsets[num_cells]] */
+} cfd_mesh_view;
+
+/* Geometry of the reference mesher (src/solver/mesh/geometry.rs).           */
+typedef struct cfd_geometry {
+  int32_t kind;  /* 0 BackwardsStep{length,h_in,h_out,step_x}
+                    1 ChannelWithObstacle{length,height,cx,cy,r}
+                    2 RectangularChannel{length,height}
+                    3 CircleObstacle{cx,cy,r,xmin,ymin,xmax,ymax} (mesh/tests.rs) */
+  double p[8];
+} cfd_geometry;
+
+typedef struct cfd_mesh cfd_mesh; /* owned host mesh */
+
+/* generate_cut_cell_mesh (src/solver/mesh/cut_cell.rs:10-16)               */
+cfd_status cfd_mesh_generate_cut_cell(const cfd_geometry* geo, double min_cell_size,
+                                      double max_cell_size, double growth_rate,
+                                      double domain_x, double domain_y, cfd_mesh** out);
+/* Mesh::smooth (structs.rs:159-292); returns iterations done in *iters.     */
+cfd_status cfd_mesh_smooth(cfd_mesh* m, const cfd_geometry* geo, double target_skew,
+                           int32_t max_iterations, int32_t* iters);
+/* Mesh::calculate_max_skewness (structs.rs:294-320)                         */
+double cfd_mesh_max_skewness(const cfd_mesh* m);
+/* Borrowed view of the mesh arrays (valid until the mesh is modified/freed). */
+cfd_status cfd_mesh_get_view(const cfd_mesh* m, cfd_mesh_view* out);
+/* Vertex arrays (vx, vy, v_fixed) for mesh-validity tests.                  */
+cfd_status cfd_mesh_get_vertices(const cfd_mesh* m, uint32_t* num_vertices, const double** vx,
+                                 const double** vy, const uint8_t** v_fixed);
+/* Binary SoA dump / load.                              */
+cfd_status cfd_mesh_save(const cfd_mesh* m, const char* path);
+cfd_status cfd_mesh_load(const char* path, cfd_mesh** out);
+void cfd_mesh_destroy(cfd_mesh* m);
+
+/* ------------------------------------------------------------------------ */
+/* Constants: same 14-field layout as GpuConstants (structs.rs:86-101).      */
+typedef struct cfd_constants {
+  float dt;
+  float dt_old;
+  float time;
+  float viscosity;
+  float density;
+  uint32_t component;
+  float alpha_p;
+  uint32_t scheme;      /* 0 Upwind, 1 SOU, 2 QUICK (scheme.rs)  */
+  float alpha_u;
+  uint32_t stride_x;
+  uint32_t time_scheme; /* 0 Euler, 1 BDF2                       */
+  float inlet_velocity;
+  float ramp_time;
+  uint32_t precond_type; /* 0 Jacobi, 1 AMG (PreconditionerType) */
+} cfd_constants;
+
+/* Build-side configuration (hard-coded numerics of the reference). */
+typedef struct cfd_config {
+  int32_t n_outer_correctors; /* 20 (init/mod.rs:144)                                  */
+  int32_t convergence_lag;    /* 1 = reference async-read model (default), 0 = exact  */
+  int32_t fixed_outer;        /* >0: exactly this many Picard iterations, no early exit */
+  int32_t fixed_inner;        /* >0: exactly this many FGMRES iterations per solve     */
+  int32_t max_restart;        /* 50  (coupled_solver_fgmres.rs:1737)                   */
+  int32_t max_outer_restarts; /* 20  (coupled_solver_fgmres.rs:1738)                   */
+  float fgmres_rtol;          /* 1e-5                                                   */
+  float fgmres_atol;          /* 1e-7                                                   */
+  int32_t log_level;          /* 0 silent, 1 reference println! lines to stderr        */
+  int32_t use_graphs;         /* capture the fixed-schedule inner solve in a hipGraph   */
+} cfd_config;
+
+void cfd_config_default(cfd_config* cfg);
+
+typedef struct cfd_linear_stats { /* LinearSolverStats, structs.rs:11-18 */
+  uint32_t iterations;
+  float residual;
+  int32_t converged;
+  int32_t diverged;
+  double time_s;
+} cfd_linear_stats;
+
+typedef struct cfd_step_info {
+  int32_t should_stop;
+  uint32_t degenerate_count;
+  uint32_t steady_state_count;
+  float outer_residual_u;
+  float outer_residual_p;
+  uint32_t outer_iterations;
+  cfd_linear_stats stats_p; /* the only stats field the reference writes */
+  uint32_t total_linear_iterations; /* summed over the step's outer iterations */
+} cfd_step_info;
+
+typedef struct cfd_solver cfd_solver;
+
+/* GpuSolver::new (init/mod.rs:15-19).  hip_device selects the GPU.           */
+cfd_status cfd_solver_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
+                             cfd_solver** out);
+void cfd_solver_destroy(cfd_solver* s);
+
+/* solver.rs:9-34: each call overwrites the WHOLE state (other fields = 0).   */
+cfd_status cfd_set_u(cfd_solver* s, const double* uv /* [2N] interleaved */);
+cfd_status cfd_set_p(cfd_solver* s, const double* p /* [N] */);
+/* `constants` public field: host copy; takes effect at update_constants/step */
+cfd_status cfd_get_constants(const cfd_solver* s, cfd_constants* out);
+cfd_status cfd_set_constants(cfd_solver* s, const cfd_constants* c);
+/* setters, solver.rs:36-95 (set_dt keeps the dt_old rule)                    */
+cfd_status cfd_set_dt(cfd_solver* s, float dt);
+cfd_status cfd_set_viscosity(cfd_solver* s, float nu);
+cfd_status cfd_set_alpha_p(cfd_solver* s, float a);
+cfd_status cfd_set_alpha_u(cfd_solver* s, float a);
+cfd_status cfd_set_density(cfd_solver* s, float rho);
+cfd_status cfd_set_scheme(cfd_solver* s, uint32_t scheme);
+cfd_status cfd_set_time_scheme(cfd_solver* s, uint32_t scheme);
+cfd_status cfd_set_inlet_velocity(cfd_solver* s, float v);
+cfd_status cfd_set_ramp_time(cfd_solver* s, float t);
+cfd_status cfd_set_precond_type(cfd_solver* s, uint32_t precond_type);
+cfd_status cfd_update_constants(cfd_solver* s);
+/* solver.rs:276-294                                                          */
+cfd_status cfd_initialize_history(cfd_solver* s);
+/* solver.rs:242 -> coupled_solver.rs:33-499                                  */
+cfd_status cfd_step(cfd_solver* s);
+/* solver.rs:97-128 (blocking)                                               */
+cfd_status cfd_get_u(cfd_solver* s, double* uv /* [2N] */);
+cfd_status cfd_get_p(cfd_solver* s, double* p /* [N] */);
+cfd_status cfd_get_d_p(cfd_solver* s, double* dp /* [N] */);
+cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out);
+uint32_t cfd_num_cells(const cfd_solver* s);
+uint32_t cfd_num_faces(const cfd_solver* s);
+
+/* ------------------------------------------------------------------------ */
+/* Instrumentation (replaces profiling.rs): HIP-event timing of the level-0
+ * AMG smoother sweep, on the solver's own stream.                            */
+cfd_status cfd_profile_enable(cfd_solver* s, int32_t enable);
+cfd_status cfd_profile_reset(cfd_solver* s);
+/* total_ms / launches for the level-0 smoother; bytes = algorithmic bytes per
+ * sweep (4(n+1) + 8 nnz + 12 n).                              */
+cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t* launches,
+                                double* bytes_per_launch);
+/* AMG hierarchy summary: number of levels and rows/nnz per level.            */
+cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* rows /*[20]*/,
+                          uint64_t* nnz /*[20]*/);
+/* Algorithmic bytes of one step under the fixed schedule.    */
+double cfd_step_algorithmic_bytes(const cfd_solver* s);
+
+/* Debug/parity access to internal device buffers, copied to host.
+ * ids: 0 fluxes-by-face[F], 1 grad_u[2N], 2 grad_v[2N], 3 rhs[3N], 4 x[3N],
+ * 5 diag_u_inv[N], 6 diag_v_inv[N], 7 diag_p_inv[N], 8 scalar_matrix[nnz_s],
+ * 9 coupled_matrix_csr[9 nnz_s] (reference CSR order), 10 grad_p[2N],
+ * 11 state_old u[2N], 12 state_old_old u[2N]                                 */
+cfd_status cfd_debug_buffer(cfd_solver* s, int32_t id, float* out, size_t count);
+size_t cfd_debug_buffer_len(const cfd_solver* s, int32_t id);
+/* Runs only prepare_coupled (+ coupled_assembly_merged when assemble != 0) on
+ * the current state without rotating the ring (kernel-level parity).        */
+cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFD2_AMD_H */

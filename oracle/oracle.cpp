@@ -1,0 +1,1540 @@
+// CPU oracle — TEST INFRASTRUCTURE ONLY (see oracle.h).  PARITY UNPINNED.
+//
+// Literal f32 restatement of the reference hot path (TSultanov/cfd-demo2):
+//   prepare_coupled.wgsl:63-348          -> prepare()
+//   coupled_assembly_merged.wgsl:70-463  -> assemble()
+//   update_fields_from_coupled.wgsl:45-98-> update_fields()
+//   schur_precond.wgsl:52-188            -> precond_*()
+//   amg.wgsl:24-120 + linear_solver/amg.rs:84-235,374-595,666-770 -> Amg
+//   gmres_ops/gmres_cgs/gmres_logic.wgsl -> fgmres pieces
+//   coupled_solver.rs:33-580, coupled_solver_fgmres.rs:1728-2448 -> step()/solve()
+//   init/mesh.rs:24-212, init/linear_solver/mod.rs:72-216, init/fields.rs:62-188,
+//   solver.rs:9-44,276-294 -> setup / API
+// Deterministic choices: snapshot reads in prepare (§0.1-3),
+// out-of-place Jacobi in the AMG smoother (§0.1-4), lag-0/1 model of the async
+// residual reads (§0.1-5), frozen AMG hierarchy (§0.1-6), restrict rows beyond
+// the coarse size skipped (§0.1-7).  Reductions use the CANONICAL ORDER below
+// (the reference's order is an artefact of its 64-wide workgroups + serial sums;
+// any fixed order is a valid restatement).  Build with -ffp-contract=off.
+#include "oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <string>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string& m) {
+  g_err = m;
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
+// Canonical reduction order (shared contract with the HIP kernels):
+//   vectors of 3 floats per cell; chunk = 1024 cells; 256 "threads" per chunk,
+//   thread t serially sums cells c = 1024*k + t + 256*q (q = 0..3, c < N),
+//   components s = 0..2 in order; then a halving tree (128,64,...,1) over the
+//   256 thread sums.  Stage 2: thread t sums partials t, t+256, ... serially,
+//   then the same halving tree.
+constexpr int kThreads = 256;
+constexpr int kCellsPerThread = 4;
+constexpr int kChunkCells = kThreads * kCellsPerThread;
+
+inline float tree256(float* s) {
+  for (int h = kThreads / 2; h >= 1; h >>= 1)
+    for (int t = 0; t < h; ++t) s[t] = s[t] + s[t + h];
+  return s[0];
+}
+
+inline size_t num_chunks(size_t ncells) { return (ncells + kChunkCells - 1) / kChunkCells; }
+
+template <class F>  // F(cell, comp) -> float term
+float canon_partial(size_t chunk, size_t ncells, F term) {
+  float s[kThreads];
+  for (int t = 0; t < kThreads; ++t) {
+    float acc = 0.0f;
+    for (int q = 0; q < kCellsPerThread; ++q) {
+      const size_t c = chunk * kChunkCells + t + (size_t)kThreads * q;
+      if (c < ncells)
+        for (int comp = 0; comp < 3; ++comp) acc += term(c, comp);
+    }
+    s[t] = acc;
+  }
+  return tree256(s);
+}
+
+inline float canon_final(const float* partials, size_t np) {
+  float s[kThreads];
+  for (int t = 0; t < kThreads; ++t) {
+    float acc = 0.0f;
+    for (size_t q = t; q < np; q += kThreads) acc += partials[q];
+    s[t] = acc;
+  }
+  return tree256(s);
+}
+
+float canon_dot(const float* x, const float* y, size_t ncells) {
+  const size_t nc = num_chunks(ncells);
+  std::vector<float> part(nc);
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < (long)nc; ++k)
+    part[k] = canon_partial(k, ncells, [&](size_t c, int s) { return x[3 * c + s] * y[3 * c + s]; });
+  return canon_final(part.data(), nc);
+}
+
+// WGSL builtins (WGSL spec formulas).
+inline float wdistance(float ax, float ay, float bx, float by) {
+  const float dx = ax - bx, dy = ay - by;
+  return std::sqrt(dx * dx + dy * dy);
+}
+inline float wclamp(float e, float lo, float hi) { return std::fmin(std::fmax(e, lo), hi); }
+inline float wsmoothstep(float lo, float hi, float x) {
+  const float t = wclamp((x - lo) / (hi - lo), 0.0f, 1.0f);
+  return t * t * (3.0f - 2.0f * t);
+}
+inline float wmix(float a, float b, float t) { return a * (1.0f - t) + b * t; }
+inline float safe_inverse(float v) { return std::fabs(v) > 1e-14f ? 1.0f / v : 0.0f; }
+
+struct FluidState {
+  float ux, uy, p, d_p, gpx, gpy, gcx, gcy;
+};
+static_assert(sizeof(FluidState) == 32, "FluidState must be 32 bytes");
+
+struct Csr {
+  std::vector<uint32_t> row, col;
+  std::vector<float> val;
+  size_t rows = 0, cols = 0;
+};
+
+// --------------------------- AMG (linear_solver/amg.rs) ---------------------------
+struct AmgLevel {
+  Csr A, P, R;
+  bool has_op = false;
+  std::vector<float> x, b, tmp;
+  size_t n = 0;
+};
+
+void aggregate(const Csr& m, std::vector<size_t>& agg, size_t& nagg) {  // amg.rs:84-116
+  const size_t n = m.rows, NONE = std::numeric_limits<size_t>::max();
+  agg.assign(n, NONE);
+  nagg = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (agg[i] != NONE) continue;
+    agg[i] = nagg;
+    for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
+      const size_t j = m.col[k];
+      if (j != i && agg[j] == NONE) agg[j] = nagg;
+    }
+    ++nagg;
+  }
+}
+
+Csr build_prolongation(const std::vector<size_t>& agg, size_t nagg, size_t nf) {  // :118-139
+  Csr p;
+  p.rows = nf;
+  p.cols = nagg;
+  p.row.assign(nf + 1, 0);
+  uint32_t count = 0;
+  for (size_t i = 0; i < nf; ++i) {
+    p.row[i] = count;
+    if (agg[i] < nagg) {
+      p.col.push_back((uint32_t)agg[i]);
+      p.val.push_back(1.0f);
+      ++count;
+    }
+  }
+  p.row[nf] = count;
+  return p;
+}
+
+Csr transpose(const Csr& m) {  // :141-185
+  Csr t;
+  t.rows = m.cols;
+  t.cols = m.rows;
+  std::vector<std::vector<std::pair<uint32_t, float>>> rows(m.cols);
+  for (size_t i = 0; i < m.rows; ++i)
+    for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) rows[m.col[k]].push_back({(uint32_t)i, m.val[k]});
+  t.row.assign(m.cols + 1, 0);
+  uint32_t off = 0;
+  for (size_t i = 0; i < m.cols; ++i) {
+    t.row[i] = off;
+    for (auto& e : rows[i]) {
+      t.col.push_back(e.first);
+      t.val.push_back(e.second);
+      ++off;
+    }
+  }
+  t.row[m.cols] = off;
+  return t;
+}
+
+Csr mat_mat_mult(const Csr& a, const Csr& b) {  // :187-229, f32 accumulation in visit order
+  Csr c;
+  c.rows = a.rows;
+  c.cols = b.cols;
+  c.row.assign(a.rows + 1, 0);
+  std::vector<float> acc(b.cols, 0.0f);
+  std::vector<uint8_t> seen(b.cols, 0);
+  std::vector<uint32_t> touched;
+  uint32_t off = 0;
+  for (size_t i = 0; i < a.rows; ++i) {
+    c.row[i] = off;
+    touched.clear();
+    for (uint32_t ka = a.row[i]; ka < a.row[i + 1]; ++ka) {
+      const uint32_t j = a.col[ka];
+      const float va = a.val[ka];
+      for (uint32_t kb = b.row[j]; kb < b.row[j + 1]; ++kb) {
+        const uint32_t k = b.col[kb];
+        if (!seen[k]) {
+          seen[k] = 1;
+          acc[k] = 0.0f;
+          touched.push_back(k);
+        }
+        acc[k] += va * b.val[kb];
+      }
+    }
+    std::sort(touched.begin(), touched.end());
+    for (uint32_t k : touched) {
+      c.col.push_back(k);
+      c.val.push_back(acc[k]);
+      seen[k] = 0;
+      ++off;
+    }
+  }
+  c.row[a.rows] = off;
+  return c;
+}
+
+struct Amg {
+  std::vector<AmgLevel> levels;
+
+  void build(const Csr& fine, size_t max_levels) {  // amg.rs:246-595
+    Csr cur = fine;
+    for (size_t li = 0; li < max_levels; ++li) {
+      AmgLevel L;
+      L.n = cur.rows;
+      L.A = cur;
+      L.x.assign(L.n, 0.0f);
+      L.b.assign(L.n, 0.0f);
+      L.tmp.assign(L.n, 0.0f);
+      bool coarsened = false;
+      if (li < max_levels - 1 && L.n > 100) {
+        std::vector<size_t> agg;
+        size_t nagg;
+        aggregate(cur, agg, nagg);
+        if (nagg < L.n) {
+          L.P = build_prolongation(agg, nagg, L.n);
+          L.R = transpose(L.P);
+          cur = mat_mat_mult(mat_mat_mult(L.R, cur), L.P);
+          L.has_op = true;
+          coarsened = true;
+        }
+      }
+      levels.push_back(std::move(L));
+      if (!coarsened) break;
+    }
+  }
+
+  // smooth_op (amg.wgsl:24-50), restated out-of-place: x <- mix(x, (b - sigma)/diag, 0.8)
+  static void smooth(AmgLevel& L, float* x, const float* b) {
+    const float omega = 0.8f;
+    const Csr& A = L.A;
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)L.n; ++i) {
+      float sigma = 0.0f, diag = 1.0f;
+      for (uint32_t k = A.row[i]; k < A.row[i + 1]; ++k) {
+        const uint32_t col = A.col[k];
+        const float v = A.val[k];
+        if (col == (uint32_t)i)
+          diag = v;
+        else
+          sigma += v * x[col];
+      }
+      if (std::fabs(diag) < 1e-14f) diag = 1.0f;
+      const float x_new = (b[i] - sigma) / diag;
+      L.tmp[i] = wmix(x[i], x_new, omega);
+    }
+    std::memcpy(x, L.tmp.data(), L.n * sizeof(float));
+  }
+
+  // restrict_residual (amg.wgsl:80-111) for coarse rows < n_coarse (§0.1-7: skip the rest)
+  static void restrict_residual(const AmgLevel& F, const float* x, const float* b, float* coarse_b) {
+    const Csr &R = F.R, &A = F.A;
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)R.rows; ++i) {
+      float sum = 0.0f;
+      for (uint32_t k = R.row[i]; k < R.row[i + 1]; ++k) {
+        const uint32_t f = R.col[k];
+        float ax = 0.0f;
+        for (uint32_t j = A.row[f]; j < A.row[f + 1]; ++j) ax += A.val[j] * x[A.col[j]];
+        const float fine_r = b[f] - ax;
+        sum += R.val[k] * fine_r;
+      }
+      coarse_b[i] = sum;
+    }
+  }
+
+  // prolongate_op (amg.wgsl:56-75)
+  static void prolongate(const AmgLevel& F, float* x, const float* coarse_x) {
+    const Csr& P = F.P;
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)F.n; ++i) {
+      float corr = 0.0f;
+      for (uint32_t k = P.row[i]; k < P.row[i + 1]; ++k) corr += P.val[k] * coarse_x[P.col[k]];
+      x[i] += corr;
+    }
+  }
+
+  // amg.rs:666-770 with level 0 bound to (x = p_sol, b = temp_p)
+  void v_cycle(float* x0, const float* b0) {
+    const size_t L = levels.size();
+    auto X = [&](size_t i) { return i == 0 ? x0 : levels[i].x.data(); };
+    auto B = [&](size_t i) { return i == 0 ? b0 : levels[i].b.data(); };
+    for (size_t i = 0; i + 1 < L; ++i) {
+      smooth(levels[i], X(i), B(i));
+      if (levels[i].has_op) restrict_residual(levels[i], X(i), B(i), levels[i + 1].b.data());
+      std::fill(levels[i + 1].x.begin(), levels[i + 1].x.end(), 0.0f);
+    }
+    for (int s = 0; s < 10; ++s) smooth(levels[L - 1], X(L - 1), B(L - 1));
+    for (size_t ii = L - 1; ii-- > 0;) {
+      if (levels[ii].has_op) prolongate(levels[ii], X(ii), levels[ii + 1].x.data());
+      smooth(levels[ii], X(ii), B(ii));
+    }
+  }
+};
+
+}  // namespace
+
+// ===========================================================================
+struct oracle_solver {
+  // config
+  cfd_config cfg;
+  // mesh (f32 upload, init/mesh.rs)
+  uint32_t N = 0, F = 0;
+  std::vector<uint32_t> face_owner, face_boundary, cell_face_offsets, cell_faces;
+  std::vector<int32_t> face_neighbor;
+  std::vector<float> face_areas, face_nx, face_ny, face_cx, face_cy, cell_cx, cell_cy, cell_vols;
+  std::vector<uint32_t> cfmi, diag_idx;  // cell_face_matrix_indices, diagonal_indices
+  Csr scalar;                             // structure + live values (scalar pressure matrix)
+  std::vector<uint32_t> c_row, c_col;     // coupled CSR structure (3N rows)
+  std::vector<float> c_val;               // coupled matrix values
+  // fields
+  std::vector<FluidState> bufs[3];
+  int step_index = 0;
+  int i_state = 0, i_old = 1, i_old_old = 2;
+  std::vector<float> fluxes, grad_u, grad_v;  // grads as float2 interleaved
+  std::vector<float> rhs, x, diag_u_inv, diag_v_inv, diag_p_inv;
+  cfd_constants constants;
+  // FGMRES resources (coupled_solver_fgmres.rs:212-1280)
+  bool fgmres_init = false;
+  int m = 50;
+  std::vector<float> basis, zvec, w, temp, temp_p, p_sol, H, givens, g, y;
+  bool inner_has_last = false;
+  float inner_last = 0.0f;
+  std::unique_ptr<Amg> amg;
+  // outer-loop / step info
+  cfd_step_info info{};
+  std::vector<float> prev_u_cpu;
+  bool have_prev = false;
+  std::vector<std::pair<double, double>> variance_history;
+
+  FluidState* S() { return bufs[i_state].data(); }
+  FluidState* SO() { return bufs[i_old].data(); }
+  FluidState* SOO() { return bufs[i_old_old].data(); }
+};
+
+namespace {
+
+bool build(oracle_solver* s, const cfd_mesh_view* mv) {
+  const uint32_t N = mv->num_cells, F = mv->num_faces;
+  s->N = N;
+  s->F = F;
+  // scalar CSR (init/mesh.rs:27-53 == init/linear_solver/mod.rs:72-100)
+  std::vector<std::vector<uint32_t>> adj(N);
+  for (uint32_t f = 0; f < F; ++f) {
+    const uint32_t o = mv->face_owner[f], n = mv->face_neighbor[f];
+    if (o >= N) return fail("face_owner out of range"), false;
+    if (n != 0xFFFFFFFFu) {
+      if (n >= N) return fail("face_neighbor out of range"), false;
+      adj[o].push_back(n);
+      adj[n].push_back(o);
+    }
+  }
+  s->scalar.rows = s->scalar.cols = N;
+  s->scalar.row.assign(N + 1, 0);
+  for (uint32_t i = 0; i < N; ++i) {
+    auto& l = adj[i];
+    l.push_back(i);
+    std::sort(l.begin(), l.end());
+    l.erase(std::unique(l.begin(), l.end()), l.end());
+    s->scalar.row[i] = (uint32_t)s->scalar.col.size();
+    s->scalar.col.insert(s->scalar.col.end(), l.begin(), l.end());
+  }
+  s->scalar.row[N] = (uint32_t)s->scalar.col.size();
+  s->scalar.val.assign(s->scalar.col.size(), 0.0f);
+  // f64 -> f32 upload (init/mesh.rs:56-155)
+  s->face_owner.assign(mv->face_owner, mv->face_owner + F);
+  s->face_neighbor.resize(F);
+  s->face_boundary.assign(mv->face_boundary, mv->face_boundary + F);
+  s->face_areas.resize(F);
+  s->face_nx.resize(F);
+  s->face_ny.resize(F);
+  s->face_cx.resize(F);
+  s->face_cy.resize(F);
+  for (uint32_t f = 0; f < F; ++f) {
+    s->face_neighbor[f] = (int32_t)mv->face_neighbor[f];  // u32::MAX reads as -1
+    s->face_areas[f] = (float)mv->face_area[f];
+    s->face_nx[f] = (float)mv->face_nx[f];
+    s->face_ny[f] = (float)mv->face_ny[f];
+    s->face_cx[f] = (float)mv->face_cx[f];
+    s->face_cy[f] = (float)mv->face_cy[f];
+  }
+  s->cell_cx.resize(N);
+  s->cell_cy.resize(N);
+  s->cell_vols.resize(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    s->cell_cx[i] = (float)mv->cell_cx[i];
+    s->cell_cy[i] = (float)mv->cell_cy[i];
+    s->cell_vols[i] = (float)mv->cell_vol[i];
+  }
+  s->cell_face_offsets.assign(mv->cell_face_offsets, mv->cell_face_offsets + N + 1);
+  const uint32_t S_ = s->cell_face_offsets[N];
+  s->cell_faces.assign(mv->cell_faces, mv->cell_faces + S_);
+  // cell_face_matrix_indices (init/mesh.rs:157-193)
+  s->cfmi.resize(S_);
+  for (uint32_t i = 0; i < N; ++i) {
+    for (uint32_t k = s->cell_face_offsets[i]; k < s->cell_face_offsets[i + 1]; ++k) {
+      const uint32_t f = s->cell_faces[k];
+      if (f >= F) return fail("cell_faces out of range"), false;
+      const uint32_t o = mv->face_owner[f];
+      const uint32_t nb = (o == i) ? mv->face_neighbor[f] : o;
+      if (nb == 0xFFFFFFFFu) {
+        s->cfmi[k] = 0xFFFFFFFFu;
+      } else {
+        const uint32_t* b = s->scalar.col.data() + s->scalar.row[i];
+        const uint32_t* e = s->scalar.col.data() + s->scalar.row[i + 1];
+        const uint32_t* it = std::lower_bound(b, e, nb);
+        s->cfmi[k] = (it != e && *it == nb) ? (uint32_t)(it - s->scalar.col.data()) : 0xFFFFFFFFu;
+      }
+    }
+  }
+  s->diag_idx.resize(N);
+  for (uint32_t i = 0; i < N; ++i) {
+    const uint32_t* b = s->scalar.col.data() + s->scalar.row[i];
+    const uint32_t* e = s->scalar.col.data() + s->scalar.row[i + 1];
+    const uint32_t* it = std::lower_bound(b, e, i);
+    if (it == e || *it != i) return fail("Diagonal not found in CSR cols"), false;
+    s->diag_idx[i] = (uint32_t)(it - s->scalar.col.data());
+  }
+  // coupled CSR (init/linear_solver/mod.rs:180-216)
+  s->c_row.assign(3 * (size_t)N + 1, 0);
+  uint32_t off = 0;
+  for (uint32_t i = 0; i < N; ++i) {
+    const uint32_t a = s->scalar.row[i], b = s->scalar.row[i + 1];
+    for (int sub = 0; sub < 3; ++sub) {
+      s->c_row[3 * i + sub] = off;
+      for (uint32_t k = a; k < b; ++k) {
+        const uint32_t j = s->scalar.col[k];
+        s->c_col.push_back(3 * j);
+        s->c_col.push_back(3 * j + 1);
+        s->c_col.push_back(3 * j + 2);
+      }
+      off += 3 * (b - a);
+    }
+  }
+  s->c_row[3 * (size_t)N] = off;
+  s->c_val.assign(off, 0.0f);
+  // fields (init/fields.rs:62-139)
+  for (auto& b : s->bufs) b.assign(N, FluidState{0, 0, 0, 0, 0, 0, 0, 0});
+  s->fluxes.assign(F, 0.0f);
+  s->grad_u.assign(2 * (size_t)N, 0.0f);
+  s->grad_v.assign(2 * (size_t)N, 0.0f);
+  s->rhs.assign(3 * (size_t)N, 0.0f);
+  s->x.assign(3 * (size_t)N, 0.0f);
+  s->diag_u_inv.assign(N, 0.0f);
+  s->diag_v_inv.assign(N, 0.0f);
+  s->diag_p_inv.assign(N, 0.0f);
+  cfd_constants& c = s->constants;
+  c.dt = 0.0001f;
+  c.dt_old = 0.0001f;
+  c.time = 0.0f;
+  c.viscosity = 0.01f;
+  c.density = 1.0f;
+  c.component = 0;
+  c.alpha_p = 1.0f;
+  c.scheme = 0;
+  c.alpha_u = 0.7f;
+  c.stride_x = 65535u * 64u;
+  c.time_scheme = 0;
+  c.inlet_velocity = 1.0f;
+  c.ramp_time = 0.1f;
+  c.precond_type = 0;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// prepare_coupled.wgsl:63-348.  Snapshot semantics (§0.1-3): every read of
+// state comes from the pre-kernel state; d_p / grad_p are committed after.
+void prepare(oracle_solver* s) {
+  const cfd_constants c = s->constants;
+  const uint32_t N = s->N;
+  FluidState* st = s->S();
+  std::vector<float> new_dp(N), new_gpx(N), new_gpy(N);
+#pragma omp parallel for schedule(static)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t idx = (uint32_t)li;
+    const float cx = s->cell_cx[idx], cy = s->cell_cy[idx];
+    const float vol = s->cell_vols[idx];
+    const uint32_t start = s->cell_face_offsets[idx], end = s->cell_face_offsets[idx + 1];
+    float diag_coeff = 0.0f;
+    float time_coeff = vol * c.density / c.dt;
+    if (c.time_scheme == 1u) {
+      const float r = c.dt / c.dt_old;
+      time_coeff = vol * c.density / c.dt * (1.0f + 2.0f * r) / (1.0f + r);
+    }
+    diag_coeff += time_coeff;
+    const float val_c_p = st[idx].p;
+    float gpx = 0.0f, gpy = 0.0f;
+    const float val_c_u = st[idx].ux, val_c_v = st[idx].uy;
+    float gux = 0.0f, guy = 0.0f, gvx = 0.0f, gvy = 0.0f;
+    for (uint32_t k = start; k < end; ++k) {
+      const uint32_t f = s->cell_faces[k];
+      const uint32_t owner = s->face_owner[f];
+      const int32_t neigh = s->face_neighbor[f];
+      const uint32_t bt = s->face_boundary[f];
+      float nx = s->face_nx[f], ny = s->face_ny[f];
+      const float area = s->face_areas[f];
+      const float fcx = s->face_cx[f], fcy = s->face_cy[f];
+      if (owner != idx) {
+        nx = -nx;
+        ny = -ny;
+      }
+      const float cox = s->cell_cx[owner], coy = s->cell_cy[owner];
+      float nfx = s->face_nx[f], nfy = s->face_ny[f];
+      const float dxv = fcx - cox, dyv = fcy - coy;
+      if (dxv * nfx + dyv * nfy < 0.0f) {
+        nfx = -nfx;
+        nfy = -nfy;
+      }
+      float flux = 0.0f;
+      if (neigh != -1) {
+        const uint32_t n = (uint32_t)neigh;
+        const float cnx = s->cell_cx[n], cny = s->cell_cy[n];
+        const FluidState& so = st[owner];
+        const FluidState& sn = st[n];
+        const float d_own = wdistance(cox, coy, fcx, fcy);
+        const float d_ngh = wdistance(cnx, cny, fcx, fcy);
+        const float total = d_own + d_ngh;
+        float lambda = 0.5f;
+        if (total > 1e-6f) lambda = d_ngh / total;
+        const float ufx = lambda * so.ux + (1.0f - lambda) * sn.ux;
+        const float ufy = lambda * so.uy + (1.0f - lambda) * sn.uy;
+        const float dp_face = lambda * so.d_p + (1.0f - lambda) * sn.d_p;
+        const float gfx = lambda * so.gpx + (1.0f - lambda) * sn.gpx;
+        const float gfy = lambda * so.gpy + (1.0f - lambda) * sn.gpy;
+        const float ddx = cnx - cox, ddy = cny - coy;
+        const float dist_proj = std::fabs(ddx * nfx + ddy * nfy);
+        const float dist = std::fmax(dist_proj, 1e-6f);
+        const float grad_p_n = gfx * nfx + gfy * nfy;
+        const float p_grad_f = (sn.p - so.p) / dist;
+        const float rc_term = dp_face * area * (grad_p_n - p_grad_f);
+        const float u_n = ufx * nfx + ufy * nfy;
+        flux = c.density * (u_n * area + rc_term);
+      } else {
+        if (bt == 1u) {
+          const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+          const float ubx = c.inlet_velocity * ramp, uby = 0.0f;
+          flux = c.density * (ubx * nfx + uby * nfy) * area;
+        } else if (bt == 3u) {
+          flux = 0.0f;
+        } else if (bt == 2u) {
+          const FluidState& so = st[owner];
+          const float u_n = so.ux * nfx + so.uy * nfy;
+          const float raw = c.density * u_n * area;
+          flux = std::fmax(0.0f, raw);
+        }
+      }
+      if (owner == idx) s->fluxes[f] = flux;  // owner is the unique writer
+      float flux_out = flux;
+      if (owner != idx) flux_out = -flux;
+      float ocx, ocy;
+      bool is_boundary = false;
+      uint32_t other = 0;
+      if (neigh != -1) {
+        other = (uint32_t)neigh;
+        if (owner != idx) other = owner;
+        ocx = s->cell_cx[other];
+        ocy = s->cell_cy[other];
+      } else {
+        is_boundary = true;
+        ocx = fcx;
+        ocy = fcy;
+      }
+      const float dvx = ocx - cx, dvy = ocy - cy;
+      const float dist = std::sqrt(dvx * dvx + dvy * dvy);
+      const float diff_coeff = c.viscosity * area / dist;
+      float conv_diag = 0.0f;
+      if (flux_out > 0.0f) conv_diag = flux_out;
+      if (!is_boundary) {
+        diag_coeff += diff_coeff + conv_diag;
+      } else {
+        if (bt == 1u) {
+          diag_coeff += diff_coeff;
+          if (flux_out > 0.0f) diag_coeff += flux_out;
+        } else if (bt == 3u) {
+          diag_coeff += diff_coeff;
+          if (flux_out > 0.0f) diag_coeff += flux_out;
+        } else if (bt == 2u) {
+          if (flux_out > 0.0f) diag_coeff += flux_out;
+        }
+      }
+      if (!is_boundary) {
+        const float d_c = wdistance(cx, cy, fcx, fcy);
+        const float d_o = wdistance(ocx, ocy, fcx, fcy);
+        const float tot = d_c + d_o;
+        float lp = 0.5f;
+        if (tot > 1e-6f) lp = d_o / tot;
+        const float vfp = lp * val_c_p + (1.0f - lp) * st[other].p;
+        gpx += vfp * nx * area;
+        gpy += vfp * ny * area;
+      } else {
+        float vfp = val_c_p;
+        if (bt == 2u) vfp = 0.0f;
+        gpx += vfp * nx * area;
+        gpy += vfp * ny * area;
+      }
+      float vfu = 0.0f, vfv = 0.0f;
+      if (!is_boundary) {
+        const float ouu = st[other].ux, ouv = st[other].uy;
+        const float d_c = wdistance(cx, cy, fcx, fcy);
+        const float d_o = wdistance(ocx, ocy, fcx, fcy);
+        const float tot = d_c + d_o;
+        if (tot > 1e-6f) {
+          const float l = d_o / tot;
+          vfu = l * val_c_u + (1.0f - l) * ouu;
+          vfv = l * val_c_v + (1.0f - l) * ouv;
+        } else {
+          vfu = 0.5f * (val_c_u + ouu);
+          vfv = 0.5f * (val_c_v + ouv);
+        }
+      } else {
+        if (bt == 1u) {
+          const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+          vfu = c.inlet_velocity * ramp;
+          vfv = 0.0f;
+        } else if (bt == 3u) {
+          vfu = 0.0f;
+          vfv = 0.0f;
+        } else {
+          vfu = val_c_u;
+          vfv = val_c_v;
+        }
+      }
+      gux += vfu * nx * area;
+      guy += vfu * ny * area;
+      gvx += vfv * nx * area;
+      gvy += vfv * ny * area;
+    }
+    new_dp[idx] = (std::fabs(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
+    new_gpx[idx] = gpx / vol;
+    new_gpy[idx] = gpy / vol;
+    s->grad_u[2 * idx] = gux / vol;
+    s->grad_u[2 * idx + 1] = guy / vol;
+    s->grad_v[2 * idx] = gvx / vol;
+    s->grad_v[2 * idx + 1] = gvy / vol;
+  }
+  for (uint32_t i = 0; i < N; ++i) {
+    st[i].d_p = new_dp[i];
+    st[i].gpx = new_gpx[i];
+    st[i].gpy = new_gpy[i];
+  }
+}
+
+// coupled_assembly_merged.wgsl:70-463
+void assemble(oracle_solver* s) {
+  const cfd_constants c = s->constants;
+  const uint32_t N = s->N;
+  FluidState* st = s->S();
+  const FluidState* so_ = s->SO();
+  const FluidState* soo_ = s->SOO();
+  float* mv = s->c_val.data();
+  float* smv = s->scalar.val.data();
+#pragma omp parallel for schedule(static)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t idx = (uint32_t)li;
+    const float cx = s->cell_cx[idx], cy = s->cell_cy[idx];
+    const float vol = s->cell_vols[idx];
+    const uint32_t start = s->cell_face_offsets[idx], end = s->cell_face_offsets[idx + 1];
+    const uint32_t soff = s->scalar.row[idx];
+    const uint32_t nnb = s->scalar.row[idx + 1] - soff;
+    const uint32_t r0 = 9u * soff, r1 = r0 + 3u * nnb, r2 = r0 + 6u * nnb;
+    float diag_u = 0.0f, diag_v = 0.0f, diag_p = 0.0f;
+    float sdup = 0.0f, sdvp = 0.0f, sdpu = 0.0f, sdpv = 0.0f, sdpp = 0.0f;
+    float rhs_u = 0.0f, rhs_v = 0.0f, rhs_p = 0.0f;
+    float scalar_diag_p = 0.0f;
+    const float unx = so_[idx].ux, uny = so_[idx].uy;
+    float coeff_time = vol * c.density / c.dt;
+    float rtu = coeff_time * unx, rtv = coeff_time * uny;
+    if (c.time_scheme == 1u) {
+      const float dt = c.dt, dt_old = c.dt_old;
+      const float r = dt / dt_old;
+      const float unm1x = soo_[idx].ux, unm1y = soo_[idx].uy;
+      coeff_time = vol * c.density / dt * (1.0f + 2.0f * r) / (1.0f + r);
+      const float fn = (1.0f + r);
+      const float fnm1 = (r * r) / (1.0f + r);
+      rtu = (vol * c.density / dt) * (fn * unx - fnm1 * unm1x);
+      rtv = (vol * c.density / dt) * (fn * uny - fnm1 * unm1y);
+    }
+    diag_u += coeff_time;
+    diag_v += coeff_time;
+    rhs_u += rtu;
+    rhs_v += rtv;
+    for (uint32_t k = start; k < end; ++k) {
+      const uint32_t f = s->cell_faces[k];
+      const uint32_t owner = s->face_owner[f];
+      const int32_t neigh = s->face_neighbor[f];
+      const uint32_t bt = s->face_boundary[f];
+      float nx = s->face_nx[f], ny = s->face_ny[f];
+      const float area = s->face_areas[f];
+      const float fcx = s->face_cx[f], fcy = s->face_cy[f];
+      float normal_sign = 1.0f;
+      if (owner != idx) {
+        nx = -nx;
+        ny = -ny;
+        normal_sign = -1.0f;
+      }
+      const float flux = s->fluxes[f] * normal_sign;
+      float ocx, ocy;
+      bool is_boundary = false;
+      uint32_t other = 0;
+      float d_p_neigh = 0.0f;
+      if (neigh != -1) {
+        other = (uint32_t)neigh;
+        if (owner != idx) other = owner;
+        ocx = s->cell_cx[other];
+        ocy = s->cell_cy[other];
+        d_p_neigh = st[other].d_p;
+      } else {
+        is_boundary = true;
+        ocx = fcx;
+        ocy = fcy;
+        d_p_neigh = st[idx].d_p;
+      }
+      const float dvx = ocx - cx, dvy = ocy - cy;
+      const float dist_proj = std::fabs(dvx * nx + dvy * ny);
+      const float dist = std::fmax(dist_proj, 1e-6f);
+      const float diff_coeff = c.viscosity * area / dist;
+      float conv_diag = 0.0f, conv_off = 0.0f;
+      if (flux > 0.0f)
+        conv_diag = flux;
+      else
+        conv_off = flux;
+      const uint32_t smi = s->cfmi[k];
+      const uint32_t rank = smi - soff;  // wraps for boundary faces; unused then
+      if (!is_boundary) {
+        const float coeff = -diff_coeff + conv_off;
+        mv[r0 + 3u * rank + 0u] = coeff;
+        mv[r0 + 3u * rank + 1u] = 0.0f;
+        mv[r1 + 3u * rank + 0u] = 0.0f;
+        mv[r1 + 3u * rank + 1u] = coeff;
+        diag_u += diff_coeff + conv_diag;
+        diag_v += diff_coeff + conv_diag;
+        if (c.scheme != 0u) {
+          const float uox = st[idx].ux, uoy = st[idx].uy;
+          const float unbx = st[other].ux, unby = st[other].uy;
+          float pu_u = uox, pu_v = uoy;
+          if (flux < 0.0f) {
+            pu_u = unbx;
+            pu_v = unby;
+          }
+          float ph_u = pu_u, ph_v = pu_v;
+          if (c.scheme == 1u) {
+            if (flux > 0.0f) {
+              const float gux = s->grad_u[2 * idx], guy = s->grad_u[2 * idx + 1];
+              const float gvx = s->grad_v[2 * idx], gvy = s->grad_v[2 * idx + 1];
+              const float rx = fcx - cx, ry = fcy - cy;
+              ph_u = uox + (gux * rx + guy * ry);
+              ph_v = uoy + (gvx * rx + gvy * ry);
+            } else {
+              const float gux = s->grad_u[2 * other], guy = s->grad_u[2 * other + 1];
+              const float gvx = s->grad_v[2 * other], gvy = s->grad_v[2 * other + 1];
+              const float rx = fcx - ocx, ry = fcy - ocy;
+              ph_u = unbx + (gux * rx + guy * ry);
+              ph_v = unby + (gvx * rx + gvy * ry);
+            }
+          } else if (c.scheme == 2u) {
+            if (flux > 0.0f) {
+              const float gux = s->grad_u[2 * idx], guy = s->grad_u[2 * idx + 1];
+              const float gvx = s->grad_v[2 * idx], gvy = s->grad_v[2 * idx + 1];
+              const float dx = ocx - cx, dy = ocy - cy;
+              const float gtu = gux * dx + guy * dy, gtv = gvx * dx + gvy * dy;
+              ph_u = 0.625f * uox + 0.375f * unbx + 0.125f * gtu;
+              ph_v = 0.625f * uoy + 0.375f * unby + 0.125f * gtv;
+            } else {
+              const float gux = s->grad_u[2 * other], guy = s->grad_u[2 * other + 1];
+              const float gvx = s->grad_v[2 * other], gvy = s->grad_v[2 * other + 1];
+              const float dx = cx - ocx, dy = cy - ocy;
+              const float gtu = gux * dx + guy * dy, gtv = gvx * dx + gvy * dy;
+              ph_u = 0.625f * unbx + 0.375f * uox + 0.125f * gtu;
+              ph_v = 0.625f * unby + 0.375f * uoy + 0.125f * gtv;
+            }
+          }
+          rhs_u -= flux * (ph_u - pu_u);
+          rhs_v -= flux * (ph_v - pu_v);
+        }
+        const float d_own = wdistance(cx, cy, fcx, fcy);
+        const float d_neigh = wdistance(ocx, ocy, fcx, fcy);
+        const float total = d_own + d_neigh;
+        float lambda = 0.5f;
+        if (total > 1e-6f) lambda = d_neigh / total;
+        const float pgx = area * nx, pgy = area * ny;
+        mv[r0 + 3u * rank + 2u] = (1.0f - lambda) * pgx;
+        mv[r1 + 3u * rank + 2u] = (1.0f - lambda) * pgy;
+        sdup += lambda * pgx;
+        sdvp += lambda * pgy;
+        const float dcx = nx * area, dcy = ny * area;
+        mv[r2 + 3u * rank + 0u] = (1.0f - lambda) * dcx;
+        mv[r2 + 3u * rank + 1u] = (1.0f - lambda) * dcy;
+        sdpu += lambda * dcx;
+        sdpv += lambda * dcy;
+        const float dp_f = lambda * st[idx].d_p + (1.0f - lambda) * st[other].d_p;
+        const float lapl = dp_f * area / dist;
+        mv[r2 + 3u * rank + 2u] = -lapl;
+        sdpp += lapl;
+        const float dpo = st[idx].d_p;
+        const float dpface = lambda * dpo + (1.0f - lambda) * d_p_neigh;
+        const float scoeff = c.density * dpface * area / dist;
+        if (smi != 0xFFFFFFFFu) smv[smi] = -scoeff;
+        scalar_diag_p += scoeff;
+      } else {
+        if (bt == 1u) {
+          const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
+          const float ubx = c.inlet_velocity * ramp, uby = 0.0f;
+          diag_u += diff_coeff;
+          diag_v += diff_coeff;
+          rhs_u += diff_coeff * ubx;
+          rhs_v += diff_coeff * uby;
+          if (flux > 0.0f) {
+            diag_u += flux;
+            diag_v += flux;
+          } else {
+            rhs_u -= flux * ubx;
+            rhs_v -= flux * uby;
+          }
+          const float pgx = area * nx, pgy = area * ny;
+          sdup += pgx;
+          sdvp += pgy;
+          const float flux_bc = (ubx * nx + uby * ny) * area;
+          rhs_p -= flux_bc;
+        } else if (bt == 3u) {
+          diag_u += diff_coeff;
+          diag_v += diff_coeff;
+          const float pgx = area * nx, pgy = area * ny;
+          sdup += pgx;
+          sdvp += pgy;
+        } else if (bt == 2u) {
+          if (flux > 0.0f) {
+            diag_u += flux;
+            diag_v += flux;
+          }
+          const float dcx = nx * area, dcy = ny * area;
+          sdpu += dcx;
+          sdpv += dcy;
+          const float dp_f = st[idx].d_p;
+          const float lapl = dp_f * area / dist;
+          sdpp += lapl;
+          const float dpo = st[idx].d_p;
+          const float scoeff = c.density * dpo * area / dist;
+          scalar_diag_p += scoeff;
+        }
+      }
+    }
+    const uint32_t sdi = s->diag_idx[idx];
+    const uint32_t dr = sdi - soff;
+    mv[r0 + 3u * dr + 0u] = diag_u;
+    mv[r0 + 3u * dr + 1u] = 0.0f;
+    mv[r0 + 3u * dr + 2u] = sdup;
+    mv[r1 + 3u * dr + 0u] = 0.0f;
+    mv[r1 + 3u * dr + 1u] = diag_v;
+    mv[r1 + 3u * dr + 2u] = sdvp;
+    mv[r2 + 3u * dr + 0u] = sdpu;
+    mv[r2 + 3u * dr + 1u] = sdpv;
+    mv[r2 + 3u * dr + 2u] = diag_p + sdpp;
+    s->rhs[3 * idx + 0] = rhs_u;
+    s->rhs[3 * idx + 1] = rhs_v;
+    s->rhs[3 * idx + 2] = rhs_p;
+    smv[sdi] = scalar_diag_p;
+    s->diag_u_inv[idx] = safe_inverse(diag_u);
+    s->diag_v_inv[idx] = safe_inverse(diag_v);
+    s->diag_p_inv[idx] = safe_inverse(scalar_diag_p);
+  }
+}
+
+// gmres_ops.wgsl:63-81
+void spmv(const oracle_solver* s, const float* xin, float* yout) {
+  const size_t n = 3 * (size_t)s->N;
+#pragma omp parallel for schedule(static)
+  for (long r = 0; r < (long)n; ++r) {
+    float sum = 0.0f;
+    for (uint32_t k = s->c_row[r]; k < s->c_row[r + 1]; ++k) sum += s->c_val[k] * xin[s->c_col[k]];
+    yout[r] = sum;
+  }
+}
+
+// schur_precond.wgsl:142-188 (predict_and_form_schur)
+void precond_predict(oracle_solver* s, const float* r_in, float* z_out) {
+  const uint32_t N = s->N;
+  float* p_prev = s->temp.data();  // binding 4 = b_temp (bg_schur[j])
+#pragma omp parallel for schedule(static)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t cell = (uint32_t)li;
+    const uint32_t base = cell * 3u;
+    z_out[base + 0] = s->diag_u_inv[cell] * r_in[base + 0];
+    z_out[base + 1] = s->diag_v_inv[cell] * r_in[base + 1];
+    z_out[base + 2] = 0.0f;
+    const uint32_t row_p = base + 2u;
+    float rhs_p = r_in[row_p];
+    for (uint32_t k = s->c_row[row_p]; k < s->c_row[row_p + 1]; ++k) {
+      const uint32_t col = s->c_col[k];
+      const uint32_t rem = col % 3u;
+      float z_val = 0.0f;
+      if (rem == 0u)
+        z_val = r_in[col] * s->diag_u_inv[col / 3u];
+      else if (rem == 1u)
+        z_val = r_in[col] * s->diag_v_inv[col / 3u];
+      rhs_p -= s->c_val[k] * z_val;
+    }
+    s->temp_p[cell] = rhs_p;
+    s->p_sol[cell] = s->diag_p_inv[cell] * rhs_p;
+    p_prev[cell] = 0.0f;
+  }
+}
+
+// schur_precond.wgsl:52-90 (relax_pressure), live scalar matrix, omega 1.2
+void relax_pressure(oracle_solver* s, const float* p_sol, float* p_prev) {
+  const float omega = 1.2f;
+  const uint32_t N = s->N;
+#pragma omp parallel for schedule(static)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t cell = (uint32_t)li;
+    float sigma = 0.0f;
+    for (uint32_t k = s->scalar.row[cell]; k < s->scalar.row[cell + 1]; ++k) {
+      const uint32_t col = s->scalar.col[k];
+      if (col != cell) sigma += s->scalar.val[k] * p_sol[col];
+    }
+    const float d_inv = s->diag_p_inv[cell];
+    const float hat_x = d_inv * (s->temp_p[cell] - sigma);
+    p_prev[cell] = wmix(p_prev[cell], hat_x, omega);
+  }
+}
+
+// schur_precond.wgsl:93-139 (correct_velocity)
+void precond_correct(oracle_solver* s, const float* p_sol, float* z_out) {
+  const uint32_t N = s->N;
+#pragma omp parallel for schedule(static)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t cell = (uint32_t)li;
+    const uint32_t base = cell * 3u, row_u = base, row_v = base + 1u;
+    const float p_val = p_sol[cell];
+    float cu = 0.0f;
+    for (uint32_t k = s->c_row[row_u]; k < s->c_row[row_u + 1]; ++k) {
+      const uint32_t col = s->c_col[k];
+      if (col % 3u == 2u) cu += s->c_val[k] * p_sol[col / 3u];
+    }
+    z_out[row_u] -= s->diag_u_inv[cell] * cu;
+    float cv = 0.0f;
+    for (uint32_t k = s->c_row[row_v]; k < s->c_row[row_v + 1]; ++k) {
+      const uint32_t col = s->c_col[k];
+      if (col % 3u == 2u) cv += s->c_val[k] * p_sol[col / 3u];
+    }
+    z_out[row_v] -= s->diag_v_inv[cell] * cv;
+    z_out[base + 2u] = p_val;
+  }
+}
+
+void ensure_fgmres(oracle_solver* s) {
+  if (s->fgmres_init) return;
+  const size_t n = 3 * (size_t)s->N;
+  const int m = s->m;
+  s->basis.assign((size_t)(m + 1) * n, 0.0f);
+  s->zvec.assign((size_t)m * n, 0.0f);
+  s->w.assign(n, 0.0f);
+  s->temp.assign(n, 0.0f);
+  s->temp_p.assign(s->N, 0.0f);
+  s->p_sol.assign(s->N, 0.0f);
+  s->H.assign((size_t)(m + 1) * m, 0.0f);
+  s->givens.assign((size_t)m * 2, 0.0f);
+  s->g.assign(m + 1, 0.0f);
+  s->y.assign(m, 0.0f);
+  s->fgmres_init = true;
+}
+
+void apply_precond(oracle_solver* s, const float* v, float* z) {
+  precond_predict(s, v, z);
+  bool in_sol = true;
+  if (s->constants.precond_type == 1) {
+    s->amg->v_cycle(s->p_sol.data(), s->temp_p.data());
+  } else {
+    const size_t p_iters_raw = 20u + (size_t)std::sqrt((float)s->N) / 2u;
+    const size_t p_iters = std::min<size_t>(p_iters_raw, 200) == 0 ? 0 : std::min<size_t>(p_iters_raw, 200) - 1;
+    for (size_t it = 0; it < p_iters; ++it) {
+      if (in_sol)
+        relax_pressure(s, s->p_sol.data(), s->temp.data());
+      else
+        relax_pressure(s, s->temp.data(), s->p_sol.data());
+      in_sol = !in_sol;
+    }
+  }
+  precond_correct(s, in_sol ? s->p_sol.data() : s->temp.data(), z);
+}
+
+// gmres_logic.wgsl:24-76
+float update_hessenberg_givens(oracle_solver* s, int j) {
+  const int m1 = s->m + 1;
+  auto hi = [&](int row, int col) { return (size_t)col * m1 + row; };
+  float* H = s->H.data();
+  for (int i = 0; i < j; ++i) {
+    const float hij = H[hi(i, j)], hi1j = H[hi(i + 1, j)];
+    const float cc = s->givens[2 * i], ss = s->givens[2 * i + 1];
+    H[hi(i, j)] = cc * hij + ss * hi1j;
+    H[hi(i + 1, j)] = -ss * hij + cc * hi1j;
+  }
+  const float hjj = H[hi(j, j)], hj1j = H[hi(j + 1, j)];
+  float cc = 1.0f, ss = 0.0f;
+  const float rho = std::sqrt(hjj * hjj + hj1j * hj1j);
+  if (std::fabs(rho) > 1e-20f) {
+    cc = hjj / rho;
+    ss = hj1j / rho;
+  }
+  s->givens[2 * j] = cc;
+  s->givens[2 * j + 1] = ss;
+  H[hi(j, j)] = rho;
+  H[hi(j + 1, j)] = 0.0f;
+  const float gj = s->g[j], gj1 = s->g[j + 1];
+  s->g[j] = cc * gj + ss * gj1;
+  s->g[j + 1] = -ss * gj + cc * gj1;
+  return std::fabs(s->g[j + 1]);
+}
+
+// gmres_logic.wgsl:78-104
+void solve_triangular(oracle_solver* s, int k) {
+  const int m1 = s->m + 1;
+  for (int li = 0; li < k; ++li) {
+    const int i = k - 1 - li;
+    float sum = s->g[i];
+    for (int j = i + 1; j < k; ++j) sum -= s->H[(size_t)j * m1 + i] * s->y[j];
+    const float diag = s->H[(size_t)i * m1 + i];
+    s->y[i] = (std::fabs(diag) > 1e-12f) ? sum / diag : 0.0f;
+  }
+}
+
+// r = b - A x into V0 (compute_residual_into, coupled_solver_fgmres.rs:1637-1667)
+float residual_into_v0(oracle_solver* s) {
+  const size_t n = 3 * (size_t)s->N;
+  spmv(s, s->x.data(), s->w.data());
+  float* v0 = s->basis.data();
+  const float alpha = 1.0f, beta = -1.0f;
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) v0[i] = alpha * s->rhs[i] + beta * s->w[i];
+  return std::sqrt(canon_dot(v0, v0, s->N));
+}
+
+void scale_in_place(float* v, size_t n, float a) {
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) v[i] = a * v[i];
+}
+
+// solve_coupled_fgmres, coupled_solver_fgmres.rs:1728-2448
+cfd_linear_stats solve(oracle_solver* s) {
+  cfd_linear_stats st{};
+  const uint32_t N = s->N;
+  const size_t n = 3 * (size_t)N;
+  const int m = s->m;
+  const int max_outer = s->cfg.max_outer_restarts;
+  const float tol = s->cfg.fgmres_rtol, abstol = s->cfg.fgmres_atol;
+  const bool fixed = s->cfg.fixed_inner > 0;
+  const int lag = s->cfg.convergence_lag;
+  ensure_fgmres(s);
+  if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
+    s->amg.reset(new Amg);
+    s->amg->build(s->scalar, 20);
+  }
+  const float rhs_norm = std::sqrt(canon_dot(s->rhs.data(), s->rhs.data(), N));
+  // The two early exits are kept even under the fixed schedule: the first
+  // step of a run at t=0 has b == 0 (inlet ramp smoothstep(0,ramp,0) = 0).
+  if (rhs_norm < abstol || !std::isfinite(rhs_norm)) {
+    st.iterations = 0;
+    st.residual = rhs_norm;
+    st.converged = rhs_norm < abstol;
+    st.diverged = !std::isfinite(rhs_norm);
+    return st;
+  }
+  const int m1 = m + 1;
+  float residual_norm = residual_into_v0(s);
+  const float target = std::fmax(tol * rhs_norm, abstol);
+  if (residual_norm < target) {
+    st.iterations = 0;
+    st.residual = residual_norm;
+    st.converged = 1;
+    return st;
+  }
+  scale_in_place(s->basis.data(), n, 1.0f / residual_norm);
+  std::fill(s->g.begin(), s->g.end(), 0.0f);
+  s->g[0] = residual_norm;
+  uint32_t total_iters = 0;
+  float final_resid = residual_norm;
+  bool converged = false;
+  int stagnation = 0;
+  float prev_resid = residual_norm;
+  const int inner_max = fixed ? std::min(s->cfg.fixed_inner, m) : m;
+  const int outer_max = fixed ? 1 : max_outer;
+  for (int outer = 0; outer < outer_max; ++outer) {
+    int basis_size = 0;
+    float resid_j = 0.0f;
+    for (int j = 0; j < inner_max; ++j) {
+      basis_size = j + 1;
+      ++total_iters;
+      float* vj = s->basis.data() + (size_t)j * n;
+      float* zj = s->zvec.data() + (size_t)j * n;
+      apply_precond(s, vj, zj);
+      spmv(s, zj, s->w.data());
+      // CGS (gmres_cgs.wgsl): H[i,j] = <w, V_i>, then w -= sum_i H[i,j] V_i
+      for (int i = 0; i <= j; ++i)
+        s->H[(size_t)j * m1 + i] = canon_dot(s->w.data(), s->basis.data() + (size_t)i * n, N);
+      {
+        const float* Hc = s->H.data() + (size_t)j * m1;
+        float* wv = s->w.data();
+        const float* B = s->basis.data();
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < (long)n; ++e) {
+          float corr = 0.0f;
+          for (int i = 0; i <= j; ++i) corr += Hc[i] * B[(size_t)i * n + e];
+          wv[e] = wv[e] - corr;
+        }
+      }
+      const float norm = std::sqrt(canon_dot(s->w.data(), s->w.data(), N));
+      s->H[(size_t)j * m1 + j + 1] = norm;
+      const float inv = norm > 1e-20f ? 1.0f / norm : 0.0f;
+      {
+        float* vn = s->basis.data() + (size_t)(j + 1) * n;
+        const float* wv = s->w.data();
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < (long)n; ++e) vn[e] = inv * wv[e];
+      }
+      resid_j = update_hessenberg_givens(s, j);
+      if (fixed) continue;
+      // async residual read, lag model (async_buffer.rs; §0.1-5)
+      bool have_check = false;
+      float check = 0.0f;
+      if (lag == 0) {
+        have_check = true;
+        check = resid_j;
+      } else if (s->inner_has_last) {
+        have_check = true;
+        check = s->inner_last;
+      }
+      s->inner_has_last = true;
+      s->inner_last = resid_j;
+      if (have_check && check < tol * rhs_norm) {
+        converged = true;
+        break;
+      }
+    }
+    solve_triangular(s, basis_size);
+    for (int i = 0; i < basis_size; ++i) {
+      const float a = s->y[i];
+      const float* zi = s->zvec.data() + (size_t)i * n;
+      float* xv = s->x.data();
+#pragma omp parallel for schedule(static)
+      for (long e = 0; e < (long)n; ++e) xv[e] = a * zi[e] + xv[e];
+    }
+    if (converged) {
+      final_resid = s->inner_last;  // flush -> last value
+      break;
+    }
+    residual_norm = residual_into_v0(s);
+    final_resid = residual_norm;
+    if (fixed) {
+      converged = residual_norm < tol * rhs_norm;
+      break;
+    }
+    if (residual_norm < tol * rhs_norm) {
+      converged = true;
+      break;
+    }
+    std::fill(s->g.begin(), s->g.end(), 0.0f);
+    s->g[0] = residual_norm;
+    if (residual_norm <= 0.0f) {
+      converged = true;
+      break;
+    }
+    scale_in_place(s->basis.data(), n, 1.0f / residual_norm);
+    const float improvement = (prev_resid - residual_norm) / prev_resid;
+    if (improvement < 1e-3f) {
+      ++stagnation;
+      if (stagnation >= 3) {
+        converged = true;
+        break;
+      }
+    } else {
+      stagnation = 0;
+    }
+    prev_resid = residual_norm;
+  }
+  st.iterations = total_iters;
+  st.residual = final_resid;
+  st.converged = converged;
+  st.diverged = std::isnan(final_resid);
+  return st;
+}
+
+// update_fields_from_coupled.wgsl:45-98 ; returns (max|du|, max|dp|)
+void update_fields(oracle_solver* s, float* mdu, float* mdp) {
+  const cfd_constants c = s->constants;
+  FluidState* st = s->S();
+  const uint32_t N = s->N;
+  // atomicMax on the f32 bit pattern (non-negative values; NaN wins), as the WGSL does
+  uint32_t bu = 0, bp = 0;
+#pragma omp parallel for schedule(static) reduction(max : bu, bp)
+  for (long li = 0; li < (long)N; ++li) {
+    const uint32_t idx = (uint32_t)li;
+    const float un = s->x[3 * idx], vn = s->x[3 * idx + 1], pn = s->x[3 * idx + 2];
+    const float uox = st[idx].ux, uoy = st[idx].uy, po = st[idx].p;
+    const float ux = uox + c.alpha_u * (un - uox);
+    const float uy = uoy + c.alpha_u * (vn - uoy);
+    const float pu = po + c.alpha_p * (pn - po);
+    st[idx].ux = ux;
+    st[idx].uy = uy;
+    st[idx].p = pu;
+    const float du = std::fmax(std::fabs(ux - uox), std::fabs(uy - uoy));
+    const float dp = std::fabs(pu - po);
+    uint32_t ubits, pbits;
+    std::memcpy(&ubits, &du, 4);
+    std::memcpy(&pbits, &dp, 4);
+    bu = std::max(bu, ubits);
+    bp = std::max(bp, pbits);
+  }
+  std::memcpy(mdu, &bu, 4);
+  std::memcpy(mdp, &bp, 4);
+}
+
+// coupled_solver.rs:501-580 (stride bug §0.1-12 reproduced: AoS view, floats 2i, 2i+1).
+// The f64 sums use the canonical chunk order (1024 records per chunk, 256
+// threads x 4, halving tree) instead of the reference's serial order: the two
+// differ only by f64 reassociation (~1e-16 relative).
+double tree256d(double* s) {
+  for (int h = kThreads / 2; h >= 1; h >>= 1)
+    for (int t = 0; t < h; ++t) s[t] = s[t] + s[t + h];
+  return s[0];
+}
+
+void check_evolution(oracle_solver* s) {
+  const uint32_t N = s->N;
+  const float* u_data = reinterpret_cast<const float*>(s->S());
+  const size_t len = 8 * (size_t)N;
+  const bool have = s->have_prev && s->prev_u_cpu.size() == len;
+  const size_t nc = num_chunks(N);
+  std::vector<double> part(5 * nc);
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < (long)nc; ++k) {
+    double acc[5][kThreads];
+    for (int t = 0; t < kThreads; ++t) {
+      double evo = 0, su = 0, sv = 0, squ = 0, sqv = 0;
+      for (int q = 0; q < kCellsPerThread; ++q) {
+        const size_t c = (size_t)k * kChunkCells + t + (size_t)kThreads * q;
+        if (c >= N) continue;
+        if (have)
+          for (int f = 0; f < 8; ++f) {
+            const float d = u_data[8 * c + f] - s->prev_u_cpu[8 * c + f];
+            evo += (double)(d * d);
+          }
+        const double u = (double)u_data[2 * c], v = (double)u_data[2 * c + 1];
+        su += u;
+        sv += v;
+        squ += u * u;
+        sqv += v * v;
+      }
+      acc[0][t] = evo;
+      acc[1][t] = su;
+      acc[2][t] = sv;
+      acc[3][t] = squ;
+      acc[4][t] = sqv;
+    }
+    for (int f = 0; f < 5; ++f) part[5 * k + f] = tree256d(acc[f]);
+  }
+  double tot[5];
+  for (int f = 0; f < 5; ++f) {
+    double acc[kThreads];
+    for (int t = 0; t < kThreads; ++t) {
+      double a = 0.0;
+      for (size_t q = t; q < nc; q += kThreads) a += part[5 * q + f];
+      acc[t] = a;
+    }
+    tot[f] = tree256d(acc);
+  }
+  const double n = (double)N;
+  const double mean_u = tot[1] / n, mean_v = tot[2] / n;
+  const double var_u = std::fmax(tot[3] / n - mean_u * mean_u, 0.0);
+  const double var_v = std::fmax(tot[4] / n - mean_v * mean_v, 0.0);
+  s->variance_history.push_back({var_u, var_v});
+  if (s->variance_history.size() > 10) s->variance_history.erase(s->variance_history.begin());
+  const double evo = have ? std::sqrt(tot[0] / n) : std::numeric_limits<double>::max();
+  s->prev_u_cpu.assign(u_data, u_data + len);
+  s->have_prev = true;
+  if (evo < 1e-6) {
+    if (var_u < 1e-10 && var_v < 1e-10) {
+      s->info.degenerate_count++;
+      s->info.steady_state_count = 0;
+    } else {
+      s->info.steady_state_count++;
+      s->info.degenerate_count = 0;
+    }
+  } else {
+    s->info.degenerate_count = 0;
+    s->info.steady_state_count = 0;
+  }
+  if (s->info.degenerate_count > 10) s->info.should_stop = 1;
+  if (s->info.steady_state_count > 10) s->info.should_stop = 1;
+}
+
+void rotate(oracle_solver* s) {  // coupled_solver.rs:43-71
+  s->step_index = (s->step_index + 1) % 3;
+  static const int tab[3][3] = {{0, 1, 2}, {2, 0, 1}, {1, 2, 0}};
+  s->i_state = tab[s->step_index][0];
+  s->i_old = tab[s->step_index][1];
+  s->i_old_old = tab[s->step_index][2];
+}
+
+int step(oracle_solver* s) {  // coupled_solver.rs:33-499
+  rotate(s);
+  s->constants.component = 0;
+  prepare(s);
+  const int max_iters = s->cfg.fixed_outer > 0 ? s->cfg.fixed_outer : std::max(s->cfg.n_outer_correctors, 10);
+  const bool fixed = s->cfg.fixed_outer > 0;
+  const double tol_u = 1e-5, tol_p = 1e-4;
+  double prev_u = std::numeric_limits<double>::max(), prev_p = std::numeric_limits<double>::max();
+  bool outer_has_last = false;
+  float last_u = 0, last_p = 0;
+  s->info.total_linear_iterations = 0;
+  for (int iter = 0; iter < max_iters; ++iter) {
+    if (iter > 0 || s->constants.scheme != 0) prepare(s);
+    assemble(s);
+    cfd_linear_stats ls = solve(s);
+    s->info.stats_p = ls;
+    s->info.total_linear_iterations += ls.iterations;
+    if (std::isnan(ls.residual)) return fail("Coupled Linear Solver Diverged: NaN detected in linear residual"), 3;
+    float mdu, mdp;
+    update_fields(s, &mdu, &mdp);
+    if (iter > 0) {
+      bool have = false;
+      float cu = 0, cp = 0;
+      if (s->cfg.convergence_lag == 0) {
+        have = true;
+        cu = mdu;
+        cp = mdp;
+      } else if (outer_has_last) {
+        have = true;
+        cu = last_u;
+        cp = last_p;
+      }
+      outer_has_last = true;
+      last_u = mdu;
+      last_p = mdp;
+      if (have) {
+        const double du = cu, dp = cp;
+        if (std::isnan(du) || std::isnan(dp))
+          return fail("Coupled Solver Diverged: NaN detected in outer residuals"), 3;
+        s->info.outer_residual_u = cu;
+        s->info.outer_residual_p = cp;
+        s->info.outer_iterations = iter + 1;
+        if (!fixed) {
+          if (du < tol_u && dp < tol_p) break;
+          const double rel_u = (std::isfinite(prev_u) && std::fabs(prev_u) > 1e-14)
+                                   ? std::fabs((du - prev_u) / prev_u)
+                                   : std::numeric_limits<double>::infinity();
+          const double rel_p = (std::isfinite(prev_p) && std::fabs(prev_p) > 1e-14)
+                                   ? std::fabs((dp - prev_p) / prev_p)
+                                   : std::numeric_limits<double>::infinity();
+          if (rel_u < 1e-2 && rel_p < 1e-2 && iter > 2) break;
+        }
+        prev_u = du;
+        prev_p = dp;
+      }
+    } else {
+      s->info.outer_residual_u = std::numeric_limits<float>::max();
+      s->info.outer_residual_p = std::numeric_limits<float>::max();
+      s->info.outer_iterations = 1;
+    }
+  }
+  s->constants.time += s->constants.dt;
+  check_evolution(s);
+  return 0;
+}
+
+}  // namespace
+
+// =============================== C API =====================================
+extern "C" {
+
+const char* oracle_last_error(void) { return g_err.c_str(); }
+
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
+oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg) {
+  if (!mesh || !cfg) return nullptr;
+  auto* s = new oracle_solver;
+  s->cfg = *cfg;
+  s->m = cfg->max_restart > 0 ? cfg->max_restart : 50;
+  if (!build(s, mesh)) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void oracle_destroy(oracle_solver* s) { delete s; }
+
+int oracle_set_u(oracle_solver* s, const double* uv) {  // solver.rs:9-21
+  FluidState* st = s->S();
+  for (uint32_t i = 0; i < s->N; ++i) st[i] = FluidState{(float)uv[2 * i], (float)uv[2 * i + 1], 0, 0, 0, 0, 0, 0};
+  return 0;
+}
+
+int oracle_set_p(oracle_solver* s, const double* p) {  // solver.rs:23-34
+  FluidState* st = s->S();
+  for (uint32_t i = 0; i < s->N; ++i) st[i] = FluidState{0, 0, (float)p[i], 0, 0, 0, 0, 0};
+  return 0;
+}
+
+int oracle_get_constants(const oracle_solver* s, cfd_constants* c) {
+  *c = s->constants;
+  return 0;
+}
+int oracle_set_constants(oracle_solver* s, const cfd_constants* c) {
+  s->constants = *c;
+  return 0;
+}
+int oracle_set_dt(oracle_solver* s, float dt) {  // solver.rs:36-44
+  if (s->constants.dt > 0.0f)
+    s->constants.dt_old = s->constants.dt;
+  else
+    s->constants.dt_old = dt;
+  s->constants.dt = dt;
+  return 0;
+}
+
+int oracle_initialize_history(oracle_solver* s) {  // solver.rs:276-294
+  s->bufs[s->i_old] = s->bufs[s->i_state];
+  s->bufs[s->i_old_old] = s->bufs[s->i_state];
+  return 0;
+}
+
+int oracle_step(oracle_solver* s) { return step(s); }
+
+int oracle_get_u(oracle_solver* s, double* uv) {
+  const FluidState* st = s->S();
+  for (uint32_t i = 0; i < s->N; ++i) {
+    uv[2 * i] = st[i].ux;
+    uv[2 * i + 1] = st[i].uy;
+  }
+  return 0;
+}
+int oracle_get_p(oracle_solver* s, double* p) {
+  const FluidState* st = s->S();
+  for (uint32_t i = 0; i < s->N; ++i) p[i] = st[i].p;
+  return 0;
+}
+int oracle_get_d_p(oracle_solver* s, double* dp) {
+  const FluidState* st = s->S();
+  for (uint32_t i = 0; i < s->N; ++i) dp[i] = st[i].d_p;
+  return 0;
+}
+int oracle_get_step_info(const oracle_solver* s, cfd_step_info* out) {
+  *out = s->info;
+  return 0;
+}
+
+size_t oracle_debug_buffer_len(const oracle_solver* s, int id) {
+  const size_t N = s->N;
+  switch (id) {
+    case 0: return s->F;
+    case 1: case 2: case 10: case 11: case 12: return 2 * N;
+    case 3: case 4: return 3 * N;
+    case 5: case 6: case 7: return N;
+    case 8: return s->scalar.val.size();
+    case 9: return s->c_val.size();
+    default: return 0;
+  }
+}
+
+int oracle_debug_buffer(oracle_solver* s, int id, float* out, size_t count) {
+  const size_t len = oracle_debug_buffer_len(s, id);
+  if (count < len || len == 0) return fail("bad debug buffer request");
+  const uint32_t N = s->N;
+  const FluidState* st = s->S();
+  switch (id) {
+    case 0: std::memcpy(out, s->fluxes.data(), len * 4); break;
+    case 1: std::memcpy(out, s->grad_u.data(), len * 4); break;
+    case 2: std::memcpy(out, s->grad_v.data(), len * 4); break;
+    case 3: std::memcpy(out, s->rhs.data(), len * 4); break;
+    case 4: std::memcpy(out, s->x.data(), len * 4); break;
+    case 5: std::memcpy(out, s->diag_u_inv.data(), len * 4); break;
+    case 6: std::memcpy(out, s->diag_v_inv.data(), len * 4); break;
+    case 7: std::memcpy(out, s->diag_p_inv.data(), len * 4); break;
+    case 8: std::memcpy(out, s->scalar.val.data(), len * 4); break;
+    case 9: std::memcpy(out, s->c_val.data(), len * 4); break;
+    case 10:
+      for (uint32_t i = 0; i < N; ++i) {
+        out[2 * i] = st[i].gpx;
+        out[2 * i + 1] = st[i].gpy;
+      }
+      break;
+    case 11:
+    case 12: {
+      const FluidState* b = id == 11 ? s->SO() : s->SOO();
+      for (uint32_t i = 0; i < N; ++i) {
+        out[2 * i] = b[i].ux;
+        out[2 * i + 1] = b[i].uy;
+      }
+      break;
+    }
+  }
+  return 0;
+}
+
+int oracle_debug_prepare_assemble(oracle_solver* s, int assemble_too) {
+  s->constants.component = 0;
+  prepare(s);
+  if (assemble_too) assemble(s);
+  return 0;
+}
+
+int oracle_amg_levels(const oracle_solver* s, int* num_levels, uint32_t* rows, uint64_t* nnz) {
+  if (!s->amg) {
+    *num_levels = 0;
+    return 0;
+  }
+  *num_levels = (int)s->amg->levels.size();
+  for (size_t i = 0; i < s->amg->levels.size() && i < 20; ++i) {
+    rows[i] = (uint32_t)s->amg->levels[i].n;
+    nnz[i] = s->amg->levels[i].A.col.size();
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+/*
+ * CPU oracle for the coupled-step hot path — TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / reported CPU baseline.  The
+ * product (cfd-demo2_amd/) never links or calls it.
+ *
+ * PARITY UNPINNED: the reference (Rust + wgpu, TSultanov/cfd-demo2) cannot be
+ * built here (no cargo/rustc, needs a wgpu adapter) and its own tests hold no
+ * golden field values.  The oracle is a literal f32 restatement
+ * of the reference WGSL + Rust control flow with the deterministic choices of
+ * SURVEY §0.1, checked against the reference tests' behavioural assertions.
+ */
+#ifndef CFD2_ORACLE_H
+#define CFD2_ORACLE_H
+#include "../include/cfd2_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_solver oracle_solver;
+
+oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg);
+void oracle_destroy(oracle_solver* s);
+void oracle_set_threads(int n);
+int oracle_set_u(oracle_solver* s, const double* uv);
+int oracle_set_p(oracle_solver* s, const double* p);
+int oracle_get_constants(const oracle_solver* s, cfd_constants* c);
+int oracle_set_constants(oracle_solver* s, const cfd_constants* c);
+int oracle_set_dt(oracle_solver* s, float dt);
+int oracle_initialize_history(oracle_solver* s);
+int oracle_step(oracle_solver* s);
+int oracle_get_u(oracle_solver* s, double* uv);
+int oracle_get_p(oracle_solver* s, double* p);
+int oracle_get_d_p(oracle_solver* s, double* dp);
+int oracle_get_step_info(const oracle_solver* s, cfd_step_info* out);
+/* same buffer ids as cfd_debug_buffer */
+size_t oracle_debug_buffer_len(const oracle_solver* s, int id);
+int oracle_debug_buffer(oracle_solver* s, int id, float* out, size_t count);
+int oracle_debug_prepare_assemble(oracle_solver* s, int assemble);
+int oracle_amg_levels(const oracle_solver* s, int* num_levels, uint32_t* rows, uint64_t* nnz);
+const char* oracle_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,194 @@
+"""HIP path vs CPU oracle (tests/oracle_py.py) through the C ABI.
+
+Parity bar: the HIP kernels reproduce the oracle's f32 arithmetic operation
+for operation (-ffp-contract=off, canonical reduction order), so fields,
+matrices and step statistics must be BIT-EXACT (np.array_equal).  North-star
+tolerance (fields within 1e-5 relative) is checked as well, as a weaker bound.
+"""
+import numpy as np
+import pytest
+
+from cfd2_amd import GpuSolver, default_config
+from tests.meshes import backwards_step, bench_mesh, channel_obstacle
+from tests.oracle_py import OracleSolver
+
+pytestmark = pytest.mark.gpu
+
+DEBUG_IDS = list(range(13))
+
+
+def _pair(mesh, **cfg):
+    c = default_config(**cfg)
+    return GpuSolver(mesh, config=c), OracleSolver(mesh, config=default_config(**cfg))
+
+
+def _setup_amg_test(s, mesh, precond):
+    """tests/amg_test.rs:22-43."""
+    s.set_dt(0.001)
+    s.set_viscosity(0.001)
+    s.set_density(1.0)
+    s.set_alpha_p(0.3)
+    s.set_alpha_u(0.7)
+    s.set_scheme(0)
+    a = mesh.arrays()
+    u = np.zeros((mesh.num_cells(), 2))
+    u[(a["cell_cx"] < 0.05) & (a["cell_cy"] > 0.5), 0] = 1.0
+    s.set_u(u)
+    s.initialize_history()
+    s.set_precond_type(precond)
+
+
+def _setup_schemes_test(s, mesh, scheme, time_scheme):
+    """tests/coupled_schemes_test.rs:28-49 (set_u then set_p zeroes u; dt written directly)."""
+    n = mesh.num_cells()
+    s.set_u(np.tile([0.1, 0.0], (n, 1)))
+    s.set_p(np.zeros(n))
+    c = s.constants
+    c.dt = 0.001
+    s.constants = c
+    s.set_density(1.0)
+    s.set_viscosity(0.01)
+    s.set_alpha_u(0.9)
+    s.set_alpha_p(0.9)
+    s.set_scheme(scheme)
+    s.set_time_scheme(time_scheme)
+    s.update_constants()
+
+
+def _assert_same_fields(g, o, ctx=""):
+    ug, uo = g.get_u(), o.get_u()
+    pg, po = g.get_p(), o.get_p()
+    dg, do = g.get_d_p(), o.get_d_p()
+    assert np.all(np.isfinite(ug)) and np.all(np.isfinite(pg)), ctx
+    # north-star tolerance first (informative), then the bit-exact bar
+    for a, b, name in ((ug, uo, "u"), (pg, po, "p"), (dg, do, "d_p")):
+        den = max(np.linalg.norm(b), 1e-30)
+        assert np.linalg.norm(a - b) / den <= 1e-5, f"{ctx} {name} rel-L2 > 1e-5"
+        assert np.array_equal(a, b), f"{ctx} {name} not bit-exact (max diff {np.abs(a - b).max()})"
+
+
+def _assert_same_info(g, o, ctx=""):
+    ig, io = g.step_info(), o.step_info()
+    for f in ("should_stop", "degenerate_count", "steady_state_count", "outer_iterations",
+              "total_linear_iterations"):
+        assert getattr(ig, f) == getattr(io, f), f"{ctx} step_info.{f}: {getattr(ig, f)} vs {getattr(io, f)}"
+    assert ig.outer_residual_u == io.outer_residual_u, ctx
+    assert ig.outer_residual_p == io.outer_residual_p, ctx
+    assert ig.stats_p.iterations == io.stats_p.iterations, ctx
+    assert ig.stats_p.residual == io.stats_p.residual, ctx
+
+
+@pytest.mark.parametrize("scheme,time_scheme", [(0, 0), (1, 0), (2, 0), (0, 1)])
+def test_prepare_assemble_kernels_bitexact(scheme, time_scheme):
+    """prepare_coupled + coupled_assembly_merged: every output buffer bit-exact."""
+    mesh = channel_obstacle()
+    g, o = _pair(mesh)
+    rng = np.random.default_rng(1234)
+    u0 = rng.uniform(-1, 1, size=(mesh.num_cells(), 2))
+    for s in (g, o):
+        s.set_u(u0)
+        s.initialize_history()
+        s.set_dt(0.002)
+        s.set_scheme(scheme)
+        s.set_time_scheme(time_scheme)
+        c = s.constants
+        c.time = 0.05  # inlet ramp active
+        s.constants = c
+        s.debug_prepare_assemble(False)  # d_p / grad_p from the zero state
+        s.debug_prepare_assemble(True)   # Rhie-Chow with non-zero d_p / grad_p
+    for bid in DEBUG_IDS:
+        a, b = g.debug_buffer(bid), o.debug_buffer(bid)
+        assert a.shape == b.shape, bid
+        assert np.all(np.isfinite(a)), bid
+        assert np.array_equal(a, b), f"debug buffer {bid}: max diff {np.abs(a - b).max()}"
+
+
+@pytest.mark.parametrize("precond", [0, 1])
+def test_amg_test_parity_and_bounds(precond):
+    """tests/amg_test.rs: 5 steps; 0 < max|p| < 1000; GPU == oracle bit-exact each step."""
+    mesh = backwards_step()
+    g, o = _pair(mesh)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, precond)
+    for k in range(5):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"step {k}")
+        _assert_same_info(g, o, f"step {k}")
+    max_p = np.abs(g.get_p()).max()
+    assert 0.0 < max_p < 1000.0
+    if precond == 1:
+        assert g.amg_levels() == o.amg_levels()
+
+
+@pytest.mark.parametrize("scheme,time_scheme", [(0, 0), (1, 0), (2, 0), (0, 1)])
+def test_coupled_schemes_parity(scheme, time_scheme):
+    """tests/coupled_schemes_test.rs: 2 steps per scheme, all fields finite, GPU == oracle."""
+    mesh = backwards_step()
+    g, o = _pair(mesh)
+    for s in (g, o):
+        _setup_schemes_test(s, mesh, scheme, time_scheme)
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"scheme {scheme}/{time_scheme} step {k}")
+        _assert_same_info(g, o)
+
+
+def test_divergence_channel_obstacle_gpu():
+    """tests/gpu_divergence_test.rs (shortened to 20 steps): adaptive dt, max|u| <= 20."""
+    mesh = channel_obstacle()
+    g = GpuSolver(mesh)
+    g.set_dt(0.01)
+    g.set_viscosity(0.01)
+    g.set_density(1.0)
+    g.set_scheme(0)
+    a = mesh.arrays()
+    u = np.zeros((mesh.num_cells(), 2))
+    u[a["cell_cx"] < 0.025, 0] = 1.0
+    g.set_u(u)
+    for _ in range(20):
+        uu = g.get_u()
+        vmax = float(np.sqrt((uu ** 2).sum(1)).max())
+        if vmax > 1e-6:
+            g.set_dt(float(np.clip(0.5 * 0.025 / vmax, 1e-5, 0.1)))
+        g.step()
+        assert not g.should_stop or g.degenerate_count <= 10
+        assert vmax <= 20.0 and np.isfinite(vmax)
+
+
+@pytest.mark.parametrize("lag", [0, 1])
+def test_fixed_schedule_and_lag_parity(lag):
+    """Fixed benchmark schedule (K outer x M inner) and both lag models: bit-exact."""
+    mesh = channel_obstacle(h=0.03)
+    for cfg in (dict(fixed_outer=3, fixed_inner=12, convergence_lag=lag),
+                dict(convergence_lag=lag)):
+        g, o = _pair(mesh, **cfg)
+        for s in (g, o):
+            _setup_amg_test(s, mesh, 1)
+        for k in range(3):
+            g.step()
+            o.step()
+            _assert_same_fields(g, o, f"{cfg} step {k}")
+            _assert_same_info(g, o, f"{cfg} step {k}")
+
+
+def test_bench_geometry_parity_medium():
+    """SURVEY §8(d) geometry at ~100k cells, fixed schedule, AMG: one step bit-exact."""
+    mesh = bench_mesh(0.0055, 30)
+    g, o = _pair(mesh, fixed_outer=2, fixed_inner=8)
+    for s in (g, o):
+        s.set_dt(1e-3)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_alpha_u(0.7)
+        s.set_alpha_p(0.3)
+        s.set_precond_type(1)
+        s.initialize_history()
+        c = s.constants
+        c.time = 0.05
+        s.constants = c
+    g.step()
+    o.step()
+    _assert_same_fields(g, o, "bench geometry")
+    assert g.amg_levels() == o.amg_levels()
