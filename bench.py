@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the coupled FV step (BASELINE.json metric: cell-updates/sec +
+AMG smoother HBM GB/s on the channel+obstacle mesh).
+
+One "step" = one GpuSolver.step() (reference coupled_solver.rs:33-499) on the
+SURVEY §8(d) workload under its fixed schedule: 5 Picard iterations x 30
+FGMRES(Schur + 1 AMG V-cycle) iterations, Upwind/Euler, rho=1, nu=0.01,
+dt=1e-3, alpha_u=0.7, alpha_p=0.3, U_in=1 ramped over 0.1.  Synthetic input:
+the deterministic cut-cell mesh of ChannelWithObstacle{3x1, (1.0,0.51), r 0.1}
+(h=5.449e-4 -> ~10M cells per GPU), smoothed (0.3, 100); initial u = p = 0.
+
+Launch: ``python bench.py`` (N=1) or, for N GPUs, under torch.distributed.run
+with one process per GPU; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cfd-demo2_amd"))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (h, target cells per GPU, BASELINE.json configs[] index)
+    "c1": (0.001723, 1.0e6, 1),
+    "c2": (5.449e-4, 1.0e7, 2),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_solver(solver, ramp_time=0.1):
+    solver.set_dt(1e-3)
+    solver.set_viscosity(0.01)
+    solver.set_density(1.0)
+    solver.set_alpha_u(0.7)
+    solver.set_alpha_p(0.3)
+    solver.set_scheme(0)
+    solver.set_time_scheme(0)
+    solver.set_inlet_velocity(1.0)
+    solver.set_ramp_time(ramp_time)
+    solver.set_precond_type(1)  # AMG
+    solver.initialize_history()
+
+
+def cpu_baseline(mesh, n_cells, outer_fixed, inner_fixed):
+    """Oracle (C++ CPU restatement, OpenMP) on a bounded sample of the workload:
+    the same mesh and physics, the trivial t=0 step untimed (it also builds the
+    AMG hierarchy), then ONE Picard iteration (1 of the step's 5) of step 2.
+    value = cells * (1 / outer_fixed) / seconds, i.e. in cell-updates/sec."""
+    from tests.oracle_py import OracleSolver, set_threads
+    from cfd2_amd import default_config
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    set_threads(threads)
+    o = OracleSolver(mesh, config=default_config(fixed_outer=1, fixed_inner=inner_fixed))
+    setup_solver(o)
+    o.step()  # t = 0: b == 0 -> early exits; builds the AMG hierarchy
+    t0 = time.perf_counter()
+    o.step()
+    dt = time.perf_counter() - t0
+    value = n_cells * (1.0 / outer_fixed) / dt
+    return {
+        "value": value,
+        "unit": "cell-updates/sec",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle/oracle.cpp (f32, OpenMP {threads} threads), same {n_cells}-cell mesh, "
+                   f"1 Picard iteration x {inner_fixed} FGMRES iterations of step 2 "
+                   f"({dt:.2f} s), scaled by 1/{outer_fixed} step"),
+    }
+
+
+def load_traffic(round_tag):
+    """HBM bytes per level-0 smoother launch from the committed rocprofv3 PMC
+    summary (profiles/<round>/smoother_pmc.json), or None."""
+    p = os.path.join(ROOT, "profiles", round_tag, "smoother_pmc.json")
+    try:
+        with open(p) as f:
+            return float(json.load(f)["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--outer", type=int, default=5)
+    ap.add_argument("--inner", type=int, default=30)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--round", default="r01")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo")
+
+    import numpy as np  # noqa: F401
+    from cfd2_amd import GpuSolver, default_config
+    from cfd2_amd.mesh import bench_channel
+
+    h, _, cfg_idx = CONFIGS[args.config]
+    t0 = time.perf_counter()
+    mesh = bench_channel(h, 100)
+    n_cells = mesh.num_cells()
+    log(f"[rank {rank}] mesh {n_cells} cells / {mesh.num_faces()} faces in {time.perf_counter() - t0:.1f}s")
+
+    cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner)
+    t0 = time.perf_counter()
+    solver = GpuSolver(mesh, config=cfg, device=local_rank if world > 1 else 0)
+    setup_solver(solver)
+    log(f"[rank {rank}] solver created in {time.perf_counter() - t0:.1f}s")
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for k in range(args.warmup):
+        t0 = time.perf_counter()
+        solver.step()
+        log(f"[rank {rank}] warmup step {k}: {time.perf_counter() - t0:.3f}s")
+    barrier_sync()
+    solver.profile_enable(True)
+    solver.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solver.step()
+    # step() returns after its blocking check_evolution read: the stream is idle
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    sm_ms, sm_n, sm_bytes = solver.profile_smoother()
+    solver.profile_enable(False)
+    info = solver.step_info()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([n_cells], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        total_cells = float(c.item())
+    else:
+        total_cells = float(n_cells)
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = total_cells * args.steps / elapsed
+    sm_avg_s = (sm_ms / 1e3) / max(sm_n, 1)
+    achieved = sm_bytes / sm_avg_s / 1e9 if sm_n else 0.0
+    step_bytes = solver.step_algorithmic_bytes()
+    out = {
+        "metric": "cell-updates/sec + AMG smoother HBM GB/s, channel+obstacle",
+        "value": value,
+        "unit": "cell-updates/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: deterministic cut-cell channel+obstacle mesh (reference generator restated)",
+        "config": {
+            "workload": (f"BASELINE configs[{cfg_idx}]: channel+obstacle {n_cells} cells per GPU, "
+                         f"fixed schedule {args.outer} Picard x {args.inner} FGMRES/AMG per step"),
+            "cells_per_gpu": n_cells,
+            "h": h,
+            "parallelism": f"replicas{world}" if world > 1 else "single",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_amg_smooth (level 0)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": load_traffic(args.round),
+            "bytes_per_launch": sm_bytes,
+            "avg_launch_us": sm_avg_s * 1e6,
+            "launches": sm_n,
+        },
+        "step_algorithmic_gbs": step_bytes / (ms_per_step / 1e3) / 1e9,
+        "linear_iterations_last_step": int(info.total_linear_iterations),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(mesh, n_cells, args.outer, args.inner)
+        except Exception as e:  # the baseline is reported, never the target
+            log("cpu baseline failed:", e)
+            out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
