@@ -192,3 +192,14 @@ def test_bench_geometry_parity_medium():
     o.step()
     _assert_same_fields(g, o, "bench geometry")
     assert g.amg_levels() == o.amg_levels()
+
+
+@pytest.mark.parametrize("name", ["schemes", "amg"])
+def test_golden_fixtures_gpu(name):
+    """HIP path reproduces the committed golden vectors (tests/golden) bit-for-bit."""
+    import os
+    from tests.golden.make_golden import run_case
+    ref = np.load(os.path.join(os.path.dirname(__file__), "golden", f"{name}.npz"), allow_pickle=False)
+    got = run_case(name, GpuSolver)
+    for k in ref.files:
+        assert np.array_equal(ref[k], got[k]), k

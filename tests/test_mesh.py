@@ -1,0 +1,110 @@
+"""Mesh input (restated cut-cell generator, src/solver/mesh): the reference's own
+mesh tests (src/solver/mesh/tests.rs:63-145) plus structural invariants the
+solver relies on."""
+import math
+import os
+import tempfile
+
+import numpy as np
+
+from cfd2_amd.mesh import (BackwardsStep, ChannelWithObstacle, CircleObstacle, Mesh,
+                           bench_channel, generate_cut_cell_mesh)
+from tests.meshes import backwards_step
+
+
+def test_mesh_generation_circle_obstacle():
+    """tests.rs:63-115: fixed vertices stay on the surface after smoothing; skew < 0.25."""
+    geo = CircleObstacle(center=(0.5001, 0.5001), radius=0.2, domain_min=(0.0, 0.0),
+                         domain_max=(1.0, 1.0))
+    m = generate_cut_cell_mesh(geo, 0.1, 0.1, 1.2, (1.0, 1.0))
+    assert m.num_cells() > 0
+    vx, vy, vf = m.vertices()
+    fixed = np.nonzero(vf)[0]
+    assert len(fixed) > 0
+    m.smooth(geo, 0.05, 50)
+    vx, vy, _ = m.vertices()
+    g = geo._geo()
+    for i in fixed:  # sdf of the smoothed fixed vertices (re-evaluated with numpy)
+        x, y = vx[i], vy[i]
+        dx = abs(x - 0.5) - 0.5
+        dy = abs(y - 0.5) - 0.5
+        box = min(max(dx, dy), 0.0) + math.hypot(max(dx, 0.0), max(dy, 0.0))
+        circ = math.hypot(x - 0.5001, y - 0.5001) - 0.2
+        assert abs(max(box, -circ)) < 1e-4
+    assert g.kind == 3
+    assert m.calculate_max_skewness() < 0.25
+
+
+def test_mesh_generation_backwards_step():
+    """tests.rs:117-145: misaligned step (0.501) -> sliver cells; skew < 0.6 after smoothing."""
+    geo = BackwardsStep(length=2.0, height_inlet=0.501, height_outlet=1.0, step_x=0.501)
+    m = generate_cut_cell_mesh(geo, 0.1, 0.1, 1.2, (2.0, 1.0))
+    assert m.num_cells() > 0
+    m.smooth(geo, 0.1, 50)
+    assert m.calculate_max_skewness() < 0.6
+
+
+def _check_structure(m, domain_area, rtol=1e-9):
+    a = m.arrays()
+    n, f = m.num_cells(), m.num_faces()
+    assert np.all(a["cell_vol"] > 0)
+    assert abs(a["cell_vol"].sum() - domain_area) <= rtol * domain_area
+    assert np.allclose(a["face_nx"] ** 2 + a["face_ny"] ** 2, 1.0)
+    assert np.all(a["face_area"] > 0)
+    internal = a["face_neighbor"] != 0xFFFFFFFF
+    assert np.all(a["face_boundary"][internal] == 0)
+    assert np.all(np.isin(a["face_boundary"][~internal], [1, 2, 3]))
+    # every face is listed exactly by its owner (and its neighbour if internal)
+    counts = np.bincount(a["cell_faces"], minlength=f)
+    assert np.all(counts == np.where(internal, 2, 1))
+    offs = a["cell_face_offsets"]
+    assert offs[0] == 0 and offs[-1] == len(a["cell_faces"]) and np.all(np.diff(offs) >= 3)
+    # stored normals point out of the owner for boundary faces (cut_cell.rs:455)
+    b = ~internal
+    ow = a["face_owner"][b]
+    d = (a["face_cx"][b] - a["cell_cx"][ow]) * a["face_nx"][b] + \
+        (a["face_cy"][b] - a["cell_cy"][ow]) * a["face_ny"][b]
+    assert np.all(d > 0)
+    # inlet faces at x = 0, outlet at x = L
+    return a
+
+
+def test_coupled_schemes_mesh():
+    """The mesh of coupled_schemes_test.rs / amg_test.rs: ~1.3k cells."""
+    m = backwards_step()
+    assert m.num_cells() == 1300
+    a = _check_structure(m, 3.5 * 1.0 - 0.5 * 0.5)
+    inlet = a["face_boundary"] == 1
+    assert np.all(np.abs(a["face_cx"][inlet]) < 1e-6)
+    outlet = a["face_boundary"] == 2
+    assert np.all(np.abs(a["face_cx"][outlet] - 3.5) < 1e-6)
+
+
+def test_channel_obstacle_mesh_area_and_determinism():
+    geo = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.51), obstacle_radius=0.1)
+    m1 = generate_cut_cell_mesh(geo, 0.02, 0.02, 1.2, (3.0, 1.0))
+    m1.smooth(geo, 0.3, 30)
+    m2 = bench_channel(0.02, 30)
+    _check_structure(m1, 3.0 - math.pi * 0.01, rtol=1e-4)  # polygonal circle
+    a1, a2 = m1.arrays(), m2.arrays()
+    for k in a1:
+        assert np.array_equal(a1[k], a2[k]), k
+
+
+def test_bench_cell_count_formula():
+    """N ~ 2.9686 / h^2 for the benchmark geometry (partial edge cells: <3%)."""
+    for h in (0.0172, 0.01):
+        m = bench_channel(h, 0)
+        assert abs(m.num_cells() - 2.9686 / h ** 2) / (2.9686 / h ** 2) < 0.03
+
+
+def test_save_load_roundtrip():
+    m = backwards_step()
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "m.bin")
+        m.save(p)
+        m2 = Mesh.load(p)
+        a, b = m.arrays(), m2.arrays()
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+        assert m2.calculate_max_skewness() == m.calculate_max_skewness()
