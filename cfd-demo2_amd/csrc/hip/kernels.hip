@@ -32,6 +32,18 @@ __device__ __forceinline__ float safe_inverse(float v) {
 
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// XCD-aware block -> tile remap (cdna_hip_programming.md T1): the dispatcher
+// deals blocks round-robin over the 8 XCDs; remapping gives XCD k a contiguous
+// range of rows, so the i +- n_y neighbour gathers of a structured-ish cut-cell
+// mesh hit that XCD's L2.  Bijective for any grid size; a speed choice only.
+__device__ __forceinline__ uint32_t xcd_block() {
+  const uint32_t b = blockIdx.x, nb = gridDim.x;
+  const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+  const uint32_t base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+__device__ __forceinline__ uint32_t row_id() { return xcd_block() * kBlock + threadIdx.x; }
+
 // Halving tree over 256 per-thread values (canonical order): levels 128 and 64
 // through LDS, levels 32..1 by wavefront shuffles in wave 0.  Result valid in
 // thread 0.  `lds` must hold 256 floats; caller syncs before reusing it.
@@ -65,7 +77,7 @@ __device__ __forceinline__ float block_final(const float* partial, uint32_t np, 
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
 // Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
 __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -183,7 +195,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
 
 // coupled_assembly_merged.wgsl:70-463
 __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -280,7 +292,8 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
       const float scoeff = c.density * dp_f * area / dist;
       sdiag += scoeff;
       const size_t slot = (size_t)rank * N + i;
-      a.cval[slot] = make_float4(coeff, oml * pgx, oml * pgy, -lapl);
+      a.cval_a[slot] = make_float2(coeff, -lapl);
+      a.cval_g[slot] = make_float2(oml * pgx, oml * pgy);
       a.sval[slot] = -scoeff;
     } else if (bt == 1u) {
       const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
@@ -314,7 +327,8 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
   }
   const uint32_t dr = a.srank_diag[i];
   const size_t dslot = (size_t)dr * N + i;
-  a.cval[dslot] = make_float4(diag_uv, sdup, sdvp, 0.0f + sdpp);
+  a.cval_a[dslot] = make_float2(diag_uv, 0.0f + sdpp);
+  a.cval_g[dslot] = make_float2(sdup, sdvp);
   a.cdiag2[i] = make_float2(sdpu, sdpv);
   a.sval[dslot] = sdiag;
   a.rhs[3 * (size_t)i + 0] = rhs_u;
@@ -324,12 +338,16 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
   a.dinv_p[i] = safe_inverse(sdiag);
 }
 
-// update_fields_from_coupled.wgsl:45-98; per-wave max of the f32 bit patterns
-// then one atomicMax per wave (max is order-independent: deterministic).
+// update_fields_from_coupled.wgsl:45-98.  The reference folds max|du|, max|dp|
+// with one atomicMax per workgroup into a single word; here each block writes
+// the max of its bit patterns (order-independent) and k_maxdiff_final folds
+// them, avoiding ~40k same-address atomics per call.
 __global__ void __launch_bounds__(kBlock) k_update_fields(uint32_t N, float alpha_u, float alpha_p,
                                                           const float* __restrict__ x, float2* u,
-                                                          float* p, uint32_t* maxbits) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+                                                          float* p, uint32_t* blockmax) {
+  __shared__ uint32_t su[4], sp[4];
+  const uint32_t lb = xcd_block();
+  const uint32_t i = lb * kBlock + threadIdx.x;
   uint32_t bu = 0, bp = 0;
   if (i < N) {
     const float un = x[3 * (size_t)i], vn = x[3 * (size_t)i + 1], pn = x[3 * (size_t)i + 2];
@@ -349,9 +367,39 @@ __global__ void __launch_bounds__(kBlock) k_update_fields(uint32_t N, float alph
     bu = max(bu, (uint32_t)__shfl_xor((int)bu, o));
     bp = max(bp, (uint32_t)__shfl_xor((int)bp, o));
   }
+  const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(&maxbits[0], bu);
-    atomicMax(&maxbits[1], bp);
+    su[wv] = bu;
+    sp[wv] = bp;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    blockmax[2 * lb] = max(max(su[0], su[1]), max(su[2], su[3]));
+    blockmax[2 * lb + 1] = max(max(sp[0], sp[1]), max(sp[2], sp[3]));
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_maxdiff_final(const uint32_t* __restrict__ blockmax,
+                                                          uint32_t nb, uint32_t* maxbits) {
+  __shared__ uint32_t su[4], sp[4];
+  uint32_t bu = 0, bp = 0;
+  for (uint32_t q = threadIdx.x; q < nb; q += kBlock) {
+    bu = max(bu, blockmax[2 * q]);
+    bp = max(bp, blockmax[2 * q + 1]);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    bu = max(bu, (uint32_t)__shfl_xor((int)bu, o));
+    bp = max(bp, (uint32_t)__shfl_xor((int)bp, o));
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    su[wv] = bu;
+    sp[wv] = bp;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    maxbits[0] = max(max(su[0], su[1]), max(su[2], su[3]));
+    maxbits[1] = max(max(sp[0], sp[1]), max(sp[2], sp[3]));
   }
 }
 
@@ -379,20 +427,15 @@ __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict_
 
 __global__ void __launch_bounds__(kBlock) k_reduce_final(const float* __restrict__ partial,
                                                          uint32_t np, int mode, float* out,
-                                                         float* H, int hidx) {
+                                                         float* inv, float* g0) {
   __shared__ float lds[kBlock];
   const float s = block_final(partial, np, lds);
   if (threadIdx.x == 0) {
-    if (mode == 0) {
-      out[0] = s;
-    } else {
-      const float nrm = sqrtf(s);
-      out[0] = nrm;
-      if (mode == 2) out[1] = 1.0f / nrm;
-      if (mode == 3) {
-        H[hidx] = nrm;
-        out[1] = nrm > 1e-20f ? 1.0f / nrm : 0.0f;
-      }
+    const float nrm = sqrtf(s);
+    out[0] = nrm;
+    if (mode == 2) {
+      inv[0] = 1.0f / nrm;  // host-side `1.0 / residual_norm` (coupled_solver_fgmres.rs:1872)
+      if (g0) g0[0] = nrm;
     }
   }
 }
@@ -405,26 +448,20 @@ __global__ void __launch_bounds__(kBlock) k_residual_axpby(const float* __restri
   if (e < n) v0[e] = 1.0f * b[e] + -1.0f * w[e];
 }
 
-// scale (gmres_ops.wgsl:120-129): y = alpha * x, alpha from device scalar
-__global__ void __launch_bounds__(kBlock) k_scale(const float* __restrict__ x, float* y,
-                                                  const float* alpha, size_t n) {
-  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e < n) y[e] = alpha[0] * x[e];
-}
-
 struct BlockCoeffs {
   float uu, up, vp, pu, pv, pp;
 };
 __device__ __forceinline__ BlockCoeffs load_block(const CoupledMatrix& A, uint32_t r, uint32_t dr,
                                                   size_t slot, float2 d2) {
-  const float4 b = A.cval[slot];
+  const float2 a = A.cval_a[slot];
+  const float2 g = A.cval_g[slot];
   BlockCoeffs k;
-  k.uu = b.x;
-  k.up = b.y;
-  k.vp = b.z;
-  k.pp = b.w;
-  k.pu = (r == dr) ? d2.x : b.y;
-  k.pv = (r == dr) ? d2.y : b.z;
+  k.uu = a.x;
+  k.pp = a.y;
+  k.up = g.x;
+  k.vp = g.y;
+  k.pu = (r == dr) ? d2.x : g.x;
+  k.pv = (r == dr) ? d2.y : g.y;
   return k;
 }
 
@@ -432,7 +469,7 @@ __device__ __forceinline__ BlockCoeffs load_block(const CoupledMatrix& A, uint32
 // rows; per-row term order identical to the CSR row (neighbour-major, u,v,p).
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t N = A.N;
   if (i >= N) return;
   const uint32_t len = A.len[i], dr = A.drank[i];
@@ -458,11 +495,12 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   y[3 * (size_t)i + 2] = sp;
 }
 
-// calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j
+// calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j,
+// V_ii = binv[ii] * W_ii
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
                                                      const float* __restrict__ basis,
-                                                     size_t stride, int j, uint32_t N,
-                                                     float* partial, uint32_t np) {
+                                                     const float* __restrict__ binv, size_t stride,
+                                                     int j, uint32_t N, float* partial, uint32_t np) {
   __shared__ float lds[kBlock];
   const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
   float wv[kRedCellsPerThread][3];
@@ -476,13 +514,17 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
   }
   for (int ii = 0; ii <= j; ++ii) {
     const float* v = basis + (size_t)ii * stride;
+    const float sc = binv[ii];
     float acc = 0.0f;
 #pragma unroll
     for (int q = 0; q < kRedCellsPerThread; ++q) {
       const size_t c = base + (size_t)kBlock * q;
       if (ok[q]) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) acc += wv[q][s] * v[3 * c + s];
+        for (int s = 0; s < 3; ++s) {
+          const float vv = sc * v[3 * c + s];
+          acc += wv[q][s] * vv;
+        }
       }
     }
     const float r = block_tree(acc, lds);
@@ -500,15 +542,20 @@ __global__ void __launch_bounds__(kBlock) k_cgs_reduce(const float* __restrict__
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
 }
 
-// update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 chunk partial
-__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w,
-                                                            const float* __restrict__ basis,
+// update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 chunk partial; the
+// updated w is written straight into basis slot j+1 (unnormalised, see binv).
+__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
+                                                            float* basis,
+                                                            const float* __restrict__ binv,
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
                                                             uint32_t N, float* partial) {
   __shared__ float lds[kBlock];
-  __shared__ float hcol[64];
-  if (threadIdx.x <= (unsigned)j) hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
+  __shared__ float hcol[64], scol[64];
+  if (threadIdx.x <= (unsigned)j) {
+    hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
+    scol[threadIdx.x] = binv[threadIdx.x];
+  }
   __syncthreads();
   const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
   float corr[kRedCellsPerThread][3];
@@ -517,17 +564,21 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w,
 #pragma unroll
     for (int s = 0; s < 3; ++s) corr[q][s] = 0.0f;
   for (int ii = 0; ii <= j; ++ii) {
-    const float h = hcol[ii];
+    const float h = hcol[ii], sc = scol[ii];
     const float* v = basis + (size_t)ii * stride;
 #pragma unroll
     for (int q = 0; q < kRedCellsPerThread; ++q) {
       const size_t c = base + (size_t)kBlock * q;
       if (c < N) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) corr[q][s] += h * v[3 * c + s];
+        for (int s = 0; s < 3; ++s) {
+          const float vv = sc * v[3 * c + s];
+          corr[q][s] += h * vv;
+        }
       }
     }
   }
+  float* out = basis + (size_t)(j + 1) * stride;
   float acc = 0.0f;
 #pragma unroll
   for (int q = 0; q < kRedCellsPerThread; ++q) {
@@ -536,7 +587,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w,
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
         const float wn = w[3 * c + s] - corr[q][s];
-        w[3 * c + s] = wn;
+        out[3 * c + s] = wn;
         acc += wn * wn;
       }
     }
@@ -549,15 +600,14 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w,
 // (gmres_logic.wgsl:24-76).  scal[3] = ||w||, scal[4] = 1/||w||, scal[5] = |g[j+1]|.
 __global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict__ partial,
                                                         uint32_t np, int j, float* H, int m1,
-                                                        float* givens, float* g, float* scal,
+                                                        float* givens, float* g, float* binv,
                                                         float* resid_hist) {
   __shared__ float lds[kBlock];
   const float s = block_final(partial, np, lds);
   if (threadIdx.x != 0) return;
   const float norm = sqrtf(s);
   H[(size_t)j * m1 + j + 1] = norm;
-  scal[3] = norm;
-  scal[4] = norm > 1e-20f ? 1.0f / norm : 0.0f;
+  binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
   float* Hc = H + (size_t)j * m1;
   for (int ii = 0; ii < j; ++ii) {
     const float hij = Hc[ii], hi1j = Hc[ii + 1];
@@ -579,38 +629,39 @@ __global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict_
   const float gj = g[j], gj1 = g[j + 1];
   g[j] = cc * gj + ss * gj1;
   g[j + 1] = -ss * gj + cc * gj1;
-  const float res = fabsf(g[j + 1]);
-  scal[5] = res;
-  resid_hist[j] = res;
+  resid_hist[j] = fabsf(g[j + 1]);
 }
 
-// predict_and_form_schur (schur_precond.wgsl:142-188)
+// predict_and_form_schur (schur_precond.wgsl:142-188).  z_u, z_v of the
+// prediction are recomputed by k_precond_correct (same two multiplies), so this
+// kernel writes only the Schur rhs and the first Jacobi iterate.  The term
+// `A_pp * 0.0` of the reference loop is dropped: it can only flip the sign of a
+// zero rhs_p, and its A_pp read is the largest byte cost of the row.
 __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
-                                                            const float* __restrict__ r_in,
+                                                            const float* __restrict__ w_in,
+                                                            const float* __restrict__ binv, int jv,
                                                             const float* __restrict__ dinv_uv,
                                                             const float* __restrict__ dinv_p,
-                                                            float* z, float* temp_p, float* p_sol,
+                                                            float* temp_p, float* p_sol,
                                                             float* p_prev) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t N = A.N;
   if (i >= N) return;
-  const float du = dinv_uv[i];
-  z[3 * (size_t)i] = du * r_in[3 * (size_t)i];
-  z[3 * (size_t)i + 1] = du * r_in[3 * (size_t)i + 1];
-  z[3 * (size_t)i + 2] = 0.0f;
-  float rhs_p = r_in[3 * (size_t)i + 2];
+  const float sc = binv[jv];
+  float rhs_p = sc * w_in[3 * (size_t)i + 2];
   const uint32_t len = A.len[i], dr = A.drank[i];
   const float2 d2 = A.cdiag2[i];
   for (uint32_t r = 0; r < len; ++r) {
     const size_t slot = (size_t)r * N + i;
     const uint32_t j = A.col[slot];
-    const BlockCoeffs k = load_block(A, r, dr, slot, d2);
+    const float2 g = A.cval_g[slot];
+    const float pu = (r == dr) ? d2.x : g.x, pv = (r == dr) ? d2.y : g.y;
     const float dj = dinv_uv[j];
-    const float zu = r_in[3 * (size_t)j] * dj;
-    const float zv = r_in[3 * (size_t)j + 1] * dj;
-    rhs_p -= k.pu * zu;
-    rhs_p -= k.pv * zv;
-    rhs_p -= k.pp * 0.0f;
+    const float ru = sc * w_in[3 * (size_t)j], rv = sc * w_in[3 * (size_t)j + 1];
+    const float zu = ru * dj;
+    const float zv = rv * dj;
+    rhs_p -= pu * zu;
+    rhs_p -= pv * zv;
   }
   temp_p[i] = rhs_p;
   p_sol[i] = dinv_p[i] * rhs_p;
@@ -625,7 +676,7 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const uin
                                                            const float* __restrict__ temp_p,
                                                            const float* __restrict__ p_sol,
                                                            float* p_prev) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   if (i >= N) return;
   float sigma = 0.0f;
   const uint32_t l = len[i];
@@ -638,12 +689,15 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const uin
   p_prev[i] = wmix(p_prev[i], hat_x, 1.2f);
 }
 
-// correct_velocity (schur_precond.wgsl:93-139)
+// correct_velocity (schur_precond.wgsl:93-139) fused with the velocity
+// prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol)
 __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
+                                                            const float* __restrict__ w_in,
+                                                            const float* __restrict__ binv, int jv,
                                                             const float* __restrict__ p_sol,
                                                             const float* __restrict__ dinv_uv,
-                                                            float* z) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+                                                            float* __restrict__ z) {
+  const uint32_t i = row_id();
   const uint32_t N = A.N;
   if (i >= N) return;
   const uint32_t len = A.len[i];
@@ -651,14 +705,17 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
   for (uint32_t r = 0; r < len; ++r) {
     const size_t slot = (size_t)r * N + i;
     const uint32_t j = A.col[slot];
-    const float4 b = A.cval[slot];
+    const float2 g = A.cval_g[slot];
     const float pj = p_sol[j];
-    cu += b.y * pj;
-    cv += b.z * pj;
+    cu += g.x * pj;
+    cv += g.y * pj;
   }
+  const float sc = binv[jv];
   const float du = dinv_uv[i];
-  z[3 * (size_t)i] = z[3 * (size_t)i] - du * cu;
-  z[3 * (size_t)i + 1] = z[3 * (size_t)i + 1] - du * cv;
+  const float ru = sc * w_in[3 * (size_t)i], rv = sc * w_in[3 * (size_t)i + 1];
+  const float zu = du * ru, zv = du * rv;
+  z[3 * (size_t)i] = zu - du * cu;
+  z[3 * (size_t)i + 1] = zv - du * cv;
   z[3 * (size_t)i + 2] = p_sol[i];
 }
 
@@ -690,7 +747,7 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t n = L.n;
   if (i >= n) return;
   const uint32_t len = L.len[i];
@@ -707,7 +764,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ r) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   const uint32_t n = L.n;
   if (i >= n) return;
   const uint32_t len = L.len[i], dr = L.drank[i];
@@ -723,20 +780,55 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
   r[i] = b[i] - ax;
 }
 
-// restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f]
+// restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
+// also clears the coarse solution (amg.rs:721-725 `clear`, fused)
 __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
-                                                         float* __restrict__ cb) {
-  const uint32_t I = blockIdx.x * kBlock + threadIdx.x;
+                                                         float* __restrict__ cb,
+                                                         float* __restrict__ cx) {
+  const uint32_t I = row_id();
   if (I >= L.nc) return;
   float sum = 0.0f;
   for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
   cb[I] = sum;
+  cx[I] = 0.0f;
+}
+
+// `sweeps` out-of-place Jacobi sweeps (smooth_op) of a small level (n <= 1024)
+// by one workgroup, x ping-ponged in LDS: the coarsest solve's 10 launches
+// (amg.rs:730-742) become one.
+__global__ void __launch_bounds__(1024) k_amg_coarse(AmgLevelDev L, float* x,
+                                                     const float* __restrict__ b, int sweeps) {
+  __shared__ float xs[2][1024];
+  const uint32_t i = threadIdx.x, n = L.n;
+  float bi = 0.0f, de = 1.0f;
+  uint32_t len = 0;
+  if (i < n) {
+    xs[0][i] = x[i];
+    bi = b[i];
+    de = L.de[i];
+    len = L.len[i];
+  }
+  __syncthreads();
+  for (int s = 0; s < sweeps; ++s) {
+    const int cur = s & 1;
+    if (i < n) {
+      float sigma = 0.0f;
+      for (uint32_t r = 0; r < len; ++r) {
+        const size_t slot = (size_t)r * n + i;
+        sigma += L.val[slot] * xs[cur][L.col[slot]];
+      }
+      const float x_new = (bi - sigma) / de;
+      xs[cur ^ 1][i] = wmix(xs[cur][i], x_new, 0.8f);
+    }
+    __syncthreads();
+  }
+  if (i < n) x[i] = xs[sweeps & 1][i];
 }
 
 // prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg])
 __global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* x,
                                                         const float* __restrict__ xc) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t i = row_id();
   if (i >= L.n) return;
   float corr = 0.0f;
   corr += 1.0f * xc[L.agg[i]];
@@ -853,49 +945,51 @@ void launch_assemble(const AssembleArgs& a, hipStream_t s) {
   if (a.N) hipLaunchKernelGGL(k_assemble, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
 }
 void launch_update_fields(uint32_t N, float au, float ap, const float* x, float2* u, float* p,
-                          uint32_t* maxbits, hipStream_t s) {
-  if (N) hipLaunchKernelGGL(k_update_fields, dim3(grid_for(N)), dim3(kBlock), 0, s, N, au, ap, x, u, p, maxbits);
+                          uint32_t* blockmax, uint32_t* maxbits, hipStream_t s) {
+  if (!N) return;
+  const unsigned nb = grid_for(N);
+  hipLaunchKernelGGL(k_update_fields, dim3(nb), dim3(kBlock), 0, s, N, au, ap, x, u, p, blockmax);
+  hipLaunchKernelGGL(k_maxdiff_final, dim3(1), dim3(kBlock), 0, s, blockmax, nb, maxbits);
 }
 void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s) {
   const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
   if (nb) hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, x, y, N, partial);
 }
-void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* H, int hidx,
+void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* inv, float* g0,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, partial, np, mode, out, H, hidx);
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, partial, np, mode, out, inv, g0);
 }
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
 }
-void launch_scale(const float* x, float* y, const float* alpha, size_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(kBlock), 0, s, x, y, alpha, n);
-}
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
   if (A.N) hipLaunchKernelGGL(k_spmv, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, x, y);
 }
-void launch_cgs_dots(const float* w, const float* basis, size_t stride, int j, uint32_t N,
+void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      float* partial, uint32_t np, hipStream_t s) {
-  if (np) hipLaunchKernelGGL(k_cgs_dots, dim3(np), dim3(kBlock), 0, s, w, basis, stride, j, N, partial, np);
+  if (np) hipLaunchKernelGGL(k_cgs_dots, dim3(np), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, partial, np);
 }
 void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kBlock), 0, s, partial, np, j, H, m1);
 }
-void launch_cgs_update_norm(float* w, const float* basis, size_t stride, int j, const float* H, int m1,
-                            uint32_t N, float* partial, hipStream_t s) {
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
+                            const float* H, int m1, uint32_t N, float* partial, hipStream_t s) {
   const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
-  if (nb) hipLaunchKernelGGL(k_cgs_update_norm, dim3(nb), dim3(kBlock), 0, s, w, basis, stride, j, H, m1, N, partial);
+  if (nb)
+    hipLaunchKernelGGL(k_cgs_update_norm, dim3(nb), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N,
+                       partial);
 }
 void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
-                        float* g, float* scal, float* resid_hist, hipStream_t s) {
-  hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kBlock), 0, s, partial, np, j, H, m1, givens, g, scal,
+                        float* g, float* binv, float* resid_hist, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kBlock), 0, s, partial, np, j, H, m1, givens, g, binv,
                      resid_hist);
 }
-void launch_precond_predict(const CoupledMatrix& A, const float* r_in, const float* dinv_uv,
-                            const float* dinv_p, float* z, float* temp_p, float* p_sol, float* p_prev,
-                            hipStream_t s) {
+void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
+                            const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
+                            float* p_prev, hipStream_t s) {
   if (A.N)
-    hipLaunchKernelGGL(k_precond_predict, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, r_in, dinv_uv,
-                       dinv_p, z, temp_p, p_sol, p_prev);
+    hipLaunchKernelGGL(k_precond_predict, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv,
+                       dinv_p, temp_p, p_sol, p_prev);
 }
 void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len, const float* sval,
                            const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
@@ -905,9 +999,11 @@ void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32
     hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, col, len, sval, dinv_p,
                        temp_p, p_sol, p_prev);
 }
-void launch_precond_correct(const CoupledMatrix& A, const float* p_sol, const float* dinv_uv, float* z,
-                            hipStream_t s) {
-  if (A.N) hipLaunchKernelGGL(k_precond_correct, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, p_sol, dinv_uv, z);
+void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
+                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
+  if (A.N)
+    hipLaunchKernelGGL(k_precond_correct, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol,
+                       dinv_uv, z);
 }
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(64), 0, s, H, g, y, k, m1);
@@ -922,8 +1018,11 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_residual, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, b, r);
 }
-void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, hipStream_t s) {
-  if (L.nc) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(L.nc)), dim3(kBlock), 0, s, L, r, cb);
+void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, hipStream_t s) {
+  if (L.nc) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(L.nc)), dim3(kBlock), 0, s, L, r, cb, cx);
+}
+void launch_amg_coarse(const AmgLevelDev& L, float* x, const float* b, int sweeps, hipStream_t s) {
+  if (L.n) hipLaunchKernelGGL(k_amg_coarse, dim3(1), dim3(1024), 0, s, L, x, b, sweeps);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, xc);

@@ -8,8 +8,12 @@
 //  * the coupled 3N x 3N matrix is stored as compressed 3x3 blocks: the
 //    reference CSR (init/linear_solver/mod.rs:180-216) always holds
 //    A_uu == A_vv, A_uv == A_vu == 0, A_up == A_pu, A_vp == A_pv per
-//    off-diagonal block (coupled_assembly_merged.wgsl:221-333), so one float4
-//    {c, gx, gy, pp} per block reproduces every CSR entry bit-for-bit.
+//    off-diagonal block (coupled_assembly_merged.wgsl:221-333), so two float2
+//    per block -- cval_a {c, pp} and cval_g {gx, gy} -- reproduce every CSR
+//    entry bit-for-bit.  The Schur predict/correct kernels read cval_g only.
+//  * Krylov basis vectors are stored unnormalised (W_i) with their scale
+//    binv[i]; every consumer forms V_i[e] = binv[i] * W_i[e] (one f32 multiply,
+//    the same rounding as the reference's `scale` pass, which is thereby gone).
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -82,8 +86,9 @@ struct AssembleArgs {
   const float2* grad_u;
   const float2* grad_v;
   const uint32_t* srank_diag;  // [N] diagonal rank in the scalar row
-  float4* cval;   // [r*N + i] compressed coupled blocks
-  float2* cdiag2; // [N] {s_pu, s_pv}
+  float2* cval_a; // [r*N + i] {A_uu (=A_vv), A_pp}
+  float2* cval_g; // [r*N + i] {A_up (=A_pu), A_vp (=A_pv)}
+  float2* cdiag2; // [N] {s_pu, s_pv} of the diagonal block
   float* sval;    // [r*N + i] scalar pressure matrix
   float* rhs;     // [3N]
   float* dinv_uv; // [N]
@@ -96,7 +101,8 @@ struct CoupledMatrix {
   const uint32_t* col;  // [r*N + i]
   const uint32_t* len;  // [N]
   const uint32_t* drank;  // [N]
-  const float4* cval;
+  const float2* cval_a;
+  const float2* cval_g;
   const float2* cdiag2;
 };
 
@@ -119,32 +125,35 @@ struct AmgLevelDev {
 // ---------------- launch wrappers (kernels.hip) ----------------
 void launch_prepare(const PrepareArgs& a, hipStream_t s);
 void launch_assemble(const AssembleArgs& a, hipStream_t s);
+// writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
-                          float* p, uint32_t* maxbits, hipStream_t s);
+                          float* p, uint32_t* blockmax, uint32_t* maxbits, hipStream_t s);
 void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s);
-// mode 0: out[0] = sum; 1: out[0] = sqrt(sum); 2: out[0] = sqrt, out[1] = 1/sqrt (host-style
-// 1.0f/norm); 3: w-norm: out[0]=sqrt, H[hidx]=sqrt, out[1] = norm>1e-20 ? 1/norm : 0
-void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* H,
-                         int hidx, hipStream_t s);
+// mode 1: out[0] = sqrt(sum); mode 2: out[0] = sqrt, *inv = 1.0f / sqrt (host-style)
+// and g0 (if non-null) = sqrt
+void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* inv,
+                         float* g0, hipStream_t s);
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
-void launch_scale(const float* x, float* y, const float* alpha, size_t n, hipStream_t s);
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
-void launch_cgs_dots(const float* w, const float* basis, size_t stride, int j, uint32_t N,
-                     float* partial, uint32_t np, hipStream_t s);
+// basis: unnormalised W_i at basis + i*stride, scales binv[i]
+void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
+                     uint32_t N, float* partial, uint32_t np, hipStream_t s);
 void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s);
-void launch_cgs_update_norm(float* w, const float* basis, size_t stride, int j, const float* H,
-                            int m1, uint32_t N, float* partial, hipStream_t s);
-// ||w|| final + Givens update of column j; resid -> out_resid (device)
+// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 partials
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
+                            const float* H, int m1, uint32_t N, float* partial, hipStream_t s);
+// ||W_{j+1}|| final -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|
 void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
-                        float* g, float* scal, float* resid_hist, hipStream_t s);
-void launch_precond_predict(const CoupledMatrix& A, const float* r_in, const float* dinv_uv,
-                            const float* dinv_p, float* z, float* temp_p, float* p_sol,
+                        float* g, float* binv, float* resid_hist, hipStream_t s);
+// r_in = binv[j] * W_j
+void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
+                            const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s);
 void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
-void launch_precond_correct(const CoupledMatrix& A, const float* p_sol, const float* dinv_uv,
-                            float* z, hipStream_t s);
+void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
+                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s);
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,
                              hipStream_t s);
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
@@ -153,7 +162,11 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
                        hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,
                          hipStream_t s);
-void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, hipStream_t s);
+// coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused)
+void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
+                         hipStream_t s);
+// `sweeps` smoother sweeps of a level with n <= 1024 rows in one workgroup (LDS ping-pong)
+void launch_amg_coarse(const AmgLevelDev& L, float* x, const float* b, int sweeps, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
 void launch_fill(float* x, float v, size_t n, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:

@@ -77,8 +77,10 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev) : cfg(c)
   grad_v = arena.alloc<float2>(Nz);
   CFD_HIP(hipMemsetAsync(grad_u, 0, Nz * sizeof(float2), stream));
   CFD_HIP(hipMemsetAsync(grad_v, 0, Nz * sizeof(float2), stream));
-  cval = arena.alloc<float4>(slots_s);
-  CFD_HIP(hipMemsetAsync(cval, 0, slots_s * sizeof(float4), stream));
+  cval_a = arena.alloc<float2>(slots_s);
+  cval_g = arena.alloc<float2>(slots_s);
+  CFD_HIP(hipMemsetAsync(cval_a, 0, slots_s * sizeof(float2), stream));
+  CFD_HIP(hipMemsetAsync(cval_g, 0, slots_s * sizeof(float2), stream));
   cdiag2 = arena.alloc<float2>(Nz);
   CFD_HIP(hipMemsetAsync(cdiag2, 0, Nz * sizeof(float2), stream));
   sval = arena.alloc<float>(slots_s);
@@ -93,6 +95,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev) : cfg(c)
   CFD_HIP(hipMemsetAsync(dinv_p, 0, Nz * sizeof(float), stream));
   partial_d = arena.alloc<double>(5 * (size_t)nchunks + 5);
   maxbits = arena.alloc<uint32_t>(4);
+  blockmax = arena.alloc<uint32_t>(2 * (((size_t)N + 255) / 256) + 2);
   CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float), hipHostMallocDefault));
   for (auto& e : ev_outer) CFD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // constants (init/fields.rs:100-115)
@@ -132,7 +135,8 @@ CoupledMatrix Solver::cmat() const {
   A.col = d_scol;
   A.len = d_slen;
   A.drank = d_sdrank;
-  A.cval = cval;
+  A.cval_a = cval_a;
+  A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
   return A;
 }
@@ -237,7 +241,8 @@ void Solver::assemble() {
   a.grad_u = grad_u;
   a.grad_v = grad_v;
   a.srank_diag = d_sdrank;
-  a.cval = cval;
+  a.cval_a = cval_a;
+  a.cval_g = cval_g;
   a.cdiag2 = cdiag2;
   a.sval = sval;
   a.rhs = rhs;
@@ -264,7 +269,7 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   CFD_HIP(hipMemsetAsync(p_sol, 0, N * sizeof(float), stream));
   partial = arena.alloc<float>((size_t)m1 * nchunks);
   partial_n = arena.alloc<float>(nchunks);
-  const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m;
+  const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
   dsc = arena.alloc<float>(nsc);
   CFD_HIP(hipMemsetAsync(dsc, 0, nsc * sizeof(float), stream));
   H = dsc + kHOff;
@@ -272,6 +277,7 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   g = givens + 2 * m;
   y = g + m1;
   resid_hist = y + m;
+  binv = resid_hist + m;
   ev_iter.resize(m);
   for (auto& e : ev_iter) CFD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   fgmres_ready = true;
@@ -399,10 +405,12 @@ void Solver::v_cycle() {
   for (size_t i = 0; i + 1 < L; ++i) {
     amg_smooth(i, levels[i].x, levels[i].b);
     launch_amg_residual(levels[i].dev, levels[i].x, levels[i].b, levels[i].r, stream);
-    launch_amg_restrict(levels[i].dev, levels[i].r, levels[i + 1].b, stream);
-    launch_fill(levels[i + 1].x, 0.0f, levels[i + 1].dev.n, stream);
+    launch_amg_restrict(levels[i].dev, levels[i].r, levels[i + 1].b, levels[i + 1].x, stream);
   }
-  for (int s = 0; s < 10; ++s) amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
+  if (L > 1 && levels[L - 1].dev.n <= 1024 && !(prof && L == 1))
+    launch_amg_coarse(levels[L - 1].dev, levels[L - 1].x, levels[L - 1].b, 10, stream);
+  else
+    for (int s = 0; s < 10; ++s) amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
   for (size_t ii = L - 1; ii-- > 0;) {
     launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
     amg_smooth(ii, levels[ii].x, levels[ii].b);
@@ -412,10 +420,11 @@ void Solver::v_cycle() {
 }
 
 // FGMRES Preconditioner Step (coupled_solver_fgmres.rs:1911-1994)
-void Solver::precondition(const float* v, float* z) {
+void Solver::precondition(int j, float* z) {
   const CoupledMatrix A = cmat();
   const bool jacobi = constants.precond_type != 1;
-  launch_precond_predict(A, v, dinv_uv, dinv_p, z, temp_p, p_sol, jacobi ? temp : nullptr, stream);
+  const float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
+  launch_precond_predict(A, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
   bool in_sol = true;
   if (!jacobi) {
     v_cycle();
@@ -430,22 +439,25 @@ void Solver::precondition(const float* v, float* z) {
       in_sol = !in_sol;
     }
   }
-  launch_precond_correct(A, in_sol ? p_sol : temp, dinv_uv, z, stream);
+  launch_precond_correct(A, v, binv, j, in_sol ? p_sol : temp, dinv_uv, z, stream);
 }
 
 float Solver::norm_blocking(const float* v, int mode, int slot) {
   launch_dot_partial(v, v, N, partial_n, stream);
-  launch_reduce_final(partial_n, nchunks, mode, dsc + slot, nullptr, 0, stream);
-  CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, 2 * sizeof(float), hipMemcpyDeviceToHost, stream));
+  launch_reduce_final(partial_n, nchunks, mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
+  CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   return h_pin[0];
 }
 
 // compute_residual_into (coupled_solver_fgmres.rs:1637-1667): V0 = b - A x, ||V0||
+// V0 is stored unnormalised: binv[0] = 1/||r|| (the reference's scale_in_place),
+// g = [||r||, 0, ...] (coupled_solver_fgmres.rs:1880-1890, 2380-2392).
 float Solver::residual_into_v0_blocking() {
+  CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
   launch_spmv(cmat(), x, w, stream);
   launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
-  return norm_blocking(basis, 2, 1);  // dsc[1] = norm, dsc[2] = 1/norm
+  return norm_blocking(basis, 2, 1);
 }
 
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
@@ -470,9 +482,6 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     st.converged = 1;
     return st;
   }
-  launch_scale(basis, basis, dsc + 2, n, stream);  // V0 *= 1/||r|| (host-style 1.0/norm)
-  CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
-  CFD_HIP(hipMemcpyAsync(g, dsc + 1, sizeof(float), hipMemcpyDeviceToDevice, stream));
   uint32_t total = 0;
   float final_resid = residual_norm;
   bool converged = false;
@@ -485,15 +494,13 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     for (int j = 0; j < inner_max; ++j) {
       basis_size = j + 1;
       ++total;
-      float* vj = basis + (size_t)j * stride;
       float* zj = zvec + (size_t)j * stride;
-      precondition(vj, zj);
+      precondition(j, zj);
       launch_spmv(cmat(), zj, w, stream);
-      launch_cgs_dots(w, basis, stride, j, N, partial, nchunks, stream);
+      launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);
       launch_cgs_reduce(partial, nchunks, j, H, m1, stream);
-      launch_cgs_update_norm(w, basis, stride, j, H, m1, N, partial_n, stream);
-      launch_norm_givens(partial_n, nchunks, j, H, m1, givens, g, dsc, resid_hist, stream);
-      launch_scale(w, basis + (size_t)(j + 1) * stride, dsc + 4, n, stream);
+      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
+      launch_norm_givens(partial_n, nchunks, j, H, m1, givens, g, binv, resid_hist, stream);
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
       if (inner.pending >= 0) {
@@ -544,13 +551,10 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       converged = true;
       break;
     }
-    CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
-    CFD_HIP(hipMemcpyAsync(g, dsc + 1, sizeof(float), hipMemcpyDeviceToDevice, stream));
     if (residual_norm <= 0.0f) {
       converged = true;
       break;
     }
-    launch_scale(basis, basis, dsc + 2, n, stream);
     const float improvement = (prev_resid - residual_norm) / prev_resid;
     if (improvement < 1e-3f) {
       if (++stagnation >= 3) {
@@ -620,8 +624,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
     info.stats_p = ls;
     info.total_linear_iterations += ls.iterations;
     if (std::isnan(ls.residual)) throw std::domain_error("Coupled Linear Solver Diverged: NaN detected in linear residual");
-    CFD_HIP(hipMemsetAsync(maxbits, 0, 2 * sizeof(uint32_t), stream));
-    launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, maxbits, stream);
+    launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, blockmax, maxbits, stream);
     if (iter == 0) {
       info.outer_residual_u = std::numeric_limits<float>::max();
       info.outer_residual_p = std::numeric_limits<float>::max();
@@ -725,25 +728,26 @@ void Solver::debug_buffer(int id, float* out) {
       break;
     }
     case 9: {  // expand compressed blocks to the reference CSR (init/linear_solver/mod.rs:180-216)
-      std::vector<float4> cv((size_t)topo.ws * n);
+      std::vector<float2> ca((size_t)topo.ws * n), cg((size_t)topo.ws * n);
       std::vector<float2> d2(n);
-      d2h(cv.data(), cval, cv.size() * sizeof(float4));
+      d2h(ca.data(), cval_a, ca.size() * sizeof(float2));
+      d2h(cg.data(), cval_g, cg.size() * sizeof(float2));
       d2h(d2.data(), cdiag2, n * sizeof(float2));
       for (uint32_t i = 0; i < N; ++i) {
         const uint32_t so = topo.srow[i], nb = topo.srow[i + 1] - so;
         const uint32_t r0 = 9 * so, r1 = r0 + 3 * nb, r2 = r0 + 6 * nb;
         for (uint32_t r = 0; r < nb; ++r) {
-          const float4 b = cv[(size_t)r * n + i];
+          const float2 a = ca[(size_t)r * n + i], gg = cg[(size_t)r * n + i];
           const bool diag = (r == topo.ell_drank[i]);
-          out[r0 + 3 * r + 0] = b.x;
+          out[r0 + 3 * r + 0] = a.x;
           out[r0 + 3 * r + 1] = 0.0f;
-          out[r0 + 3 * r + 2] = b.y;
+          out[r0 + 3 * r + 2] = gg.x;
           out[r1 + 3 * r + 0] = 0.0f;
-          out[r1 + 3 * r + 1] = b.x;
-          out[r1 + 3 * r + 2] = b.z;
-          out[r2 + 3 * r + 0] = diag ? d2[i].x : b.y;
-          out[r2 + 3 * r + 1] = diag ? d2[i].y : b.z;
-          out[r2 + 3 * r + 2] = b.w;
+          out[r1 + 3 * r + 1] = a.x;
+          out[r1 + 3 * r + 2] = gg.y;
+          out[r2 + 3 * r + 0] = diag ? d2[i].x : gg.x;
+          out[r2 + 3 * r + 1] = diag ? d2[i].y : gg.y;
+          out[r2 + 3 * r + 2] = a.y;
         }
       }
       break;

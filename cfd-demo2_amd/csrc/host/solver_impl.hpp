@@ -136,7 +136,8 @@ struct Solver {
   float* flux_s = nullptr;
   float2* grad_u = nullptr;
   float2* grad_v = nullptr;
-  float4* cval = nullptr;
+  float2* cval_a = nullptr;
+  float2* cval_g = nullptr;
   float2* cdiag2 = nullptr;
   float* sval = nullptr;
   float* rhs = nullptr;
@@ -161,7 +162,9 @@ struct Solver {
   float* g = nullptr;
   float* y = nullptr;
   float* resid_hist = nullptr;
+  float* binv = nullptr;         // [m+1] scales of the unnormalised basis vectors
   uint32_t* maxbits = nullptr;
+  uint32_t* blockmax = nullptr;  // [2 * ceil(N/256)]
   float* h_pin = nullptr;        // pinned host scalars
   std::vector<hipEvent_t> ev_iter;
   hipEvent_t ev_outer[2]{};
@@ -204,7 +207,7 @@ struct Solver {
   cfd_linear_stats solve();
   void ensure_fgmres();
   void ensure_amg();
-  void precondition(const float* v, float* z);
+  void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b);
   float norm_blocking(const float* v, int mode, int slot);
