@@ -743,41 +743,98 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
 }
 
 // ------------------------------- AMG ---------------------------------------
+// Each thread owns 4 consecutive rows: b, x, de and every ELL slot are one
+// 16-byte load per thread (coalesced 1 KiB per wavefront), column deltas are
+// 8 bytes per slot, lengths 4 bytes; only the x gathers are scalar.
+template <bool D16>
+__device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uint32_t i0,
+                                           uint32_t c[4]) {
+  if constexpr (D16) {
+    const short4 d = *reinterpret_cast<const short4*>(L.col16 + off);
+    c[0] = i0 + (int)d.x;
+    c[1] = i0 + 1 + (int)d.y;
+    c[2] = i0 + 2 + (int)d.z;
+    c[3] = i0 + 3 + (int)d.w;
+  } else {
+    const uint4 q = *reinterpret_cast<const uint4*>(L.col32 + off);
+    c[0] = q.x;
+    c[1] = q.y;
+    c[2] = q.z;
+    c[3] = q.w;
+  }
+}
+
+__device__ __forceinline__ float f4(const float4& v, int k) {
+  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ uint32_t u4(const uchar4& v, int k) {
+  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
-  const uint32_t i = row_id();
-  const uint32_t n = L.n;
-  if (i >= n) return;
-  const uint32_t len = L.len[i];
-  float sigma = 0.0f;
-  for (uint32_t r = 0; r < len; ++r) {
-    const size_t slot = (size_t)r * n + i;
-    sigma += L.val[slot] * x[L.col[slot]];
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= L.n) return;
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t r = 0; r < maxlen; ++r) {
+    const size_t off = (size_t)r * L.stride + i0;
+    const float4 v = *reinterpret_cast<const float4*>(L.val + off);
+    uint32_t c[4];
+    load_cols4<D16>(L, off, i0, c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r < u4(ln, k)) sg[k] += f4(v, k) * x[c[k]];
   }
-  const float x_new = (b[i] - sigma) / L.de[i];
-  x_out[i] = wmix(x[i], x_new, 0.8f);
+  float4 o;
+  o.x = wmix(xx.x, (bb.x - sg[0]) / dd.x, 0.8f);
+  o.y = wmix(xx.y, (bb.y - sg[1]) / dd.y, 0.8f);
+  o.z = wmix(xx.z, (bb.z - sg[2]) / dd.z, 0.8f);
+  o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
+  *reinterpret_cast<float4*>(x_out + i0) = o;
 }
 
-// residual part of restrict_residual (amg.wgsl:80-111): r = b - A x (full row, column order)
+// residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
+// row in column order, the diagonal inserted at its rank.
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
-                                                         float* __restrict__ r) {
-  const uint32_t i = row_id();
-  const uint32_t n = L.n;
-  if (i >= n) return;
-  const uint32_t len = L.len[i], dr = L.drank[i];
-  const float dv = L.dv[i];
-  const float xi = x[i];
-  float ax = 0.0f;
-  for (uint32_t k = 0; k < len; ++k) {
-    if (k == dr) ax += dv * xi;
-    const size_t slot = (size_t)k * n + i;
-    ax += L.val[slot] * x[L.col[slot]];
+                                                         float* __restrict__ rr) {
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= L.n) return;
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
+  const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t r = 0; r <= maxlen; ++r) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r == u4(dr, k)) ax[k] += f4(dv, k) * f4(xx, k);
+    if (r == maxlen) break;
+    const size_t off = (size_t)r * L.stride + i0;
+    const float4 v = *reinterpret_cast<const float4*>(L.val + off);
+    uint32_t c[4];
+    load_cols4<D16>(L, off, i0, c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (r < u4(ln, k)) ax[k] += f4(v, k) * x[c[k]];
   }
-  if (dr == len) ax += dv * xi;
-  r[i] = b[i] - ax;
+  float4 o;
+  o.x = bb.x - ax[0];
+  o.y = bb.y - ax[1];
+  o.z = bb.z - ax[2];
+  o.w = bb.w - ax[3];
+  *reinterpret_cast<float4*>(rr + i0) = o;
 }
 
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
@@ -793,46 +850,97 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
   cx[I] = 0.0f;
 }
 
-// `sweeps` out-of-place Jacobi sweeps (smooth_op) of a small level (n <= 1024)
-// by one workgroup, x ping-ponged in LDS: the coarsest solve's 10 launches
-// (amg.rs:730-742) become one.
-__global__ void __launch_bounds__(1024) k_amg_coarse(AmgLevelDev L, float* x,
-                                                     const float* __restrict__ b, int sweeps) {
-  __shared__ float xs[2][1024];
-  const uint32_t i = threadIdx.x, n = L.n;
-  float bi = 0.0f, de = 1.0f;
-  uint32_t len = 0;
-  if (i < n) {
-    xs[0][i] = x[i];
-    bi = b[i];
-    de = L.de[i];
-    len = L.len[i];
+// prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread
+__global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* __restrict__ x,
+                                                        const float* __restrict__ xc) {
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= L.n) return;
+  float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const uint4 ag = *reinterpret_cast<const uint4*>(L.agg + i0);
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;  // padding rows (>= n) get 0
+  c0 += 1.0f * xc[ag.x];
+  if (i0 + 1 < L.n) c1 += 1.0f * xc[ag.y];
+  if (i0 + 2 < L.n) c2 += 1.0f * xc[ag.z];
+  if (i0 + 3 < L.n) c3 += 1.0f * xc[ag.w];
+  xx.x += c0;
+  xx.y += c1;
+  xx.z += c2;
+  xx.w += c3;
+  *reinterpret_cast<float4*>(x + i0) = xx;
+}
+
+// ---- single-row helpers for the one-workgroup kernels (small levels) ----
+__device__ __forceinline__ uint32_t col_at(const AmgLevelDev& L, size_t off, uint32_t i) {
+  return L.use16 ? (uint32_t)((int)i + (int)L.col16[off]) : L.col32[off];
+}
+__device__ __forceinline__ float smooth_row(const AmgLevelDev& L, const float* x, const float* b,
+                                            uint32_t i) {
+  float sigma = 0.0f;
+  const uint32_t len = L.len[i];
+  for (uint32_t r = 0; r < len; ++r) {
+    const size_t off = (size_t)r * L.stride + i;
+    sigma += L.val[off] * x[col_at(L, off, i)];
   }
-  __syncthreads();
-  for (int s = 0; s < sweeps; ++s) {
-    const int cur = s & 1;
-    if (i < n) {
-      float sigma = 0.0f;
-      for (uint32_t r = 0; r < len; ++r) {
-        const size_t slot = (size_t)r * n + i;
-        sigma += L.val[slot] * xs[cur][L.col[slot]];
-      }
-      const float x_new = (bi - sigma) / de;
-      xs[cur ^ 1][i] = wmix(xs[cur][i], x_new, 0.8f);
+  return wmix(x[i], (b[i] - sigma) / L.de[i], 0.8f);
+}
+__device__ __forceinline__ float residual_row(const AmgLevelDev& L, const float* x, const float* b,
+                                              uint32_t i) {
+  const uint32_t len = L.len[i], dr = L.drank[i];
+  float ax = 0.0f;
+  for (uint32_t r = 0; r <= len; ++r) {
+    if (r == dr) ax += L.dv[i] * x[i];
+    if (r == len) break;
+    const size_t off = (size_t)r * L.stride + i;
+    ax += L.val[off] * x[col_at(L, off, i)];
+  }
+  return b[i] - ax;
+}
+
+// One workgroup runs the V-cycle over the small levels [first, nlev): every
+// phase of amg.rs:666-770 with a workgroup barrier instead of a kernel boundary.
+// Each level does an even number of out-of-place sweeps, so the pre-smoother
+// goes x -> xt, the post-smoother xt -> x and the coarsest solve ends in x,
+// exactly the host-side ping-pong of Solver::amg_smooth.
+__global__ void __launch_bounds__(1024) k_amg_tail(const AmgTailLevel* __restrict__ tail, int first,
+                                                   int nlev) {
+  const uint32_t t = threadIdx.x, nt = blockDim.x;
+  for (int l = first; l + 1 < nlev; ++l) {
+    const AmgTailLevel T = tail[l];
+    for (uint32_t i = t; i < T.L.n; i += nt) T.xt[i] = smooth_row(T.L, T.x, T.b, i);
+    __syncthreads();
+    for (uint32_t i = t; i < T.L.n; i += nt) T.r[i] = residual_row(T.L, T.xt, T.b, i);
+    __syncthreads();
+    float* cb = tail[l + 1].b;
+    float* cx = tail[l + 1].x;
+    for (uint32_t I = t; I < T.L.nc; I += nt) {
+      float sum = 0.0f;
+      for (uint32_t k = T.L.r_row[I]; k < T.L.r_row[I + 1]; ++k) sum += 1.0f * T.r[T.L.r_col[k]];
+      cb[I] = sum;
+      cx[I] = 0.0f;
     }
     __syncthreads();
   }
-  if (i < n) x[i] = xs[sweeps & 1][i];
-}
-
-// prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg])
-__global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* x,
-                                                        const float* __restrict__ xc) {
-  const uint32_t i = row_id();
-  if (i >= L.n) return;
-  float corr = 0.0f;
-  corr += 1.0f * xc[L.agg[i]];
-  x[i] += corr;
+  {
+    const AmgTailLevel T = tail[nlev - 1];
+    for (int s = 0; s < 10; ++s) {
+      const float* xin = (s & 1) ? T.xt : T.x;
+      float* xout = (s & 1) ? T.x : T.xt;
+      for (uint32_t i = t; i < T.L.n; i += nt) xout[i] = smooth_row(T.L, xin, T.b, i);
+      __syncthreads();
+    }
+  }
+  for (int l = nlev - 2; l >= first; --l) {
+    const AmgTailLevel T = tail[l];
+    const float* xc = tail[l + 1].x;
+    for (uint32_t i = t; i < T.L.n; i += nt) {
+      float corr = 0.0f;
+      corr += 1.0f * xc[T.L.agg[i]];
+      T.xt[i] += corr;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < T.L.n; i += nt) T.x[i] = smooth_row(T.L, T.xt, T.b, i);
+    __syncthreads();
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_fill(float* x, float v, size_t n) {
@@ -1013,19 +1121,29 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for(n)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s) {
-  if (L.n) hipLaunchKernelGGL(k_amg_smooth, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, b, x_out);
+  if (!L.n) return;
+  const unsigned nb = grid_for((L.n + 3) / 4);
+  if (L.use16)
+    hipLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
+  else
+    hipLaunchKernelGGL(k_amg_smooth<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
 }
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
-  if (L.n) hipLaunchKernelGGL(k_amg_residual, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, b, r);
+  if (!L.n) return;
+  const unsigned nb = grid_for((L.n + 3) / 4);
+  if (L.use16)
+    hipLaunchKernelGGL(k_amg_residual<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
+  else
+    hipLaunchKernelGGL(k_amg_residual<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, hipStream_t s) {
   if (L.nc) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(L.nc)), dim3(kBlock), 0, s, L, r, cb, cx);
 }
-void launch_amg_coarse(const AmgLevelDev& L, float* x, const float* b, int sweeps, hipStream_t s) {
-  if (L.n) hipLaunchKernelGGL(k_amg_coarse, dim3(1), dim3(1024), 0, s, L, x, b, sweeps);
-}
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
-  if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for(L.n)), dim3(kBlock), 0, s, L, x, xc);
+  if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, x, xc);
+}
+void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, hipStream_t s) {
+  hipLaunchKernelGGL(k_amg_tail, dim3(1), dim3(1024), 0, s, tail, first, nlev);
 }
 void launch_fill(float* x, float v, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);

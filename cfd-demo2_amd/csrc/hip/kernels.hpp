@@ -106,21 +106,41 @@ struct CoupledMatrix {
   const float2* cdiag2;
 };
 
+// One AMG level (linear_solver/amg.rs AmgLevel) in the layout the gfx950
+// kernels stream: off-diagonal entries only, ELL slot-major with row stride
+// `stride` (= n rounded up to 64, so four consecutive rows of one slot are one
+// 16-byte load), columns as 16-bit deltas (col - row) when every delta of the
+// level fits, else 32-bit; per-row length and diagonal position as u8.
+// Off-diagonals keep the reference CSR order (ascending column), so every
+// row sum accumulates in the reference order.
 struct AmgLevelDev {
   uint32_t n;
-  int w;              // ELL width (off-diagonals only)
-  const uint32_t* col;  // [r*n + i]
-  const float* val;
-  const uint32_t* len;   // off-diagonal count per row
-  const uint32_t* drank; // position of the diagonal among the row's entries
-  const float* dv;       // raw diagonal (0 if absent)
-  const float* de;       // effective smoother diagonal
-  // coarsening operators (only when has_op)
+  uint32_t stride;       // row stride of the ELL slots (n rounded up to 64)
+  int w;                 // ELL width (max off-diagonals per row)
+  int use16;             // 1: col16 holds deltas; 0: col32 holds absolute columns
+  const float* val;      // [r*stride + i]
+  const int16_t* col16;  // [r*stride + i]  col - i
+  const uint32_t* col32; // [r*stride + i]
+  const uint8_t* len;    // [stride] off-diagonal count per row
+  const uint8_t* drank;  // [stride] position of the diagonal among the row's entries
+  const float* dv;       // [stride] raw diagonal value (0 if absent)
+  const float* de;       // [stride] smoother diagonal (dv, or 1.0 if |dv| < 1e-14)
+  // coarsening operators (only when nc > 0)
   uint32_t nc;
-  const uint32_t* agg;     // [n] P: fine -> coarse
+  const uint32_t* agg;     // [stride] P: fine -> coarse (padding rows -> 0, never read)
   const uint32_t* r_row;   // [nc+1] R = P^T rows (fine indices ascending)
   const uint32_t* r_col;
 };
+
+// Levels handled by the single-workgroup V-cycle tail kernel.
+struct AmgTailLevel {
+  AmgLevelDev L;
+  float* x;
+  float* xt;
+  float* b;
+  float* r;
+};
+constexpr int kMaxAmgLevels = 20;
 
 // ---------------- launch wrappers (kernels.hip) ----------------
 void launch_prepare(const PrepareArgs& a, hipStream_t s);
@@ -166,7 +186,10 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
                          hipStream_t s);
 // `sweeps` smoother sweeps of a level with n <= 1024 rows in one workgroup (LDS ping-pong)
-void launch_amg_coarse(const AmgLevelDev& L, float* x, const float* b, int sweeps, hipStream_t s);
+// V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
+// pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
+// Every level's x ends in tail[l].x (even sweep counts).
+void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
 void launch_fill(float* x, float v, size_t n, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:

@@ -258,15 +258,18 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   basis = arena.alloc<float>((size_t)m1 * stride);
   zvec = arena.alloc<float>((size_t)m * stride);
   w = arena.alloc<float>(n);
-  temp = arena.alloc<float>(N);
-  temp_p = arena.alloc<float>(N);
-  p_sol = arena.alloc<float>(N);
+  // pressure vectors are padded to a multiple of 64 (zeroed): the AMG level-0
+  // kernels process 4 rows per thread with 16-byte loads
+  const size_t np = ((size_t)N + 63) & ~(size_t)63;
+  temp = arena.alloc<float>(np);
+  temp_p = arena.alloc<float>(np);
+  p_sol = arena.alloc<float>(np);
   CFD_HIP(hipMemsetAsync(basis, 0, (size_t)m1 * stride * sizeof(float), stream));
   CFD_HIP(hipMemsetAsync(zvec, 0, (size_t)m * stride * sizeof(float), stream));
   CFD_HIP(hipMemsetAsync(w, 0, n * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(temp, 0, N * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(temp_p, 0, N * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(p_sol, 0, N * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(temp, 0, np * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(temp_p, 0, np * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(p_sol, 0, np * sizeof(float), stream));
   partial = arena.alloc<float>((size_t)m1 * nchunks);
   partial_n = arena.alloc<float>(nchunks);
   const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
@@ -298,72 +301,116 @@ void Solver::ensure_amg() {
   for (uint32_t i = 0; i < N; ++i)
     for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k)
       A0.val[k] = ell[(size_t)(k - topo.srow[i]) * N + i];
-  std::vector<AmgHostLevel> H0 = build_amg_hierarchy(A0, 20);
+  std::vector<AmgHostLevel> H0 = build_amg_hierarchy(A0, kMaxAmgLevels);
   levels.clear();
   for (size_t li = 0; li < H0.size(); ++li) {
     const AmgHostLevel& L = H0[li];
     const uint32_t n = (uint32_t)L.A.rows;
+    const uint32_t st = (n + 63) & ~63u;  // padded row count (16-byte row groups)
     int wmax = 0;
-    std::vector<uint32_t> len(n), drank(n);
-    std::vector<float> dv(n), de(n);
+    bool small_delta = true;
+    std::vector<uint8_t> len(st, 0), drank(st, 0);
+    std::vector<float> dv(st, 0.0f), de(st, 1.0f);
     for (uint32_t i = 0; i < n; ++i) {
       uint32_t off = 0, dr = 0;
       bool has = false;
       float diag = 1.0f, raw = 0.0f;
       for (uint32_t k = L.A.row[i]; k < L.A.row[i + 1]; ++k) {
-        if (L.A.col[k] == i) {
+        const uint32_t c = L.A.col[k];
+        if (c == i) {
           has = true;
           raw = L.A.val[k];
           diag = raw;
           dr = off;
         } else {
           ++off;
+          const int64_t d = (int64_t)c - (int64_t)i;
+          if (d < -32768 || d > 32767) small_delta = false;
         }
       }
       if (!has) dr = off;  // no diagonal entry: raw diag contributes nothing (dv = 0)
       if (std::fabs(diag) < 1e-14f) diag = 1.0f;  // amg.wgsl:46
-      len[i] = off;
-      drank[i] = dr;
+      if (off > 255) throw std::domain_error("AMG level row wider than 255 entries");
+      len[i] = (uint8_t)off;
+      drank[i] = (uint8_t)dr;
       dv[i] = raw;
       de[i] = diag;
       wmax = std::max(wmax, (int)off);
     }
-    std::vector<uint32_t> col((size_t)std::max(wmax, 1) * n, 0);
-    std::vector<float> val((size_t)std::max(wmax, 1) * n, 0.0f);
-    for (uint32_t i = 0; i < n; ++i) {
+    const size_t slots = (size_t)std::max(wmax, 1) * st;
+    std::vector<float> val(slots, 0.0f);
+    std::vector<int16_t> col16(small_delta ? slots : 0, 0);
+    std::vector<uint32_t> col32(small_delta ? 0 : slots, 0);
+    for (uint32_t i = 0; i < st; ++i) {
       uint32_t r = 0;
-      for (uint32_t k = L.A.row[i]; k < L.A.row[i + 1]; ++k) {
-        if (L.A.col[k] == i) continue;
-        col[(size_t)r * n + i] = L.A.col[k];
-        val[(size_t)r * n + i] = L.A.val[k];
-        ++r;
-      }
-      for (; r < (uint32_t)std::max(wmax, 1); ++r) col[(size_t)r * n + i] = i;
+      if (i < n)
+        for (uint32_t k = L.A.row[i]; k < L.A.row[i + 1]; ++k) {
+          const uint32_t c = L.A.col[k];
+          if (c == i) continue;
+          const size_t o = (size_t)r * st + i;
+          val[o] = L.A.val[k];
+          if (small_delta)
+            col16[o] = (int16_t)((int64_t)c - (int64_t)i);
+          else
+            col32[o] = c;
+          ++r;
+        }
+      // padding slots: value 0, column = own row (delta 0; padding rows read x[i],
+      // which is allocated and zero-initialised)
+      if (!small_delta)
+        for (; r < (uint32_t)std::max(wmax, 1); ++r) col32[(size_t)r * st + i] = std::min(i, n - 1);
     }
+    if (small_delta)  // padding rows must not point past n-1 either
+      for (uint32_t i = n; i < st; ++i)
+        for (int r = 0; r < std::max(wmax, 1); ++r) col16[(size_t)r * st + i] = 0;
     AmgGpuLevel G;
     G.nnz = L.A.col.size();
     G.dev.n = n;
+    G.dev.stride = st;
     G.dev.w = wmax;
-    G.dev.col = arena.upload(col, stream);
+    G.dev.use16 = small_delta ? 1 : 0;
     G.dev.val = arena.upload(val, stream);
+    G.dev.col16 = small_delta ? arena.upload(col16, stream) : nullptr;
+    G.dev.col32 = small_delta ? nullptr : arena.upload(col32, stream);
     G.dev.len = arena.upload(len, stream);
     G.dev.drank = arena.upload(drank, stream);
     G.dev.dv = arena.upload(dv, stream);
     G.dev.de = arena.upload(de, stream);
     G.dev.nc = L.has_op ? L.nc : 0;
-    G.dev.agg = L.has_op ? arena.upload(L.agg, stream) : nullptr;
-    G.dev.r_row = L.has_op ? arena.upload(L.r_row, stream) : nullptr;
-    G.dev.r_col = L.has_op ? arena.upload(L.r_col, stream) : nullptr;
-    G.xt = arena.alloc<float>(n);
-    G.r = arena.alloc<float>(n);
+    if (L.has_op) {
+      std::vector<uint32_t> agg(st, 0);
+      std::copy(L.agg.begin(), L.agg.end(), agg.begin());
+      G.dev.agg = arena.upload(agg, stream);
+      G.dev.r_row = arena.upload(L.r_row, stream);
+      G.dev.r_col = arena.upload(L.r_col, stream);
+    }
+    auto zeroed = [&](size_t cnt) {
+      float* p = arena.alloc<float>(cnt);
+      CFD_HIP(hipMemsetAsync(p, 0, cnt * sizeof(float), stream));
+      return p;
+    };
+    G.xt = zeroed(st);
+    G.r = zeroed(st);
     if (li > 0) {
-      G.x = arena.alloc<float>(n);
-      G.b = arena.alloc<float>(n);
-      CFD_HIP(hipMemsetAsync(G.x, 0, n * sizeof(float), stream));
-      CFD_HIP(hipMemsetAsync(G.b, 0, n * sizeof(float), stream));
+      G.x = zeroed(st);
+      G.b = zeroed(st);
     }
     levels.push_back(G);
   }
+  // levels from `tail_first` down run inside one single-workgroup kernel
+  const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
+  const uint32_t tail_rows = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 4096u;
+  tail_first = (int)levels.size();
+  while (tail_first > 1 && levels[tail_first - 1].dev.n <= tail_rows) --tail_first;
+  std::vector<AmgTailLevel> tl(levels.size());
+  for (size_t li = 0; li < levels.size(); ++li) {
+    tl[li].L = levels[li].dev;
+    tl[li].x = levels[li].x;
+    tl[li].xt = levels[li].xt;
+    tl[li].b = levels[li].b;
+    tl[li].r = levels[li].r;
+  }
+  d_tail = arena.upload(tl, stream);
   sync();
   amg_built = true;
 }
@@ -397,21 +444,27 @@ void Solver::amg_smooth(size_t li, float*& xcur, const float* b) {
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
 
-// amg.rs:666-770, level 0 bound to (x = p_sol, b = temp_p)
+// amg.rs:666-770, level 0 bound to (x = p_sol, b = temp_p).  Levels below
+// `tail_first` (all small) run as one single-workgroup kernel (k_amg_tail).
 void Solver::v_cycle() {
-  const size_t L = levels.size();
+  const int L = (int)levels.size();
   levels[0].x = p_sol;
   levels[0].b = temp_p;
-  for (size_t i = 0; i + 1 < L; ++i) {
+  // the tail needs level >= 1 (level 0's x/b are bound per call) and is off
+  // while the level-0 smoother is being timed on a one-level hierarchy
+  const int tf = (prof && L == 1) ? L : std::max(tail_first, 1);
+  const int down = std::min(tf, L - 1);
+  for (int i = 0; i < down; ++i) {
     amg_smooth(i, levels[i].x, levels[i].b);
     launch_amg_residual(levels[i].dev, levels[i].x, levels[i].b, levels[i].r, stream);
     launch_amg_restrict(levels[i].dev, levels[i].r, levels[i + 1].b, levels[i + 1].x, stream);
   }
-  if (L > 1 && levels[L - 1].dev.n <= 1024 && !(prof && L == 1))
-    launch_amg_coarse(levels[L - 1].dev, levels[L - 1].x, levels[L - 1].b, 10, stream);
-  else
+  if (tf < L) {
+    launch_amg_tail(d_tail, tf, L, stream);
+  } else {
     for (int s = 0; s < 10; ++s) amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
-  for (size_t ii = L - 1; ii-- > 0;) {
+  }
+  for (int ii = down - 1; ii >= 0; --ii) {
     launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
     amg_smooth(ii, levels[ii].x, levels[ii].b);
   }

@@ -171,6 +171,8 @@ struct Solver {
   LagReader inner;
   // AMG
   bool amg_built = false;
+  int tail_first = 1;              // first AMG level handled by k_amg_tail
+  AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   std::vector<AmgGpuLevel> levels;
   // host-side state
   cfd_constants constants{};
