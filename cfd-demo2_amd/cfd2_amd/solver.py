@@ -54,6 +54,17 @@ def _bind():
     L.cfd_debug_buffer_len.restype = C.c_size_t
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
     L.cfd_debug_prepare_assemble.argtypes = [_vp, C.c_int32]
+    u8p = C.POINTER(C.c_uint8)
+    u32p = C.POINTER(C.c_uint32)
+    L.cfd_dist_unique_id.argtypes = [u8p]
+    L.cfd_solver_create_dist.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
+                                         C.c_int32, C.c_int32, u8p, C.POINTER(_vp)]
+    L.cfd_group_create.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
+                                   C.POINTER(C.c_int32), C.POINTER(_vp)]
+    L.cfd_group_step.argtypes = [C.POINTER(_vp), C.c_int32]
+    L.cfd_dist_info.argtypes = [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), u32p, u32p, u32p]
+    L.cfd_dist_plan.argtypes = [C.POINTER(_ffi.MeshView), C.c_int32, C.c_int32, u32p, u32p, u32p, u32p,
+                                u32p, u32p, C.POINTER(C.c_int32), u32p, u32p, u32p]
     _bound = True
     return L
 
@@ -64,18 +75,41 @@ class GpuSolver:
     JACOBI = 0
     AMG = 1
 
-    def __init__(self, mesh, config: _ffi.Config | None = None, device: int = 0, **cfg_overrides):
+    def __init__(self, mesh, config: _ffi.Config | None = None, device: int = 0, _handle=None,
+                  **cfg_overrides):
         L = _bind()
         self._mesh = mesh
         cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
         self._cfg = cfg
-        view = mesh.view()
-        h = _vp()
-        _ffi.check(L.cfd_solver_create(C.byref(view), C.byref(cfg), int(device), C.byref(h)),
-                   "cfd_solver_create")
+        if _handle is None:
+            view = mesh.view()
+            h = _vp()
+            _ffi.check(L.cfd_solver_create(C.byref(view), C.byref(cfg), int(device), C.byref(h)),
+                       "cfd_solver_create")
+        else:
+            h = _handle
         self._h = h
         self.num_cells = int(L.cfd_num_cells(h))
         self.num_faces = int(L.cfd_num_faces(h))
+        r, n, c0, c1, ng = C.c_int32(), C.c_int32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _ffi.check(L.cfd_dist_info(h, C.byref(r), C.byref(n), C.byref(c0), C.byref(c1), C.byref(ng)),
+                   "cfd_dist_info")
+        self.rank, self.nranks = r.value, n.value
+        self.owned = (c0.value, c1.value)  # global cell range this handle owns
+        self.num_global_cells = ng.value
+
+    @classmethod
+    def create_dist(cls, mesh, nranks: int, rank: int, unique_id: bytes, device: int = 0,
+                    config: _ffi.Config | None = None, **cfg_overrides):
+        """One rank of the RCCL-distributed solver (one process per GPU).  Collective."""
+        L = _bind()
+        cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
+        view = mesh.view()
+        uid = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        h = _vp()
+        _ffi.check(L.cfd_solver_create_dist(C.byref(view), C.byref(cfg), int(device), int(nranks), int(rank),
+                                            uid, C.byref(h)), "cfd_solver_create_dist")
+        return cls(mesh, config=cfg, _handle=h)
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -118,18 +152,22 @@ class GpuSolver:
     # -- state ------------------------------------------------------------------
     def set_u(self, u):
         a = np.ascontiguousarray(np.asarray(u, dtype=np.float64).reshape(-1))
-        if a.size != 2 * self.num_cells:
-            raise ValueError("set_u expects num_cells (u, v) pairs")
+        if a.size != 2 * self.num_global_cells:
+            raise ValueError("set_u expects one (u, v) pair per mesh cell")
         self._call("cfd_set_u", a.ctypes.data_as(C.POINTER(C.c_double)))
 
     def set_p(self, p):
         a = np.ascontiguousarray(np.asarray(p, dtype=np.float64).reshape(-1))
-        if a.size != self.num_cells:
-            raise ValueError("set_p expects num_cells values")
+        if a.size != self.num_global_cells:
+            raise ValueError("set_p expects one value per mesh cell")
         self._call("cfd_set_p", a.ctypes.data_as(C.POINTER(C.c_double)))
 
     def initialize_history(self): self._call("cfd_initialize_history")
     def step(self): self._call("cfd_step")
+
+    # set_u / set_p take GLOBAL arrays (a distributed rank keeps its cells + ghosts)
+    def _global_len(self):
+        return self.num_global_cells
 
     def get_u(self) -> np.ndarray:
         a = np.zeros(2 * self.num_cells)
@@ -188,3 +226,102 @@ class GpuSolver:
 
     def debug_prepare_assemble(self, assemble=True):
         self._call("cfd_debug_prepare_assemble", 1 if assemble else 0)
+
+
+def dist_unique_id() -> bytes:
+    """RCCL unique id (rank 0 creates it, every rank passes it to create_dist)."""
+    L = _bind()
+    buf = (C.c_uint8 * 128)()
+    _ffi.check(L.cfd_dist_unique_id(buf), "cfd_dist_unique_id")
+    return bytes(buf)
+
+
+class GpuGroup:
+    """In-process distributed solver: ``nranks`` ranks on ``devices`` (default
+    all on GPU 0), one host thread per rank inside the library.  Same surface
+    as GpuSolver; getters return global arrays (owned slices concatenated)."""
+
+    def __init__(self, mesh, nranks: int, devices=None, config: _ffi.Config | None = None,
+                 **cfg_overrides):
+        L = _bind()
+        cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
+        view = mesh.view()
+        devs = list(devices) if devices is not None else [0] * nranks
+        if len(devs) != nranks:
+            raise ValueError("one device per rank")
+        darr = (C.c_int32 * nranks)(*devs)
+        harr = (_vp * nranks)()
+        _ffi.check(L.cfd_group_create(C.byref(view), C.byref(cfg), int(nranks), darr, harr),
+                   "cfd_group_create")
+        self._harr = harr
+        self.ranks = [GpuSolver(mesh, config=cfg, _handle=_vp(harr[r])) for r in range(nranks)]
+        self.nranks = nranks
+        self.num_cells = self.ranks[0].num_global_cells
+
+    def close(self):
+        for r in self.ranks:
+            r.close()
+        self.ranks = []
+
+    def __getattr__(self, name):
+        # setters / state writers apply to every rank
+        if name.startswith("set_") or name in ("update_constants", "initialize_history",
+                                               "profile_enable", "profile_reset"):
+            def f(*a, **k):
+                for r in self.ranks:
+                    getattr(r, name)(*a, **k)
+            return f
+        raise AttributeError(name)
+
+    @property
+    def constants(self):
+        return self.ranks[0].constants
+
+    @constants.setter
+    def constants(self, c):
+        for r in self.ranks:
+            r.constants = c
+
+    def step(self):
+        _ffi.check(_bind().cfd_group_step(self._harr, self.nranks), "cfd_group_step")
+
+    def _gather(self, getter, comps):
+        out = np.zeros((self.num_cells, comps) if comps > 1 else self.num_cells)
+        for r in self.ranks:
+            c0, c1 = r.owned
+            out[c0:c1] = getattr(r, getter)()
+        return out
+
+    def get_u(self): return self._gather("get_u", 2)
+    def get_p(self): return self._gather("get_p", 1)
+    def get_d_p(self): return self._gather("get_d_p", 1)
+    def step_info(self): return self.ranks[0].step_info()
+    def amg_levels(self): return self.ranks[0].amg_levels()
+
+    @property
+    def should_stop(self): return self.ranks[0].should_stop
+    @property
+    def degenerate_count(self): return self.ranks[0].degenerate_count
+
+
+def dist_plan(mesh, nranks: int, rank: int) -> dict:
+    """Host-only halo plan of one rank (no GPU): owned range, ghost ids, and per
+    peer the receive / send counts and the owned ids sent."""
+    L = _bind()
+    view = mesh.view()
+    c0, c1, ng, npeer, ns = (C.c_uint32() for _ in range(5))
+    z = None
+    _ffi.check(L.cfd_dist_plan(C.byref(view), nranks, rank, C.byref(c0), C.byref(c1), C.byref(ng),
+                               C.byref(npeer), C.byref(ns), z, z, z, z, z), "cfd_dist_plan")
+    ghost = np.zeros(max(ng.value, 1), dtype=np.uint32)
+    prank = np.zeros(max(npeer.value, 1), dtype=np.int32)
+    precv = np.zeros(max(npeer.value, 1), dtype=np.uint32)
+    psend = np.zeros(max(npeer.value, 1), dtype=np.uint32)
+    sendg = np.zeros(max(ns.value, 1), dtype=np.uint32)
+    u32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
+    _ffi.check(L.cfd_dist_plan(C.byref(view), nranks, rank, None, None, None, None, None, u32(ghost),
+                               prank.ctypes.data_as(C.POINTER(C.c_int32)), u32(precv), u32(psend),
+                               u32(sendg)), "cfd_dist_plan")
+    n = npeer.value
+    return dict(c0=c0.value, c1=c1.value, ghost=ghost[:ng.value], peers=prank[:n].tolist(),
+                recv=precv[:n].tolist(), send=psend[:n].tolist(), send_ids=sendg[:ns.value])

@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
     float flux = 0.0f;
     float po_other = 0.0f;
     float2 uo = make_float2(0.0f, 0.0f);
-    if (other >= 0) {
+    if (other != kNoCell) {
       const float2 u_oth = a.st.u[other];
       const float p_oth = a.st.p[other];
       const float dp_oth = a.st.dp[other];
@@ -147,7 +147,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
     a.flux_s[e] = flux_out;
     const float diff_coeff = c.viscosity * area / fs.dist_e[e];
     const float conv_diag = flux_out > 0.0f ? flux_out : 0.0f;
-    if (other >= 0) {
+    if (other != kNoCell) {
       diag_coeff += diff_coeff + conv_diag;
     } else if (bt == 1u || bt == 3u) {
       diag_coeff += diff_coeff;
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
       if (flux_out > 0.0f) diag_coeff += flux_out;
     }
     float vfp, vfu, vfv;
-    if (other >= 0) {
+    if (other != kNoCell) {
       const float lp = fs.lam_s[e];
       vfp = lp * pc + (1.0f - lp) * po_other;
       if ((meta & kMetaDegen) == 0) {
@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
     const float diff_coeff = c.viscosity * area / dist;
     const float conv_diag = flux > 0.0f ? flux : 0.0f;
     const float conv_off = flux > 0.0f ? 0.0f : flux;
-    if (other >= 0) {
+    if (other != kNoCell) {
       const uint32_t rank = (meta >> kMetaRankShift) & 0xFFu;
       const float dp_other = a.st.dp[other];
       const float coeff = -diff_coeff + conv_off;
@@ -477,9 +477,9 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   float su = 0.0f, sv = 0.0f, sp = 0.0f;
   for (uint32_t r = 0; r < len; ++r) {
     const size_t slot = (size_t)r * N + i;
-    const uint32_t j = A.col[slot];
+    const int32_t j = A.col[slot];
     const BlockCoeffs k = load_block(A, r, dr, slot, d2);
-    const float xu = x[3 * (size_t)j], xv = x[3 * (size_t)j + 1], xp = x[3 * (size_t)j + 2];
+    const float xu = x[3 * (ptrdiff_t)j], xv = x[3 * (ptrdiff_t)j + 1], xp = x[3 * (ptrdiff_t)j + 2];
     su += k.uu * xu;
     su += 0.0f * xv;
     su += k.up * xp;
@@ -653,11 +653,11 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
   const float2 d2 = A.cdiag2[i];
   for (uint32_t r = 0; r < len; ++r) {
     const size_t slot = (size_t)r * N + i;
-    const uint32_t j = A.col[slot];
+    const int32_t j = A.col[slot];
     const float2 g = A.cval_g[slot];
     const float pu = (r == dr) ? d2.x : g.x, pv = (r == dr) ? d2.y : g.y;
     const float dj = dinv_uv[j];
-    const float ru = sc * w_in[3 * (size_t)j], rv = sc * w_in[3 * (size_t)j + 1];
+    const float ru = sc * w_in[3 * (ptrdiff_t)j], rv = sc * w_in[3 * (ptrdiff_t)j + 1];
     const float zu = ru * dj;
     const float zv = rv * dj;
     rhs_p -= pu * zu;
@@ -669,7 +669,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
 }
 
 // relax_pressure (schur_precond.wgsl:52-90), omega = 1.2, live scalar matrix
-__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const uint32_t* __restrict__ col,
+__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const int32_t* __restrict__ col,
                                                            const uint32_t* __restrict__ len,
                                                            const float* __restrict__ sval,
                                                            const float* __restrict__ dinv_p,
@@ -682,8 +682,8 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const uin
   const uint32_t l = len[i];
   for (uint32_t r = 0; r < l; ++r) {
     const size_t slot = (size_t)r * N + i;
-    const uint32_t cc = col[slot];
-    if (cc != i) sigma += sval[slot] * p_sol[cc];
+    const int32_t cc = col[slot];
+    if (cc != (int32_t)i) sigma += sval[slot] * p_sol[cc];
   }
   const float hat_x = dinv_p[i] * (temp_p[i] - sigma);
   p_prev[i] = wmix(p_prev[i], hat_x, 1.2f);
@@ -704,7 +704,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
   float cu = 0.0f, cv = 0.0f;
   for (uint32_t r = 0; r < len; ++r) {
     const size_t slot = (size_t)r * N + i;
-    const uint32_t j = A.col[slot];
+    const int32_t j = A.col[slot];
     const float2 g = A.cval_g[slot];
     const float pj = p_sol[j];
     cu += g.x * pj;
@@ -748,15 +748,15 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
 // 8 bytes per slot, lengths 4 bytes; only the x gathers are scalar.
 template <bool D16>
 __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uint32_t i0,
-                                           uint32_t c[4]) {
+                                           int c[4]) {
   if constexpr (D16) {
     const short4 d = *reinterpret_cast<const short4*>(L.col16 + off);
-    c[0] = i0 + (int)d.x;
-    c[1] = i0 + 1 + (int)d.y;
-    c[2] = i0 + 2 + (int)d.z;
-    c[3] = i0 + 3 + (int)d.w;
+    c[0] = (int)i0 + (int)d.x;
+    c[1] = (int)i0 + 1 + (int)d.y;
+    c[2] = (int)i0 + 2 + (int)d.z;
+    c[3] = (int)i0 + 3 + (int)d.w;
   } else {
-    const uint4 q = *reinterpret_cast<const uint4*>(L.col32 + off);
+    const int4 q = *reinterpret_cast<const int4*>(L.col32 + off);
     c[0] = q.x;
     c[1] = q.y;
     c[2] = q.z;
@@ -787,7 +787,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
   for (uint32_t r = 0; r < maxlen; ++r) {
     const size_t off = (size_t)r * L.stride + i0;
     const float4 v = *reinterpret_cast<const float4*>(L.val + off);
-    uint32_t c[4];
+    int c[4];
     load_cols4<D16>(L, off, i0, c);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -823,7 +823,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
     if (r == maxlen) break;
     const size_t off = (size_t)r * L.stride + i0;
     const float4 v = *reinterpret_cast<const float4*>(L.val + off);
-    uint32_t c[4];
+    int c[4];
     load_cols4<D16>(L, off, i0, c);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -838,16 +838,25 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
 }
 
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
-// also clears the coarse solution (amg.rs:721-725 `clear`, fused)
+// also clears the coarse solution (amg.rs:721-725 `clear`, fused), including
+// its ghost entries [-glo, 0) and [stride_c, stride_c + ghi) on a distributed level
 __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
                                                          float* __restrict__ cb,
-                                                         float* __restrict__ cx) {
+                                                         float* __restrict__ cx, uint32_t stride_c,
+                                                         uint32_t glo, uint32_t ghi) {
   const uint32_t I = row_id();
-  if (I >= L.nc) return;
-  float sum = 0.0f;
-  for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
-  cb[I] = sum;
-  cx[I] = 0.0f;
+  if (I < L.nc) {
+    float sum = 0.0f;
+    for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
+    cb[I] = sum;
+    cx[I] = 0.0f;
+    return;
+  }
+  const uint32_t g = I - L.nc;
+  if (g < glo)
+    cx[-1 - (int)g] = 0.0f;
+  else if (g < glo + ghi)
+    cx[stride_c + (g - glo)] = 0.0f;
 }
 
 // prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread
@@ -870,8 +879,8 @@ __global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* __
 }
 
 // ---- single-row helpers for the one-workgroup kernels (small levels) ----
-__device__ __forceinline__ uint32_t col_at(const AmgLevelDev& L, size_t off, uint32_t i) {
-  return L.use16 ? (uint32_t)((int)i + (int)L.col16[off]) : L.col32[off];
+__device__ __forceinline__ int col_at(const AmgLevelDev& L, size_t off, uint32_t i) {
+  return L.use16 ? (int)i + (int)L.col16[off] : L.col32[off];
 }
 __device__ __forceinline__ float smooth_row(const AmgLevelDev& L, const float* x, const float* b,
                                             uint32_t i) {
@@ -990,9 +999,13 @@ __device__ __forceinline__ void view_pair(const StateView& v, uint32_t rec, int 
   }
 }
 
+// `var` + (gbase, rec0): the records the variance part reads -- the record of
+// global index gbase + c is ((gbase + c) >> 2) - rec0 in `var` (on one GPU:
+// var = cur, gbase = rec0 = 0; distributed: records fetched from their owners).
 __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, StateView prev,
                                                               int have_prev, uint32_t N,
-                                                              double* partial) {
+                                                              StateView var, uint64_t gbase,
+                                                              uint64_t rec0, double* partial) {
   __shared__ double lds[kBlock];
   const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
   double evo = 0.0, su = 0.0, sv = 0.0, squ = 0.0, sqv = 0.0;
@@ -1010,7 +1023,8 @@ __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, Sta
       }
     }
     float a, b;
-    view_pair(cur, (uint32_t)(c >> 2), (int)(c & 3), &a, &b);
+    const uint64_t gi = gbase + c;
+    view_pair(var, (uint32_t)((gi >> 2) - rec0), (int)(gi & 3), &a, &b);
     const double ad = (double)a, bd = (double)b;
     su += ad;
     sv += bd;
@@ -1041,6 +1055,50 @@ __global__ void __launch_bounds__(kBlock) k_evolution_final(const double* __rest
     const double r = block_tree_d(acc, lds);
     if (threadIdx.x == 0) out5[f] = r;
   }
+}
+
+// ------------------------- distributed helpers ------------------------------
+// Halo pack: for every field f, stage[off_f + k*comps_f + c] = src_f[idx[k]*comps_f + c]
+// (idx = owned rows the peers need, concatenated per peer, ascending global id).
+__global__ void __launch_bounds__(kBlock) k_pack(PackArgs a) {
+  const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= a.n) return;
+  const int32_t i = a.idx[k];
+  for (int f = 0; f < a.nf; ++f) {
+    const PackField F = a.f[f];
+    for (int c = 0; c < F.comps; ++c)
+      a.stage[F.stage_off + (size_t)k * F.comps + c] = F.src[(ptrdiff_t)i * F.comps + c];
+  }
+}
+
+// Per-rank stage 2 of `nvec` canonical reductions: out[v] = tree(partial[v*np ...]).
+__global__ void __launch_bounds__(kBlock) k_stage2_multi(const float* __restrict__ partial,
+                                                         uint32_t np, float* out) {
+  __shared__ float lds[kBlock];
+  const int v = blockIdx.x;
+  const float s = block_final(partial + (size_t)v * np, np, lds);
+  if (threadIdx.x == 0) out[v] = s;
+}
+
+// Rank combine (distributed canonical order): out[v] = ((0 + s_0) + s_1) + ... in rank order.
+__global__ void k_rank_combine(const float* __restrict__ gathered, int R, int nvec, float* out) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nvec) return;
+  float acc = 0.0f;
+  for (int r = 0; r < R; ++r) acc += gathered[(size_t)r * nvec + v];
+  out[v] = acc;
+}
+
+// max over ranks of the (u, p) max-diff bit patterns
+__global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint32_t* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t bu = 0, bp = 0;
+  for (int r = 0; r < R; ++r) {
+    bu = max(bu, gathered[2 * r]);
+    bp = max(bp, gathered[2 * r + 1]);
+  }
+  out[0] = bu;
+  out[1] = bp;
 }
 
 }  // namespace
@@ -1099,7 +1157,7 @@ void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const flo
     hipLaunchKernelGGL(k_precond_predict, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv,
                        dinv_p, temp_p, p_sol, p_prev);
 }
-void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len, const float* sval,
+void launch_relax_pressure(uint32_t N, int ws, const int32_t* col, const uint32_t* len, const float* sval,
                            const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
                            hipStream_t s) {
   (void)ws;
@@ -1136,8 +1194,10 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
   else
     hipLaunchKernelGGL(k_amg_residual<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
-void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, hipStream_t s) {
-  if (L.nc) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(L.nc)), dim3(kBlock), 0, s, L, r, cb, cx);
+void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
+                         uint32_t glo, uint32_t ghi, hipStream_t s) {
+  const size_t n = (size_t)L.nc + glo + ghi;
+  if (n) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, x, xc);
@@ -1148,10 +1208,24 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, hipStream_t 
 void launch_fill(float* x, float v, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);
 }
-void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, double* partial,
-                              hipStream_t s) {
+void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
+                              uint64_t gbase, uint64_t rec0, double* partial, hipStream_t s) {
   const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
-  if (nb) hipLaunchKernelGGL(k_evolution_partial, dim3(nb), dim3(kBlock), 0, s, cur, prev, have_prev, N, partial);
+  if (nb)
+    hipLaunchKernelGGL(k_evolution_partial, dim3(nb), dim3(kBlock), 0, s, cur, prev, have_prev, N, var, gbase,
+                       rec0, partial);
+}
+void launch_pack(const PackArgs& a, hipStream_t s) {
+  if (a.n) hipLaunchKernelGGL(k_pack, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a);
+}
+void launch_stage2_multi(const float* partial, uint32_t np, int nvec, float* out, hipStream_t s) {
+  if (nvec > 0) hipLaunchKernelGGL(k_stage2_multi, dim3(nvec), dim3(kBlock), 0, s, partial, np, out);
+}
+void launch_rank_combine(const float* gathered, int R, int nvec, float* out, hipStream_t s) {
+  if (nvec > 0) hipLaunchKernelGGL(k_rank_combine, dim3((nvec + 63) / 64), dim3(64), 0, s, gathered, R, nvec, out);
+}
+void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_max_combine, dim3(1), dim3(64), 0, s, gathered, R, out);
 }
 void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s) {
   hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kBlock), 0, s, partial, np, out5);

@@ -34,8 +34,15 @@ constexpr int kRedThreads = 256;
 constexpr int kRedCellsPerThread = 4;
 constexpr int kRedChunkCells = kRedThreads * kRedCellsPerThread;
 
+// Local cell numbering: every per-cell device pointer points at the first
+// OWNED cell; neighbour indices are signed offsets from it.  On one GPU they
+// are the global indices; on a distributed rank ghosts of lower ranks sit at
+// [-glo, 0) and ghosts of higher ranks at [npad, npad + ghi) (npad = owned
+// count rounded up to 64), so local order == global order.
+constexpr int32_t kNoCell = INT32_MIN;  // boundary face: no neighbour
+
 struct FaceSlots {  // ELL [k*N + i], k < wf
-  const int32_t* other;
+  const int32_t* other;  // neighbour (signed local index) or kNoCell
   const uint32_t* meta;
   const float* area;
   const float* nx;  // normal oriented out of this cell
@@ -98,7 +105,7 @@ struct AssembleArgs {
 struct CoupledMatrix {
   uint32_t N;
   int ws;
-  const uint32_t* col;  // [r*N + i]
+  const int32_t* col;   // [r*N + i] signed local column
   const uint32_t* len;  // [N]
   const uint32_t* drank;  // [N]
   const float2* cval_a;
@@ -120,7 +127,7 @@ struct AmgLevelDev {
   int use16;             // 1: col16 holds deltas; 0: col32 holds absolute columns
   const float* val;      // [r*stride + i]
   const int16_t* col16;  // [r*stride + i]  col - i
-  const uint32_t* col32; // [r*stride + i]
+  const int32_t* col32;  // [r*stride + i] signed local column
   const uint8_t* len;    // [stride] off-diagonal count per row
   const uint8_t* drank;  // [stride] position of the diagonal among the row's entries
   const float* dv;       // [stride] raw diagonal value (0 if absent)
@@ -130,6 +137,20 @@ struct AmgLevelDev {
   const uint32_t* agg;     // [stride] P: fine -> coarse (padding rows -> 0, never read)
   const uint32_t* r_row;   // [nc+1] R = P^T rows (fine indices ascending)
   const uint32_t* r_col;
+};
+
+// Halo pack (distributed): up to 8 fields packed per launch.
+struct PackField {
+  const float* src;   // owned-base pointer of the field
+  int comps;          // floats per cell
+  uint32_t stage_off; // offset of this field's block in the stage buffer (floats)
+};
+struct PackArgs {
+  PackField f[8];
+  int nf;
+  const int32_t* idx;  // [n] owned local rows to send
+  uint32_t n;
+  float* stage;
 };
 
 // Levels handled by the single-workgroup V-cycle tail kernel.
@@ -169,7 +190,7 @@ void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int 
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s);
-void launch_relax_pressure(uint32_t N, int ws, const uint32_t* col, const uint32_t* len,
+void launch_relax_pressure(uint32_t N, int ws, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
@@ -182,10 +203,10 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
                        hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,
                          hipStream_t s);
-// coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused)
+// coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused); on a
+// distributed coarse level also clears its ghosts: [-glo, 0) and [stride_c, stride_c + ghi)
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
-                         hipStream_t s);
-// `sweeps` smoother sweeps of a level with n <= 1024 rows in one workgroup (LDS ping-pong)
+                         uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s);
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).
@@ -194,8 +215,17 @@ void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, h
 void launch_fill(float* x, float v, size_t n, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
 // partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
+// The variance part reads record ((gbase + c) >> 2) - rec0 of `var` (stride bug, §0.1-12).
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N,
-                              double* partial, hipStream_t s);
+                              StateView var, uint64_t gbase, uint64_t rec0, double* partial,
+                              hipStream_t s);
+// ---- distributed helpers ----
+void launch_pack(const PackArgs& a, hipStream_t s);
+// out[v] = canonical stage 2 of partial[v*np .. v*np+np) (this rank's sum)
+void launch_stage2_multi(const float* partial, uint32_t np, int nvec, float* out, hipStream_t s);
+// out[v] = ((0 + g[0][v]) + g[1][v]) + ... (rank order)
+void launch_rank_combine(const float* gathered, int R, int nvec, float* out, hipStream_t s);
+void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s);
 void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s);
 
 }  // namespace cfd2

@@ -4,6 +4,9 @@
 //   transpose            amg.rs:141-185  R = P^T, fine indices ascending per row
 //   galerkin_product     amg.rs:187-235  (R*A)*P, f32 accumulation in visit order
 //   level loop           amg.rs:374-595  stop at n <= 100, no reduction, or 20 levels
+// Distributed solver: the aggregation runs part by part (rank ranges of the
+// level's rows) and never lets an aggregate cross a part; with
+// one part this is exactly the reference's greedy index-order aggregation.
 // The hierarchy is built once (first AMG solve) and frozen.
 // P and R hold only 1.0 values, so they are stored as index arrays.
 #include <algorithm>
@@ -54,26 +57,37 @@ HostCsr spgemm(const HostCsr& a, const HostCsr& b) {
 
 }  // namespace
 
-std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels) {
+std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
+                                               const std::vector<uint64_t>& part0) {
   std::vector<AmgHostLevel> levels;
   HostCsr cur = fine;
+  // row partition of the current level (distributed solver): aggregates never
+  // cross a part, so coarse rows stay contiguous per rank (seed order = rank order)
+  std::vector<uint64_t> part = part0.empty() ? std::vector<uint64_t>{0, (uint64_t)fine.rows} : part0;
   for (size_t li = 0; li < max_levels; ++li) {
     AmgHostLevel L;
+    L.part = part;
     const size_t n = cur.rows;
     bool coarsened = false;
     if (li < max_levels - 1 && n > 100) {
       const uint32_t NONE = std::numeric_limits<uint32_t>::max();
       std::vector<uint32_t> agg(n, NONE);
+      std::vector<uint64_t> cpart(part.size(), 0);
       uint32_t nagg = 0;
-      for (size_t i = 0; i < n; ++i) {
-        if (agg[i] != NONE) continue;
-        agg[i] = nagg;
-        for (uint32_t k = cur.row[i]; k < cur.row[i + 1]; ++k) {
-          const uint32_t j = cur.col[k];
-          if (j != i && agg[j] == NONE) agg[j] = nagg;
+      for (size_t p = 0; p + 1 < part.size(); ++p) {
+        cpart[p] = nagg;
+        const uint64_t lo = part[p], hi = part[p + 1];
+        for (size_t i = lo; i < hi; ++i) {
+          if (agg[i] != NONE) continue;
+          agg[i] = nagg;
+          for (uint32_t k = cur.row[i]; k < cur.row[i + 1]; ++k) {
+            const uint32_t j = cur.col[k];
+            if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = nagg;
+          }
+          ++nagg;
         }
-        ++nagg;
       }
+      cpart.back() = nagg;
       if (nagg < n) {
         // P (n x nagg) and R = P^T as CSR with unit values
         HostCsr P, R;
@@ -106,6 +120,7 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
         L.has_op = true;
         L.A = std::move(cur);
         cur = std::move(next);
+        part = std::move(cpart);
         coarsened = true;
       }
     }

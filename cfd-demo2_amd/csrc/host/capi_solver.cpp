@@ -3,7 +3,10 @@
 // exceptions become status codes (the reference panics).
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "error.hpp"
 #include "solver_impl.hpp"
@@ -23,6 +26,8 @@ cfd_status guard(F&& f) {
     return CFD_OK;
   } catch (const cfd2::HipError& e) {
     return set_error(CFD_ERR_HIP, e.what());
+  } catch (const cfd2::RcclError& e) {
+    return set_error(CFD_ERR_RCCL, e.what());
   } catch (const std::domain_error& e) {
     return set_error(CFD_ERR_DIVERGED, e.what());
   } catch (const std::invalid_argument& e) {
@@ -219,6 +224,111 @@ cfd_status cfd_debug_buffer(cfd_solver* s, int32_t id, float* out, size_t count)
 cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble) {
   CHECK_S(s);
   return guard([&] { s->s->debug_prepare_assemble(assemble != 0); });
+}
+
+// ---------------------------------------------------------------- multi-GPU
+cfd_status cfd_dist_unique_id(uint8_t out[128]) {
+  if (!out) return set_error(CFD_ERR_INVALID, "null out");
+  return guard([&] { cfd2::rccl_unique_id(out); });
+}
+
+cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
+                                  int32_t nranks, int32_t rank, const uint8_t unique_id[128], cfd_solver** out) {
+  if (!mesh || !out || !unique_id) return set_error(CFD_ERR_INVALID, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(CFD_ERR_INVALID, "bad rank / nranks");
+  cfd_config c;
+  if (cfg)
+    c = *cfg;
+  else
+    cfd_config_default(&c);
+  cfd2::Solver* sp = nullptr;
+  const cfd_status st = guard([&] {
+    CFD_HIP(hipSetDevice(hip_device));
+    auto comm = cfd2::make_rccl_comm(nranks, rank, unique_id);
+    sp = new cfd2::Solver(*mesh, c, hip_device, std::move(comm));
+  });
+  if (st != CFD_OK) return st;
+  *out = new cfd_solver{sp};
+  return CFD_OK;
+}
+
+cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t nranks,
+                            const int32_t* devices, cfd_solver** out) {
+  if (!mesh || !out || !devices || nranks < 1) return set_error(CFD_ERR_INVALID, "bad argument");
+  cfd_config c;
+  if (cfg)
+    c = *cfg;
+  else
+    cfd_config_default(&c);
+  auto group = std::make_shared<cfd2::LocalGroup>(nranks);
+  std::vector<cfd2::Solver*> made;
+  const cfd_status st = guard([&] {
+    for (int r = 0; r < nranks; ++r) {
+      auto comm = cfd2::make_local_comm(group, r, devices[r]);
+      made.push_back(new cfd2::Solver(*mesh, c, devices[r], nranks > 1 ? std::move(comm) : nullptr));
+    }
+  });
+  if (st != CFD_OK) {
+    for (auto* p : made) delete p;
+    return st;
+  }
+  for (int r = 0; r < nranks; ++r) out[r] = new cfd_solver{made[r]};
+  return CFD_OK;
+}
+
+cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
+  if (!h || n < 1) return set_error(CFD_ERR_INVALID, "bad argument");
+  for (int r = 0; r < n; ++r) CHECK_S(h[r]);
+  std::vector<cfd_status> st(n, CFD_OK);
+  std::vector<std::string> msg(n);
+  std::vector<std::thread> th;
+  for (int r = 0; r < n; ++r)
+    th.emplace_back([&, r] {
+      st[r] = guard([&] { h[r]->s->step(); });
+      if (st[r] != CFD_OK) msg[r] = cfd_last_error();
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < n; ++r)
+    if (st[r] != CFD_OK) return set_error(st[r], "rank " + std::to_string(r) + ": " + msg[r]);
+  return CFD_OK;
+}
+
+cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0, uint32_t* c1,
+                         uint32_t* ng) {
+  CHECK_S(s);
+  if (rank) *rank = s->s->rk;
+  if (nranks) *nranks = s->s->R;
+  if (c0) *c0 = s->s->topo.c0;
+  if (c1) *c1 = s->s->topo.c1;
+  if (ng) *ng = s->s->NG;
+  return CFD_OK;
+}
+
+cfd_status cfd_dist_plan(const cfd_mesh_view* mesh, int32_t nranks, int32_t rank, uint32_t* c0, uint32_t* c1,
+                         uint32_t* num_ghosts, uint32_t* num_peers, uint32_t* num_send, uint32_t* ghost_global,
+                         int32_t* peer_rank, uint32_t* peer_recv, uint32_t* peer_send, uint32_t* send_global) {
+  if (!mesh) return set_error(CFD_ERR_INVALID, "null mesh");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(CFD_ERR_INVALID, "bad rank / nranks");
+  return guard([&] {
+    const auto starts = cfd2::partition_starts(mesh->num_cells, nranks);
+    cfd2::Topology t;
+    cfd2::build_topology(*mesh, t, (uint32_t)starts[rank], (uint32_t)starts[rank + 1]);
+    const cfd2::HaloPlan P =
+        cfd2::build_halo_plan(starts, rank, t.srow.data(), t.N, t.scol.data(), t.ghost, t.glo, t.npad);
+    if (c0) *c0 = t.c0;
+    if (c1) *c1 = t.c1;
+    if (num_ghosts) *num_ghosts = (uint32_t)t.ghost.size();
+    if (num_peers) *num_peers = (uint32_t)P.peers.size();
+    if (num_send) *num_send = (uint32_t)P.send_idx.size();
+    if (ghost_global) std::copy(t.ghost.begin(), t.ghost.end(), ghost_global);
+    for (size_t k = 0; k < P.peers.size(); ++k) {
+      if (peer_rank) peer_rank[k] = P.peers[k].rank;
+      if (peer_recv) peer_recv[k] = P.peers[k].recv_cnt;
+      if (peer_send) peer_send[k] = P.peers[k].send_cnt;
+    }
+    if (send_global)
+      for (size_t k = 0; k < P.send_idx.size(); ++k) send_global[k] = t.c0 + (uint32_t)P.send_idx[k];
+  });
 }
 
 }  // extern "C"

@@ -1,0 +1,188 @@
+// Transports of the distributed solver: RCCL (one process per GPU) and an
+// in-process group (one host thread per rank).  See comm.hpp.
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "solver_impl.hpp"
+
+namespace cfd2 {
+
+#define CFD_NCCL(expr)                                                                   \
+  do {                                                                                   \
+    ncclResult_t _r = (expr);                                                            \
+    if (_r != ncclSuccess) throw RcclError(std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+void Comm::allgatherv_inplace(void* buf, const std::vector<size_t>& off, hipStream_t s) {
+  std::vector<Msg> msgs;
+  char* b = static_cast<char*>(buf);
+  for (int q = 0; q < size; ++q) {
+    if (q == rank) continue;
+    msgs.push_back({q, b + off[rank], off[rank + 1] - off[rank], b + off[q], off[q + 1] - off[q]});
+  }
+  exchange(msgs, s);
+}
+
+// ------------------------------------------------------------------- RCCL
+void rccl_unique_id(uint8_t out[kUniqueIdBytes]) {
+  static_assert(sizeof(ncclUniqueId) == kUniqueIdBytes, "ncclUniqueId size");
+  ncclUniqueId id;
+  CFD_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+}
+
+namespace {
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(int nranks, int r, const uint8_t uid[kUniqueIdBytes]) {
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    CFD_NCCL(ncclCommInitRank(&comm_, nranks, id, r));
+    rank = r;
+    size = nranks;
+  }
+  ~RcclComm() override {
+    if (comm_) (void)ncclCommDestroy(comm_);
+  }
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    if (msgs.empty()) return;
+    CFD_NCCL(ncclGroupStart());
+    for (const Msg& m : msgs) {
+      if (m.sbytes) CFD_NCCL(ncclSend(m.sbuf, m.sbytes, ncclChar, m.peer, comm_, s));
+      if (m.rbytes) CFD_NCCL(ncclRecv(m.rbuf, m.rbytes, ncclChar, m.peer, comm_, s));
+    }
+    CFD_NCCL(ncclGroupEnd());
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    CFD_NCCL(ncclAllGather(send, recv, bytes, ncclChar, comm_, s));
+  }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUniqueIdBytes]) {
+  return std::make_unique<RcclComm>(nranks, rank, uid);
+}
+
+// ----------------------------------------------------------- local group
+LocalGroup::LocalGroup(int n) : slots(n), n_(n) {}
+
+LocalGroup::~LocalGroup() {
+  for (auto& sl : slots) {
+    if (sl.ready) (void)hipEventDestroy(sl.ready);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+}
+
+void LocalGroup::barrier() {
+  std::unique_lock<std::mutex> lk(mu_);
+  const uint64_t g = gen_;
+  if (++arrived_ == n_) {
+    arrived_ = 0;
+    ++gen_;
+    cv_.notify_all();
+  } else {
+    cv_.wait(lk, [&] { return gen_ != g; });
+  }
+}
+
+namespace {
+
+// Pull model: after barrier 1 every rank copies what it receives out of the
+// senders' buffers (ordered after the senders' `ready` events), records `done`;
+// after barrier 2 each sender's stream waits on its receivers' `done`, so
+// later writes to a send buffer cannot overtake a pending pull.
+class LocalComm final : public Comm {
+ public:
+  LocalComm(std::shared_ptr<LocalGroup> g, int r, int device) : g_(std::move(g)) {
+    rank = r;
+    size = g_->size();
+    auto& sl = g_->slots[r];
+    sl.device = device;
+    CFD_HIP(hipSetDevice(device));
+    CFD_HIP(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+    CFD_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  }
+
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    auto& me = g_->slots[rank];
+    me.posted = msgs;
+    CFD_HIP(hipEventRecord(me.ready, s));
+    g_->barrier();
+    std::vector<int> used(size, 0);
+    std::vector<char> senders(size, 0);
+    for (const Msg& m : msgs) {
+      if (!m.rbytes) continue;
+      const auto& src = g_->slots[m.peer];
+      // k-th receive from peer q <-> k-th send of q to this rank
+      int k = used[m.peer]++;
+      const Msg* match = nullptr;
+      for (const Msg& sm : src.posted) {
+        if (sm.peer != rank || !sm.sbytes) continue;
+        if (k-- == 0) {
+          match = &sm;
+          break;
+        }
+      }
+      if (!match || match->sbytes != m.rbytes)
+        throw std::logic_error("LocalComm: unmatched transfer " + std::to_string(m.peer) + " -> " +
+                               std::to_string(rank));
+      if (!senders[m.peer]) {
+        CFD_HIP(hipStreamWaitEvent(s, src.ready, 0));
+        senders[m.peer] = 1;
+      }
+      if (src.device == me.device)
+        CFD_HIP(hipMemcpyAsync(m.rbuf, match->sbuf, m.rbytes, hipMemcpyDeviceToDevice, s));
+      else
+        CFD_HIP(hipMemcpyPeerAsync(m.rbuf, me.device, match->sbuf, src.device, m.rbytes, s));
+    }
+    CFD_HIP(hipEventRecord(me.done, s));
+    g_->barrier();
+    std::vector<char> waited(size, 0);
+    for (const Msg& m : msgs)
+      if (m.sbytes && !waited[m.peer]) {
+        CFD_HIP(hipStreamWaitEvent(s, g_->slots[m.peer].done, 0));
+        waited[m.peer] = 1;
+      }
+  }
+
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    auto& me = g_->slots[rank];
+    me.gather_src = send;
+    CFD_HIP(hipEventRecord(me.ready, s));
+    g_->barrier();
+    for (int q = 0; q < size; ++q) {
+      const auto& src = g_->slots[q];
+      if (q != rank) CFD_HIP(hipStreamWaitEvent(s, src.ready, 0));
+      char* dst = static_cast<char*>(recv) + (size_t)q * bytes;
+      if (src.device == me.device)
+        CFD_HIP(hipMemcpyAsync(dst, src.gather_src, bytes, hipMemcpyDeviceToDevice, s));
+      else
+        CFD_HIP(hipMemcpyPeerAsync(dst, me.device, src.gather_src, src.device, bytes, s));
+    }
+    CFD_HIP(hipEventRecord(me.done, s));
+    g_->barrier();
+    for (int q = 0; q < size; ++q)
+      if (q != rank) CFD_HIP(hipStreamWaitEvent(s, g_->slots[q].done, 0));
+  }
+
+ private:
+  std::shared_ptr<LocalGroup> g_;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank, int device) {
+  return std::make_unique<LocalComm>(std::move(g), rank, device);
+}
+
+}  // namespace cfd2

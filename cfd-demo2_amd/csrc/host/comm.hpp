@@ -1,0 +1,82 @@
+// Communication layer of the distributed solver.
+//
+// A rank exchanges halos with its slab neighbours and all-gathers small
+// vectors of per-rank partial sums.  Every operation is stream-ordered on the
+// caller's HIP stream.  Two transports:
+//   RcclComm  -- one process per GPU, RCCL point-to-point + all-gather over
+//                xGMI (the production path; torch.distributed's "nccl" is RCCL).
+//   LocalComm -- several ranks in ONE process (one host thread per rank, any
+//                devices, including all on one GPU): peer copies ordered by HIP
+//                events.  Used by cfd_group_* and by the single-GPU parity
+//                tests of the distributed algorithm (RCCL refuses two ranks on
+//                one device).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+namespace cfd2 {
+
+struct RcclError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// One point-to-point transfer with `peer`: send sbytes from sbuf (if > 0),
+// receive rbytes into rbuf (if > 0).  Transfers with the same peer are matched
+// in list order, send k of one side with receive k of the other.
+struct Msg {
+  int peer;
+  const void* sbuf;
+  size_t sbytes;
+  void* rbuf;
+  size_t rbytes;
+};
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  int rank = 0, size = 1;
+  virtual void exchange(const std::vector<Msg>& msgs, hipStream_t s) = 0;
+  // recv[r * bytes ...] = rank r's send (bytes each), all ranks
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // Variable-size in-place all-gather: every rank's piece [off[r], off[r+1]) of
+  // buf (bytes) is distributed to all ranks.
+  void allgatherv_inplace(void* buf, const std::vector<size_t>& off, hipStream_t s);
+};
+
+// ---- RCCL ----
+constexpr int kUniqueIdBytes = 128;
+void rccl_unique_id(uint8_t out[kUniqueIdBytes]);
+std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUniqueIdBytes]);
+
+// ---- in-process group ----
+class LocalGroup {
+ public:
+  explicit LocalGroup(int n);
+  ~LocalGroup();
+  int size() const { return n_; }
+  void barrier();
+  struct Slot {
+    std::vector<Msg> posted;
+    const void* gather_src = nullptr;
+    hipEvent_t ready = nullptr, done = nullptr;
+    int device = 0;
+  };
+  std::vector<Slot> slots;
+
+ private:
+  int n_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  uint64_t gen_ = 0;
+};
+
+std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank, int device);
+
+}  // namespace cfd2

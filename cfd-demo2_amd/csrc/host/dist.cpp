@@ -1,0 +1,67 @@
+#include "dist.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace cfd2 {
+
+std::vector<uint64_t> partition_starts(uint64_t n, int R) {
+  if (R < 1) throw std::invalid_argument("nranks must be >= 1");
+  if ((uint64_t)R > n) throw std::invalid_argument("more ranks than cells");
+  std::vector<uint64_t> s(R + 1);
+  for (int r = 0; r <= R; ++r) s[r] = n * (uint64_t)r / (uint64_t)R;
+  return s;
+}
+
+int owner_of(const std::vector<uint64_t>& starts, uint64_t g) {
+  return (int)(std::upper_bound(starts.begin(), starts.end(), g) - starts.begin()) - 1;
+}
+
+uint32_t collect_ghosts(uint64_t c0, uint64_t c1, const uint32_t* row, uint32_t n, const uint32_t* col,
+                        std::vector<uint32_t>& ghost) {
+  ghost.clear();
+  for (uint64_t k = row[0]; k < row[n]; ++k)
+    if (col[k] < c0 || col[k] >= c1) ghost.push_back(col[k]);
+  std::sort(ghost.begin(), ghost.end());
+  ghost.erase(std::unique(ghost.begin(), ghost.end()), ghost.end());
+  return (uint32_t)(std::lower_bound(ghost.begin(), ghost.end(), (uint32_t)c0) - ghost.begin());
+}
+
+HaloPlan build_halo_plan(const std::vector<uint64_t>& starts, int rank, const uint32_t* row, uint32_t n,
+                         const uint32_t* col, const std::vector<uint32_t>& ghost, uint32_t glo, uint32_t npad) {
+  const int R = (int)starts.size() - 1;
+  const uint64_t c0 = starts[rank];
+  std::vector<std::vector<int32_t>> send(R);
+  for (uint32_t li = 0; li < n; ++li) {
+    int last = -1;
+    for (uint64_t k = row[li]; k < row[li + 1]; ++k) {
+      const uint32_t g = col[k];
+      if (g >= c0 && g < starts[rank + 1]) continue;
+      const int q = owner_of(starts, g);
+      if (q == last) continue;  // columns ascend: same-peer runs are contiguous
+      auto& v = send[q];
+      if (v.empty() || v.back() != (int32_t)li) v.push_back((int32_t)li);
+      last = q;
+    }
+  }
+  HaloPlan P;
+  for (int q = 0; q < R; ++q) {
+    if (q == rank) continue;
+    const auto lo = std::lower_bound(ghost.begin(), ghost.end(), (uint32_t)starts[q]);
+    const auto hi = std::lower_bound(ghost.begin(), ghost.end(), (uint32_t)starts[q + 1]);
+    const uint32_t rc = (uint32_t)(hi - lo);
+    if (rc == 0 && send[q].empty()) continue;
+    HaloPeer h;
+    h.rank = q;
+    const uint32_t k0 = (uint32_t)(lo - ghost.begin());
+    h.recv_rel = k0 < glo ? (int32_t)k0 - (int32_t)glo : (int32_t)(npad + (k0 - glo));
+    h.recv_cnt = rc;
+    h.send_off = (uint32_t)P.send_idx.size();
+    h.send_cnt = (uint32_t)send[q].size();
+    P.send_idx.insert(P.send_idx.end(), send[q].begin(), send[q].end());
+    P.peers.push_back(h);
+  }
+  return P;
+}
+
+}  // namespace cfd2

@@ -1,0 +1,44 @@
+// Slab partition and halo plans of the distributed solver.
+//
+// Rank r owns the contiguous global rows [start(r), start(r+1)), start(r) =
+// floor(n r / R).  The cut-cell mesher numbers cells x-major, so these are
+// vertical slabs and a rank's ghosts come from its slab neighbours.  A rank
+// stores ghosts of lower ranks at local indices [-glo, 0) and of higher ranks
+// at [npad, npad + ghi) (npad = owned rows rounded up to 64), so local order
+// is global order and every row keeps the reference's column order.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace cfd2 {
+
+std::vector<uint64_t> partition_starts(uint64_t n, int R);
+int owner_of(const std::vector<uint64_t>& starts, uint64_t g);
+
+struct HaloPeer {
+  int rank = 0;
+  int32_t recv_rel = 0;   // local index of the first ghost this peer sends
+  uint32_t recv_cnt = 0;
+  uint32_t send_off = 0;  // into HaloPlan::send_idx
+  uint32_t send_cnt = 0;
+};
+
+struct HaloPlan {
+  std::vector<HaloPeer> peers;
+  std::vector<int32_t> send_idx;  // owned local rows, grouped per peer, ascending
+  int32_t* d_send_idx = nullptr;
+  float* d_stage = nullptr;       // pack buffer (send_idx.size() x max comps)
+  int max_comps = 0;
+};
+
+// Ghost list (ascending) of owned rows [c0, c1) whose global CSR pattern is
+// (row[0..n], col); returns glo (ghosts below c0).
+uint32_t collect_ghosts(uint64_t c0, uint64_t c1, const uint32_t* row, uint32_t n, const uint32_t* col,
+                        std::vector<uint32_t>& ghost);
+
+// Halo plan for a symmetric pattern: the rows this rank sends to peer q are its
+// owned rows with a column owned by q (= q's ghosts from this rank).
+HaloPlan build_halo_plan(const std::vector<uint64_t>& starts, int rank, const uint32_t* row, uint32_t n,
+                         const uint32_t* col, const std::vector<uint32_t>& ghost, uint32_t glo, uint32_t npad);
+
+}  // namespace cfd2

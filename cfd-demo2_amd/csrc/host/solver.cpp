@@ -22,17 +22,69 @@ constexpr int kScalBase = 0;   // dsc[0..15]: rhs_norm, resid, inv_resid, wnorm,
 constexpr int kHOff = 16;
 }  // namespace
 
-Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev) : cfg(c), device(dev) {
+template <class T>
+T* Solver::valloc(int comps) {
+  T* base = arena.alloc<T>(vlen * comps + 64);
+  CFD_HIP(hipMemsetAsync(base, 0, (vlen * comps + 64) * sizeof(T), stream));
+  return base + (size_t)shift * comps;
+}
+
+// image of a global per-cell array in this rank's local layout (owned + ghosts)
+void Solver::local_image(const double* g, int comps, std::vector<float>& out) const {
+  out.assign(vlen * comps, 0.0f);
+  auto put = [&](size_t local, uint64_t gid) {
+    for (int c = 0; c < comps; ++c) out[local * comps + c] = (float)g[gid * comps + c];
+  };
+  for (uint32_t li = 0; li < N; ++li) put(shift + li, (uint64_t)topo.c0 + li);
+  for (uint32_t k = 0; k < topo.glo; ++k) put(shift - topo.glo + k, topo.ghost[k]);
+  for (uint32_t k = 0; k < topo.ghi; ++k) put(shift + topo.npad + k, topo.ghost[topo.glo + k]);
+}
+
+void Solver::make_plan_buffers(HaloPlan& p, int max_comps) {
+  p.d_send_idx = arena.upload(p.send_idx, stream);
+  p.max_comps = max_comps;
+  p.d_stage = arena.alloc<float>(p.send_idx.size() * (size_t)max_comps + 1);
+}
+
+Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::unique_ptr<Comm> cm)
+    : cfg(c), device(dev) {
   if (cfg.max_restart < 1 || cfg.max_restart > 63) throw std::invalid_argument("max_restart must be 1..63");
   m = cfg.max_restart;
   m1 = m + 1;
-  build_topology(mesh, topo);
+  NG = mesh.num_cells;
+  if (cm && cm->size > 1) {
+    comm = std::move(cm);
+    R = comm->size;
+    rk = comm->rank;
+  }
+  starts = partition_starts(NG, R);
+  build_topology(mesh, topo, (uint32_t)starts[rk], (uint32_t)starts[rk + 1]);
   N = topo.N;
   F = topo.F;
   nchunks = (N + kRedChunkCells - 1) / kRedChunkCells;
+  shift = (topo.glo + 63) & ~63u;
+  vlen = (size_t)shift + topo.npad + topo.ghi;
   CFD_HIP(hipSetDevice(device));
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  const size_t Nz = N;
+  if (dist()) {
+    cell_plan = build_halo_plan(starts, rk, topo.srow.data(), N, topo.scol.data(), topo.ghost, topo.glo,
+                                topo.npad);
+    make_plan_buffers(cell_plan, 8);
+    build_scalar_pattern(mesh, gpattern);
+    red_local = arena.alloc<float>(m1 + 1);
+    red_gather = arena.alloc<float>((size_t)R * (m1 + 1));
+    red_comb = arena.alloc<float>(m1 + 1);
+    mx_gather = arena.alloc<uint32_t>(2 * (size_t)R);
+    ev_gather = arena.alloc<double>(5 * (size_t)R);
+    // check_evolution's stride bug reads records (i >> 2) of the global state
+    ev_a = (uint64_t)topo.c0 >> 2;
+    ev_b = (((uint64_t)topo.c1 - 1) >> 2) + 1;
+    const size_t ne = ev_b - ev_a;
+    evrec.u = arena.alloc<float2>(ne);
+    evrec.p = arena.alloc<float>(ne);
+    evrec.dp = arena.alloc<float>(ne);
+    evrec.gp = arena.alloc<float2>(ne);
+  }
   // static mesh data
   d_vol = arena.upload(topo.vol, stream);
   fs.other = arena.upload(topo.fs_other, stream);
@@ -55,44 +107,34 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev) : cfg(c)
   d_scol = arena.upload(topo.ell_col, stream);
   d_slen = arena.upload(topo.ell_len, stream);
   d_sdrank = arena.upload(topo.ell_drank, stream);
-  // fields (init/fields.rs:62-139): zero-initialised
+  // fields (init/fields.rs:62-139): zero-initialised, with ghost space
   auto zeros_state = [&](StateView& v) {
-    v.u = arena.alloc<float2>(Nz);
-    v.p = arena.alloc<float>(Nz);
-    v.dp = arena.alloc<float>(Nz);
-    v.gp = arena.alloc<float2>(Nz);
-    CFD_HIP(hipMemsetAsync(v.u, 0, Nz * sizeof(float2), stream));
-    CFD_HIP(hipMemsetAsync(v.p, 0, Nz * sizeof(float), stream));
-    CFD_HIP(hipMemsetAsync(v.dp, 0, Nz * sizeof(float), stream));
-    CFD_HIP(hipMemsetAsync(v.gp, 0, Nz * sizeof(float2), stream));
+    v.u = valloc<float2>(1);
+    v.p = valloc<float>(1);
+    v.dp = valloc<float>(1);
+    v.gp = valloc<float2>(1);
   };
   for (auto& r : ring) zeros_state(r);
   zeros_state(prev);
-  dp_scratch = arena.alloc<float>(Nz);
-  gp_scratch = arena.alloc<float2>(Nz);
-  const size_t slots_f = (size_t)topo.wf * Nz, slots_s = (size_t)topo.ws * Nz;
+  dp_scratch = valloc<float>(1);
+  gp_scratch = valloc<float2>(1);
+  const size_t slots_f = (size_t)topo.wf * N, slots_s = (size_t)topo.ws * N;
   flux_s = arena.alloc<float>(slots_f);
   CFD_HIP(hipMemsetAsync(flux_s, 0, slots_f * sizeof(float), stream));
-  grad_u = arena.alloc<float2>(Nz);
-  grad_v = arena.alloc<float2>(Nz);
-  CFD_HIP(hipMemsetAsync(grad_u, 0, Nz * sizeof(float2), stream));
-  CFD_HIP(hipMemsetAsync(grad_v, 0, Nz * sizeof(float2), stream));
+  grad_u = valloc<float2>(1);
+  grad_v = valloc<float2>(1);
   cval_a = arena.alloc<float2>(slots_s);
   cval_g = arena.alloc<float2>(slots_s);
   CFD_HIP(hipMemsetAsync(cval_a, 0, slots_s * sizeof(float2), stream));
   CFD_HIP(hipMemsetAsync(cval_g, 0, slots_s * sizeof(float2), stream));
-  cdiag2 = arena.alloc<float2>(Nz);
-  CFD_HIP(hipMemsetAsync(cdiag2, 0, Nz * sizeof(float2), stream));
+  cdiag2 = arena.alloc<float2>(N);
+  CFD_HIP(hipMemsetAsync(cdiag2, 0, N * sizeof(float2), stream));
   sval = arena.alloc<float>(slots_s);
   CFD_HIP(hipMemsetAsync(sval, 0, slots_s * sizeof(float), stream));
-  rhs = arena.alloc<float>(3 * Nz);
-  x = arena.alloc<float>(3 * Nz);
-  CFD_HIP(hipMemsetAsync(rhs, 0, 3 * Nz * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(x, 0, 3 * Nz * sizeof(float), stream));
-  dinv_uv = arena.alloc<float>(Nz);
-  dinv_p = arena.alloc<float>(Nz);
-  CFD_HIP(hipMemsetAsync(dinv_uv, 0, Nz * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(dinv_p, 0, Nz * sizeof(float), stream));
+  rhs = valloc<float>(3);
+  x = valloc<float>(3);
+  dinv_uv = valloc<float>(1);
+  dinv_p = valloc<float>(1);
   partial_d = arena.alloc<double>(5 * (size_t)nchunks + 5);
   maxbits = arena.alloc<uint32_t>(4);
   blockmax = arena.alloc<uint32_t>(2 * (((size_t)N + 255) / 256) + 2);
@@ -142,42 +184,50 @@ CoupledMatrix Solver::cmat() const {
 }
 
 // ---------------------------------------------------------------- state API
+// set_u / set_p take the GLOBAL per-cell arrays; a distributed rank keeps its
+// owned cells and ghosts.  Getters return the owned cells.
 void Solver::set_u(const double* uv) {  // solver.rs:9-21 (clobbers the whole state)
-  std::vector<float2> u(N);
-  for (uint32_t i = 0; i < N; ++i) u[i] = make_float2((float)uv[2 * i], (float)uv[2 * i + 1]);
+  CFD_HIP(hipSetDevice(device));
+  std::vector<float> img;
+  local_image(uv, 2, img);
   StateView& s = S();
-  CFD_HIP(hipMemcpyAsync(s.u, u.data(), N * sizeof(float2), hipMemcpyHostToDevice, stream));
-  CFD_HIP(hipMemsetAsync(s.p, 0, N * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(s.dp, 0, N * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(s.gp, 0, N * sizeof(float2), stream));
+  CFD_HIP(hipMemcpyAsync(vbase(s.u, 1), img.data(), vlen * sizeof(float2), hipMemcpyHostToDevice, stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.p, 1), 0, vlen * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.dp, 1), 0, vlen * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.gp, 1), 0, vlen * sizeof(float2), stream));
   sync();
 }
 
 void Solver::set_p(const double* pv) {  // solver.rs:23-34
-  std::vector<float> p(N);
-  for (uint32_t i = 0; i < N; ++i) p[i] = (float)pv[i];
+  CFD_HIP(hipSetDevice(device));
+  std::vector<float> img;
+  local_image(pv, 1, img);
   StateView& s = S();
-  CFD_HIP(hipMemsetAsync(s.u, 0, N * sizeof(float2), stream));
-  CFD_HIP(hipMemcpyAsync(s.p, p.data(), N * sizeof(float), hipMemcpyHostToDevice, stream));
-  CFD_HIP(hipMemsetAsync(s.dp, 0, N * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(s.gp, 0, N * sizeof(float2), stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.u, 1), 0, vlen * sizeof(float2), stream));
+  CFD_HIP(hipMemcpyAsync(vbase(s.p, 1), img.data(), vlen * sizeof(float), hipMemcpyHostToDevice, stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.dp, 1), 0, vlen * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(vbase(s.gp, 1), 0, vlen * sizeof(float2), stream));
   sync();
 }
 
-static void copy_state(const StateView& src, StateView& dst, uint32_t N, hipStream_t s) {
-  CFD_HIP(hipMemcpyAsync(dst.u, src.u, N * sizeof(float2), hipMemcpyDeviceToDevice, s));
-  CFD_HIP(hipMemcpyAsync(dst.p, src.p, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-  CFD_HIP(hipMemcpyAsync(dst.dp, src.dp, N * sizeof(float), hipMemcpyDeviceToDevice, s));
-  CFD_HIP(hipMemcpyAsync(dst.gp, src.gp, N * sizeof(float2), hipMemcpyDeviceToDevice, s));
+namespace {
+void copy_state(const StateView& src, StateView& dst, size_t off, size_t n, hipStream_t s) {
+  CFD_HIP(hipMemcpyAsync(dst.u - off, src.u - off, n * sizeof(float2), hipMemcpyDeviceToDevice, s));
+  CFD_HIP(hipMemcpyAsync(dst.p - off, src.p - off, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  CFD_HIP(hipMemcpyAsync(dst.dp - off, src.dp - off, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  CFD_HIP(hipMemcpyAsync(dst.gp - off, src.gp - off, n * sizeof(float2), hipMemcpyDeviceToDevice, s));
 }
+}  // namespace
 
 void Solver::initialize_history() {  // solver.rs:276-294
-  copy_state(ring[i_state], ring[i_old], N, stream);
-  copy_state(ring[i_state], ring[i_old_old], N, stream);
+  CFD_HIP(hipSetDevice(device));
+  copy_state(ring[i_state], ring[i_old], shift, vlen, stream);
+  copy_state(ring[i_state], ring[i_old_old], shift, vlen, stream);
   sync();
 }
 
 void Solver::get_u(double* uv) {
+  CFD_HIP(hipSetDevice(device));
   std::vector<float2> u(N);
   CFD_HIP(hipMemcpyAsync(u.data(), S().u, N * sizeof(float2), hipMemcpyDeviceToHost, stream));
   sync();
@@ -188,6 +238,7 @@ void Solver::get_u(double* uv) {
 }
 
 void Solver::get_p(double* out) {
+  CFD_HIP(hipSetDevice(device));
   std::vector<float> p(N);
   CFD_HIP(hipMemcpyAsync(p.data(), S().p, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
@@ -195,10 +246,64 @@ void Solver::get_p(double* out) {
 }
 
 void Solver::get_d_p(double* out) {
+  CFD_HIP(hipSetDevice(device));
   std::vector<float> p(N);
   CFD_HIP(hipMemcpyAsync(p.data(), S().dp, N * sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   for (uint32_t i = 0; i < N; ++i) out[i] = p[i];
+}
+
+// ------------------------------------------------------------ distribution
+// Halo exchange of per-cell fields over `plan`: pack the rows the peers need,
+// then one grouped transfer per (peer, field) straight into the ghost slots.
+void Solver::halo(HaloPlan& plan, std::initializer_list<HField> fields) {
+  if (!dist()) return;
+  const uint32_t ns = (uint32_t)plan.send_idx.size();
+  PackArgs pa{};
+  int tot = 0;
+  for (const HField& f : fields) {
+    if (pa.nf == 8) throw std::logic_error("halo: too many fields");
+    pa.f[pa.nf++] = PackField{f.ptr, f.comps, (uint32_t)((size_t)ns * tot)};
+    tot += f.comps;
+  }
+  if (tot > plan.max_comps) throw std::logic_error("halo: stage buffer too small");
+  pa.idx = plan.d_send_idx;
+  pa.n = ns;
+  pa.stage = plan.d_stage;
+  launch_pack(pa, stream);
+  std::vector<Msg> msgs;
+  for (const HaloPeer& h : plan.peers) {
+    for (int f = 0; f < pa.nf; ++f) {
+      const PackField& F = pa.f[f];
+      Msg mm;
+      mm.peer = h.rank;
+      mm.sbuf = plan.d_stage + F.stage_off + (size_t)h.send_off * F.comps;
+      mm.sbytes = (size_t)h.send_cnt * F.comps * sizeof(float);
+      mm.rbuf = const_cast<float*>(F.src) + (ptrdiff_t)h.recv_rel * F.comps;
+      mm.rbytes = (size_t)h.recv_cnt * F.comps * sizeof(float);
+      msgs.push_back(mm);
+    }
+  }
+  comm->exchange(msgs, stream);
+}
+
+// ghosts of the current FluidState slot: u, p (all = also d_p, grad_p)
+void Solver::halo_state(bool all) {
+  StateView& s = S();
+  if (all)
+    halo(cell_plan, {{(float*)s.u, 2}, {s.p, 1}, {s.dp, 1}, {(float*)s.gp, 2}});
+  else
+    halo(cell_plan, {{(float*)s.u, 2}, {s.p, 1}});
+}
+
+// Distributed canonical reduction: per-rank stage 2, all-gather, rank-ordered
+// sum; the final kernels then read (combined, np = 1).
+std::pair<const float*, uint32_t> Solver::combine(const float* partial, uint32_t np, int nvec) {
+  if (!dist()) return {partial, np};
+  launch_stage2_multi(partial, np, nvec, red_local, stream);
+  comm->allgather(red_local, red_gather, (size_t)nvec * sizeof(float), stream);
+  launch_rank_combine(red_gather, R, nvec, red_comb, stream);
+  return {red_comb, 1u};
 }
 
 // ------------------------------------------------------------------ kernels
@@ -226,6 +331,8 @@ void Solver::prepare() {
   // commit d_p / grad_p (snapshot semantics): swap the scratch into the slot
   std::swap(S().dp, dp_scratch);
   std::swap(S().gp, gp_scratch);
+  if (dist())  // assemble reads the neighbours' new d_p (and gradients for SOU/QUICK)
+    halo(cell_plan, {{S().dp, 1}, {(float*)S().gp, 2}, {(float*)grad_u, 2}, {(float*)grad_v, 2}});
 }
 
 void Solver::assemble() {
@@ -249,27 +356,26 @@ void Solver::assemble() {
   a.dinv_uv = dinv_uv;
   a.dinv_p = dinv_p;
   launch_assemble(a, stream);
+  if (dist()) halo(cell_plan, {{dinv_uv, 1}});  // the Schur prediction reads neighbours' D_u^-1
 }
 
 void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   if (fgmres_ready) return;
-  const size_t n = 3 * (size_t)N;
-  stride = (n + 63) & ~(size_t)63;  // 256-byte aligned basis rows
-  basis = arena.alloc<float>((size_t)m1 * stride);
-  zvec = arena.alloc<float>((size_t)m * stride);
-  w = arena.alloc<float>(n);
-  // pressure vectors are padded to a multiple of 64 (zeroed): the AMG level-0
-  // kernels process 4 rows per thread with 16-byte loads
-  const size_t np = ((size_t)N + 63) & ~(size_t)63;
-  temp = arena.alloc<float>(np);
-  temp_p = arena.alloc<float>(np);
-  p_sol = arena.alloc<float>(np);
-  CFD_HIP(hipMemsetAsync(basis, 0, (size_t)m1 * stride * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(zvec, 0, (size_t)m * stride * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(w, 0, n * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(temp, 0, np * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(temp_p, 0, np * sizeof(float), stream));
-  CFD_HIP(hipMemsetAsync(p_sol, 0, np * sizeof(float), stream));
+  // Krylov vectors in the per-cell layout (ghost space: V_j and Z_j are read at
+  // neighbours by the Schur prediction and the SpMV); 256-byte aligned slots
+  stride = (3 * vlen + 63) & ~(size_t)63;
+  float* braw = arena.alloc<float>((size_t)m1 * stride + 64);
+  float* zraw = arena.alloc<float>((size_t)m * stride + 64);
+  CFD_HIP(hipMemsetAsync(braw, 0, ((size_t)m1 * stride + 64) * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(zraw, 0, ((size_t)m * stride + 64) * sizeof(float), stream));
+  basis = braw + 3 * (size_t)shift;
+  zvec = zraw + 3 * (size_t)shift;
+  w = valloc<float>(3);
+  // pressure vectors: padded to a multiple of 64 owned rows (the AMG level-0
+  // kernels process 4 rows per thread with 16-byte loads), plus ghosts
+  temp = valloc<float>(1);
+  temp_p = valloc<float>(1);
+  p_sol = valloc<float>(1);
   partial = arena.alloc<float>((size_t)m1 * nchunks);
   partial_n = arena.alloc<float>(nchunks);
   const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
@@ -286,124 +392,228 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   fgmres_ready = true;
 }
 
+namespace {
+
+// Device image of rows [r0, r0 + n) of the level matrix A (global numbering),
+// off-diagonal columns mapped to local indices by `rel`; see AmgLevelDev.
+template <class Rel>
+void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel& G, DeviceArena& arena,
+                 hipStream_t stream) {
+  const uint32_t st = (n + 63) & ~63u;  // padded row count (16-byte row groups)
+  int wmax = 0;
+  bool small_delta = true;
+  std::vector<uint8_t> len(st, 0), drank(st, 0);
+  std::vector<float> dv(st, 0.0f), de(st, 1.0f);
+  uint64_t nnz = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t gi = r0 + i;
+    uint32_t off = 0, dr = 0;
+    bool has = false;
+    float diag = 1.0f, raw = 0.0f;
+    for (uint32_t k = A.row[gi]; k < A.row[gi + 1]; ++k) {
+      const uint32_t c = A.col[k];
+      if (c == gi) {
+        has = true;
+        raw = A.val[k];
+        diag = raw;
+        dr = off;
+      } else {
+        ++off;
+        const int64_t d = (int64_t)rel(c) - (int64_t)i;
+        if (d < -32768 || d > 32767) small_delta = false;
+      }
+    }
+    nnz += A.row[gi + 1] - A.row[gi];
+    if (!has) dr = off;  // no diagonal entry: raw diag contributes nothing (dv = 0)
+    if (std::fabs(diag) < 1e-14f) diag = 1.0f;  // amg.wgsl:46
+    if (off > 255) throw std::domain_error("AMG level row wider than 255 entries");
+    len[i] = (uint8_t)off;
+    drank[i] = (uint8_t)dr;
+    dv[i] = raw;
+    de[i] = diag;
+    wmax = std::max(wmax, (int)off);
+  }
+  const size_t slots = (size_t)std::max(wmax, 1) * st;
+  std::vector<float> val(slots, 0.0f);
+  std::vector<int16_t> col16(small_delta ? slots : 0, 0);
+  std::vector<int32_t> col32(small_delta ? 0 : slots, 0);
+  for (uint32_t i = 0; i < st; ++i) {
+    uint32_t r = 0;
+    if (i < n) {
+      const uint64_t gi = r0 + i;
+      for (uint32_t k = A.row[gi]; k < A.row[gi + 1]; ++k) {
+        const uint32_t c = A.col[k];
+        if (c == gi) continue;
+        const size_t o = (size_t)r * st + i;
+        val[o] = A.val[k];
+        if (small_delta)
+          col16[o] = (int16_t)((int64_t)rel(c) - (int64_t)i);
+        else
+          col32[o] = rel(c);
+        ++r;
+      }
+    }
+    // padding slots / rows: value 0, column = the row itself (allocated, zeroed)
+    if (!small_delta)
+      for (; r < (uint32_t)std::max(wmax, 1); ++r) col32[(size_t)r * st + i] = (int32_t)i;
+  }
+  G.nnz = nnz;
+  G.dev.n = n;
+  G.dev.stride = st;
+  G.dev.w = wmax;
+  G.dev.use16 = small_delta ? 1 : 0;
+  G.dev.val = arena.upload(val, stream);
+  G.dev.col16 = small_delta ? arena.upload(col16, stream) : nullptr;
+  G.dev.col32 = small_delta ? nullptr : arena.upload(col32, stream);
+  G.dev.len = arena.upload(len, stream);
+  G.dev.drank = arena.upload(drank, stream);
+  G.dev.dv = arena.upload(dv, stream);
+  G.dev.de = arena.upload(de, stream);
+}
+
+}  // namespace
+
 // ensure_amg_resources (coupled_solver_fgmres.rs:174-209): read back the live
-// scalar matrix, build the frozen hierarchy on the host, upload it.
+// scalar matrix, build the frozen hierarchy on the host, upload it.  A
+// distributed rank all-gathers the scalar matrix, builds the same partition-
+// aware hierarchy as every other rank, and keeps its rows of the levels with
+// more than CFD_AMG_REPLICATE_ROWS rows (default 32768); the small levels are
+// replicated on every rank.
 void Solver::ensure_amg() {
   if (amg_built) return;
   std::vector<float> ell((size_t)topo.ws * N);
   CFD_HIP(hipMemcpyAsync(ell.data(), sval, ell.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
-  HostCsr A0;
-  A0.rows = A0.cols = N;
-  A0.row = topo.srow;
-  A0.col = topo.scol;
-  A0.val.resize(topo.scol.size());
+  std::vector<float> own(topo.scol.size());
   for (uint32_t i = 0; i < N; ++i)
-    for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k)
-      A0.val[k] = ell[(size_t)(k - topo.srow[i]) * N + i];
-  std::vector<AmgHostLevel> H0 = build_amg_hierarchy(A0, kMaxAmgLevels);
-  levels.clear();
-  for (size_t li = 0; li < H0.size(); ++li) {
-    const AmgHostLevel& L = H0[li];
-    const uint32_t n = (uint32_t)L.A.rows;
-    const uint32_t st = (n + 63) & ~63u;  // padded row count (16-byte row groups)
-    int wmax = 0;
-    bool small_delta = true;
-    std::vector<uint8_t> len(st, 0), drank(st, 0);
-    std::vector<float> dv(st, 0.0f), de(st, 1.0f);
-    for (uint32_t i = 0; i < n; ++i) {
-      uint32_t off = 0, dr = 0;
-      bool has = false;
-      float diag = 1.0f, raw = 0.0f;
-      for (uint32_t k = L.A.row[i]; k < L.A.row[i + 1]; ++k) {
-        const uint32_t c = L.A.col[k];
-        if (c == i) {
-          has = true;
-          raw = L.A.val[k];
-          diag = raw;
-          dr = off;
-        } else {
-          ++off;
-          const int64_t d = (int64_t)c - (int64_t)i;
-          if (d < -32768 || d > 32767) small_delta = false;
-        }
-      }
-      if (!has) dr = off;  // no diagonal entry: raw diag contributes nothing (dv = 0)
-      if (std::fabs(diag) < 1e-14f) diag = 1.0f;  // amg.wgsl:46
-      if (off > 255) throw std::domain_error("AMG level row wider than 255 entries");
-      len[i] = (uint8_t)off;
-      drank[i] = (uint8_t)dr;
-      dv[i] = raw;
-      de[i] = diag;
-      wmax = std::max(wmax, (int)off);
-    }
-    const size_t slots = (size_t)std::max(wmax, 1) * st;
-    std::vector<float> val(slots, 0.0f);
-    std::vector<int16_t> col16(small_delta ? slots : 0, 0);
-    std::vector<uint32_t> col32(small_delta ? 0 : slots, 0);
-    for (uint32_t i = 0; i < st; ++i) {
-      uint32_t r = 0;
-      if (i < n)
-        for (uint32_t k = L.A.row[i]; k < L.A.row[i + 1]; ++k) {
-          const uint32_t c = L.A.col[k];
-          if (c == i) continue;
-          const size_t o = (size_t)r * st + i;
-          val[o] = L.A.val[k];
-          if (small_delta)
-            col16[o] = (int16_t)((int64_t)c - (int64_t)i);
-          else
-            col32[o] = c;
-          ++r;
-        }
-      // padding slots: value 0, column = own row (delta 0; padding rows read x[i],
-      // which is allocated and zero-initialised)
-      if (!small_delta)
-        for (; r < (uint32_t)std::max(wmax, 1); ++r) col32[(size_t)r * st + i] = std::min(i, n - 1);
-    }
-    if (small_delta)  // padding rows must not point past n-1 either
-      for (uint32_t i = n; i < st; ++i)
-        for (int r = 0; r < std::max(wmax, 1); ++r) col16[(size_t)r * st + i] = 0;
-    AmgGpuLevel G;
-    G.nnz = L.A.col.size();
-    G.dev.n = n;
-    G.dev.stride = st;
-    G.dev.w = wmax;
-    G.dev.use16 = small_delta ? 1 : 0;
-    G.dev.val = arena.upload(val, stream);
-    G.dev.col16 = small_delta ? arena.upload(col16, stream) : nullptr;
-    G.dev.col32 = small_delta ? nullptr : arena.upload(col32, stream);
-    G.dev.len = arena.upload(len, stream);
-    G.dev.drank = arena.upload(drank, stream);
-    G.dev.dv = arena.upload(dv, stream);
-    G.dev.de = arena.upload(de, stream);
-    G.dev.nc = L.has_op ? L.nc : 0;
-    if (L.has_op) {
-      std::vector<uint32_t> agg(st, 0);
-      std::copy(L.agg.begin(), L.agg.end(), agg.begin());
-      G.dev.agg = arena.upload(agg, stream);
-      G.dev.r_row = arena.upload(L.r_row, stream);
-      G.dev.r_col = arena.upload(L.r_col, stream);
-    }
-    auto zeroed = [&](size_t cnt) {
-      float* p = arena.alloc<float>(cnt);
-      CFD_HIP(hipMemsetAsync(p, 0, cnt * sizeof(float), stream));
-      return p;
-    };
-    G.xt = zeroed(st);
-    G.r = zeroed(st);
-    if (li > 0) {
-      G.x = zeroed(st);
-      G.b = zeroed(st);
-    }
-    levels.push_back(G);
+    for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k) own[k] = ell[(size_t)(k - topo.srow[i]) * N + i];
+  HostCsr A0;
+  std::vector<AmgHostLevel> H;
+  if (!dist()) {
+    A0.rows = A0.cols = N;
+    A0.row = topo.srow;
+    A0.col = topo.scol;
+    A0.val = std::move(own);
+    H = build_amg_hierarchy(A0, kMaxAmgLevels);
+  } else {
+    // all-gather the matrix values (row order = global order, rank by rank)
+    A0 = gpattern;
+    std::vector<size_t> off(R + 1);
+    for (int q = 0; q <= R; ++q) off[q] = (size_t)A0.row[starts[q]] * sizeof(float);
+    if (off[rk + 1] - off[rk] != own.size() * sizeof(float)) throw std::logic_error("AMG gather: row mismatch");
+    float* dbuf = arena.alloc<float>(A0.col.size());
+    CFD_HIP(hipMemcpyAsync((char*)dbuf + off[rk], own.data(), own.size() * sizeof(float), hipMemcpyHostToDevice,
+                           stream));
+    comm->allgatherv_inplace(dbuf, off, stream);
+    A0.val.resize(A0.col.size());
+    CFD_HIP(hipMemcpyAsync(A0.val.data(), dbuf, A0.col.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
+    sync();
+    H = build_amg_hierarchy(A0, kMaxAmgLevels, starts);
   }
-  // levels from `tail_first` down run inside one single-workgroup kernel
+  const int L = (int)H.size();
+  // distributed levels [0, amg_g): the rest are replicated (all of them on one GPU)
+  amg_g = 0;
+  if (dist()) {
+    const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
+    const uint64_t rep = ev ? std::strtoull(ev, nullptr, 10) : 32768u;
+    amg_g = L;
+    for (int li = 1; li < L; ++li)
+      if (H[li].A.rows <= rep) {
+        amg_g = li;
+        break;
+      }
+  }
+  levels.assign(L, AmgGpuLevel{});
+  auto zeroed = [&](size_t cnt) {
+    float* p = arena.alloc<float>(cnt + 64);
+    CFD_HIP(hipMemsetAsync(p, 0, (cnt + 64) * sizeof(float), stream));
+    return p;
+  };
+  for (int li = 0; li < L; ++li) {
+    const AmgHostLevel& HL = H[li];
+    AmgGpuLevel& G = levels[li];
+    G.nglob = HL.A.rows;
+    G.part = HL.part;
+    G.C0 = HL.part[rk];
+    G.C1 = HL.part[rk + 1];
+    if (li < amg_g) {  // distributed level: owned rows + ghosts
+      G.dist = true;
+      const uint32_t n = (uint32_t)(G.C1 - G.C0);
+      std::vector<uint32_t> ghost;
+      std::vector<uint32_t> lrow(n + 1);
+      for (uint32_t i = 0; i <= n; ++i) lrow[i] = HL.A.row[G.C0 + i] - HL.A.row[G.C0];
+      const uint32_t* lcol = HL.A.col.data() + HL.A.row[G.C0];
+      G.glo = collect_ghosts(G.C0, G.C1, lrow.data(), n, lcol, ghost);
+      G.ghi = (uint32_t)ghost.size() - G.glo;
+      G.npad = (n + 63) & ~63u;
+      const uint64_t C0 = G.C0, C1 = G.C1;
+      const uint32_t glo = G.glo, npad = G.npad;
+      auto rel = [&](uint32_t c) -> int32_t {
+        if (c >= C0 && c < C1) return (int32_t)(c - C0);
+        const auto it = std::lower_bound(ghost.begin(), ghost.end(), c);
+        const uint32_t k = (uint32_t)(it - ghost.begin());
+        return k < glo ? (int32_t)k - (int32_t)glo : (int32_t)(npad + (k - glo));
+      };
+      level_image(HL.A, C0, n, rel, G, arena, stream);
+      G.plan = build_halo_plan(HL.part, rk, lrow.data(), n, lcol, ghost, G.glo, G.npad);
+      make_plan_buffers(G.plan, 1);
+      if (li == 0) {
+        if (G.glo != topo.glo || G.ghi != topo.ghi || G.npad != topo.npad)
+          throw std::logic_error("AMG level 0 ghosts differ from the cell ghosts");
+        G.xt = valloc<float>(1);
+        G.r = valloc<float>(1);
+      } else {
+        const uint32_t sh = (G.glo + 63) & ~63u;
+        const size_t cnt = (size_t)sh + G.npad + G.ghi;
+        G.x = zeroed(cnt) + sh;
+        G.xt = zeroed(cnt) + sh;
+        G.b = zeroed(cnt) + sh;
+        G.r = zeroed(cnt) + sh;
+      }
+    } else {  // replicated (or single-GPU) level, global numbering
+      const uint32_t n = (uint32_t)HL.A.rows;
+      level_image(HL.A, 0, n, [](uint32_t c) { return (int32_t)c; }, G, arena, stream);
+      G.npad = G.dev.stride;
+      G.xt = zeroed(G.npad);
+      G.r = zeroed(G.npad);
+      if (li > 0) {
+        G.x = zeroed(G.npad);
+        G.b = zeroed(G.npad);
+      }
+    }
+    // coarsening operators: P as an aggregate index per stored fine row, R = P^T
+    if (HL.has_op) {
+      const AmgHostLevel& HC = H[li + 1];
+      const bool next_dist = (li + 1 < amg_g);
+      std::vector<uint32_t> agg(G.dev.stride, 0), r_row, r_col;
+      if (G.dist) {
+        const uint64_t cbase = next_dist ? HC.part[rk] : 0;  // replicated next: global ids
+        for (uint64_t i = G.C0; i < G.C1; ++i) agg[i - G.C0] = (uint32_t)(HL.agg[i] - cbase);
+        const uint64_t I0 = HC.part[rk], I1 = HC.part[rk + 1];
+        r_row.resize(I1 - I0 + 1);
+        for (uint64_t I = I0; I <= I1; ++I) r_row[I - I0] = HL.r_row[I] - HL.r_row[I0];
+        r_col.assign(HL.r_col.begin() + HL.r_row[I0], HL.r_col.begin() + HL.r_row[I1]);
+        for (auto& f : r_col) f -= (uint32_t)G.C0;
+        G.dev.nc = (uint32_t)(I1 - I0);
+      } else {
+        std::copy(HL.agg.begin(), HL.agg.end(), agg.begin());
+        r_row = HL.r_row;
+        r_col = HL.r_col;
+        G.dev.nc = HL.nc;
+      }
+      G.dev.agg = arena.upload(agg, stream);
+      G.dev.r_row = arena.upload(r_row, stream);
+      G.dev.r_col = arena.upload(r_col, stream);
+    }
+  }
+  // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
   const uint32_t tail_rows = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 4096u;
-  tail_first = (int)levels.size();
-  while (tail_first > 1 && levels[tail_first - 1].dev.n <= tail_rows) --tail_first;
-  std::vector<AmgTailLevel> tl(levels.size());
-  for (size_t li = 0; li < levels.size(); ++li) {
+  const int lo = std::max(amg_g, 1);
+  tail_first = L;
+  while (tail_first > lo && levels[tail_first - 1].dev.n <= tail_rows) --tail_first;
+  std::vector<AmgTailLevel> tl(L);
+  for (int li = 0; li < L; ++li) {
     tl[li].L = levels[li].dev;
     tl[li].x = levels[li].x;
     tl[li].xt = levels[li].xt;
@@ -444,30 +654,56 @@ void Solver::amg_smooth(size_t li, float*& xcur, const float* b) {
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
 
-// amg.rs:666-770, level 0 bound to (x = p_sol, b = temp_p).  Levels below
-// `tail_first` (all small) run as one single-workgroup kernel (k_amg_tail).
+// amg.rs:666-770, level 0 bound to (x = p_sol, b = temp_p).  Replicated levels
+// from `tail_first` on run as one single-workgroup kernel (k_amg_tail).  On a
+// distributed rank the levels below amg_g are row-partitioned: each smoother
+// input gets a halo (the cleared coarse x needs none), the restriction into
+// the first replicated level is all-gathered.
 void Solver::v_cycle() {
   const int L = (int)levels.size();
   levels[0].x = p_sol;
   levels[0].b = temp_p;
+  const int D = dist() ? amg_g : 0;
   // the tail needs level >= 1 (level 0's x/b are bound per call) and is off
   // while the level-0 smoother is being timed on a one-level hierarchy
-  const int tf = (prof && L == 1) ? L : std::max(tail_first, 1);
+  const int tf = (prof && L == 1) ? L : std::max({tail_first, 1, D});
   const int down = std::min(tf, L - 1);
+  auto hx = [&](int i) {
+    if (levels[i].dist) halo(levels[i].plan, {{levels[i].x, 1}});
+  };
+  if (D > 0) hx(0);
   for (int i = 0; i < down; ++i) {
-    amg_smooth(i, levels[i].x, levels[i].b);
-    launch_amg_residual(levels[i].dev, levels[i].x, levels[i].b, levels[i].r, stream);
-    launch_amg_restrict(levels[i].dev, levels[i].r, levels[i + 1].b, levels[i + 1].x, stream);
+    AmgGpuLevel& Lv = levels[i];
+    amg_smooth(i, Lv.x, Lv.b);
+    hx(i);
+    launch_amg_residual(Lv.dev, Lv.x, Lv.b, Lv.r, stream);
+    AmgGpuLevel& C = levels[i + 1];
+    if (!Lv.dist) {
+      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream);
+    } else if (C.dist) {
+      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, C.npad, C.glo, C.ghi, stream);
+    } else {  // into the first replicated level: own slice, clear all, all-gather
+      launch_amg_restrict(Lv.dev, Lv.r, C.b + C.C0, C.x + C.C0, Lv.dev.nc, (uint32_t)C.C0,
+                          (uint32_t)(C.nglob - C.C1), stream);
+      std::vector<size_t> off(R + 1);
+      for (int q = 0; q <= R; ++q) off[q] = C.part[q] * sizeof(float);
+      comm->allgatherv_inplace(C.b, off, stream);
+    }
   }
   if (tf < L) {
     launch_amg_tail(d_tail, tf, L, stream);
   } else {
-    for (int s = 0; s < 10; ++s) amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
+    for (int s = 0; s < 10; ++s) {
+      if (s > 0) hx(L - 1);
+      amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
+    }
   }
   for (int ii = down - 1; ii >= 0; --ii) {
     launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
+    hx(ii);
     amg_smooth(ii, levels[ii].x, levels[ii].b);
   }
+  if (D > 0) hx(0);  // the velocity correction reads neighbours' p_sol
   // every level performs an even number of sweeps, so level 0 ends in p_sol
   if (levels[0].x != p_sol) throw std::logic_error("AMG level-0 ping-pong parity");
 }
@@ -476,28 +712,32 @@ void Solver::v_cycle() {
 void Solver::precondition(int j, float* z) {
   const CoupledMatrix A = cmat();
   const bool jacobi = constants.precond_type != 1;
-  const float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
+  float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
+  if (dist()) halo(cell_plan, {{v, 3}});  // the prediction reads neighbours' r_u, r_v
   launch_precond_predict(A, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
   bool in_sol = true;
   if (!jacobi) {
     v_cycle();
   } else {
-    const size_t raw = 20u + (size_t)std::sqrt((float)N) / 2u;
+    // p_iters of coupled_solver_fgmres.rs:1949-1976 (global cell count)
+    const size_t raw = 20u + (size_t)std::sqrt((float)NG) / 2u;
     const size_t p_iters = std::min<size_t>(raw, 200) == 0 ? 0 : std::min<size_t>(raw, 200) - 1;
     for (size_t it = 0; it < p_iters; ++it) {
-      if (in_sol)
-        launch_relax_pressure(N, topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, p_sol, temp, stream);
-      else
-        launch_relax_pressure(N, topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, temp, p_sol, stream);
+      float* src = in_sol ? p_sol : temp;
+      float* dst = in_sol ? temp : p_sol;
+      if (dist()) halo(cell_plan, {{src, 1}});
+      launch_relax_pressure(N, topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
       in_sol = !in_sol;
     }
+    if (dist()) halo(cell_plan, {{in_sol ? p_sol : temp, 1}});
   }
   launch_precond_correct(A, v, binv, j, in_sol ? p_sol : temp, dinv_uv, z, stream);
 }
 
 float Solver::norm_blocking(const float* v, int mode, int slot) {
   launch_dot_partial(v, v, N, partial_n, stream);
-  launch_reduce_final(partial_n, nchunks, mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
+  const auto red = combine(partial_n, nchunks, 1);
+  launch_reduce_final(red.first, red.second, mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
   CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   return h_pin[0];
@@ -508,6 +748,7 @@ float Solver::norm_blocking(const float* v, int mode, int slot) {
 // g = [||r||, 0, ...] (coupled_solver_fgmres.rs:1880-1890, 2380-2392).
 float Solver::residual_into_v0_blocking() {
   CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
+  if (dist()) halo(cell_plan, {{x, 3}});
   launch_spmv(cmat(), x, w, stream);
   launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
   return norm_blocking(basis, 2, 1);
@@ -549,11 +790,14 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       ++total;
       float* zj = zvec + (size_t)j * stride;
       precondition(j, zj);
+      if (dist()) halo(cell_plan, {{zj, 3}});
       launch_spmv(cmat(), zj, w, stream);
       launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);
-      launch_cgs_reduce(partial, nchunks, j, H, m1, stream);
+      const auto rd = combine(partial, nchunks, j + 1);
+      launch_cgs_reduce(rd.first, rd.second, j, H, m1, stream);
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
-      launch_norm_givens(partial_n, nchunks, j, H, m1, givens, g, binv, resid_hist, stream);
+      const auto rn = combine(partial_n, nchunks, 1);
+      launch_norm_givens(rn.first, rn.second, j, H, m1, givens, g, binv, resid_hist, stream);
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
       if (inner.pending >= 0) {
@@ -626,16 +870,77 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   return st;
 }
 
-// check_evolution (coupled_solver.rs:501-580), statistics on the GPU
+// check_evolution (coupled_solver.rs:501-580), statistics on the GPU.  The
+// stride bug (§0.1-12) makes index i read record i >> 2: a distributed rank
+// first fetches the records [ev_a, ev_b) its indices read from their owners.
 void Solver::check_evolution() {
-  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, partial_d, stream);
+  StateView var = S();
+  uint64_t gbase = 0, rec0 = 0;
+  if (dist()) {
+    std::vector<Msg> msgs;
+    StateView& cur = S();
+    const uint64_t c0 = topo.c0, c1 = topo.c1;
+    auto add = [&](int q, bool send, uint64_t lo, uint64_t hi) {
+      const size_t n = hi - lo;
+      if (send) {  // owned records [lo, hi) to rank q
+        const size_t o = lo - c0;
+        msgs.push_back({q, cur.u + o, n * sizeof(float2), nullptr, 0});
+        msgs.push_back({q, cur.p + o, n * sizeof(float), nullptr, 0});
+        msgs.push_back({q, cur.dp + o, n * sizeof(float), nullptr, 0});
+        msgs.push_back({q, cur.gp + o, n * sizeof(float2), nullptr, 0});
+      } else {  // records [lo, hi) of rank q
+        const size_t o = lo - ev_a;
+        msgs.push_back({q, nullptr, 0, evrec.u + o, n * sizeof(float2)});
+        msgs.push_back({q, nullptr, 0, evrec.p + o, n * sizeof(float)});
+        msgs.push_back({q, nullptr, 0, evrec.dp + o, n * sizeof(float)});
+        msgs.push_back({q, nullptr, 0, evrec.gp + o, n * sizeof(float2)});
+      }
+    };
+    for (int q = 0; q < R; ++q) {
+      const uint64_t qa = starts[q] >> 2, qb = ((starts[q + 1] - 1) >> 2) + 1;  // q's record range
+      // what q reads from me
+      const uint64_t slo = std::max(qa, c0), shi = std::min(qb, c1);
+      // what I read from q
+      const uint64_t rlo = std::max(ev_a, starts[q]), rhi = std::min(ev_b, starts[q + 1]);
+      if (q == rk) {
+        if (rlo < rhi) {
+          const size_t n = rhi - rlo, so = rlo - c0, ro = rlo - ev_a;
+          CFD_HIP(hipMemcpyAsync(evrec.u + ro, cur.u + so, n * sizeof(float2), hipMemcpyDeviceToDevice, stream));
+          CFD_HIP(hipMemcpyAsync(evrec.p + ro, cur.p + so, n * sizeof(float), hipMemcpyDeviceToDevice, stream));
+          CFD_HIP(hipMemcpyAsync(evrec.dp + ro, cur.dp + so, n * sizeof(float), hipMemcpyDeviceToDevice, stream));
+          CFD_HIP(hipMemcpyAsync(evrec.gp + ro, cur.gp + so, n * sizeof(float2), hipMemcpyDeviceToDevice, stream));
+        }
+        continue;
+      }
+      if (slo < shi) add(q, true, slo, shi);
+      if (rlo < rhi) add(q, false, rlo, rhi);
+    }
+    comm->exchange(msgs, stream);
+    var = evrec;
+    gbase = topo.c0;
+    rec0 = ev_a;
+  }
+  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, stream);
   double* out5 = partial_d + 5 * (size_t)nchunks;
   launch_evolution_final(partial_d, nchunks, out5, stream);
   double tot[5];
-  CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
-  copy_state(S(), prev, N, stream);
-  sync();
-  const double nn = (double)N;
+  if (dist()) {
+    std::vector<double> gth(5 * (size_t)R);
+    comm->allgather(out5, ev_gather, 5 * sizeof(double), stream);
+    CFD_HIP(hipMemcpyAsync(gth.data(), ev_gather, gth.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
+    copy_state(S(), prev, 0, N, stream);
+    sync();
+    for (int f = 0; f < 5; ++f) {  // rank-ordered combine
+      double acc = 0.0;
+      for (int q = 0; q < R; ++q) acc += gth[5 * (size_t)q + f];
+      tot[f] = acc;
+    }
+  } else {
+    CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
+    copy_state(S(), prev, 0, N, stream);
+    sync();
+  }
+  const double nn = (double)NG;
   const double mean_u = tot[1] / nn, mean_v = tot[2] / nn;
   const double var_u = std::fmax(tot[3] / nn - mean_u * mean_u, 0.0);
   const double var_v = std::fmax(tot[4] / nn - mean_v * mean_v, 0.0);
@@ -659,8 +964,10 @@ void Solver::check_evolution() {
 }
 
 void Solver::step() {  // coupled_solver.rs:33-499
+  CFD_HIP(hipSetDevice(device));
   rotate();
   constants.component = 0;
+  if (dist()) halo_state(true);  // the rotated slot's ghosts (last written 3 steps ago)
   prepare();
   const bool fixed = cfg.fixed_outer > 0;
   const int max_iters = fixed ? cfg.fixed_outer : std::max(cfg.n_outer_correctors, 10);
@@ -678,6 +985,11 @@ void Solver::step() {  // coupled_solver.rs:33-499
     info.total_linear_iterations += ls.iterations;
     if (std::isnan(ls.residual)) throw std::domain_error("Coupled Linear Solver Diverged: NaN detected in linear residual");
     launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, blockmax, maxbits, stream);
+    if (dist()) {
+      halo_state(false);  // the next prepare reads neighbours' u, p
+      comm->allgather(maxbits, mx_gather, 2 * sizeof(uint32_t), stream);
+      launch_max_combine(mx_gather, R, maxbits, stream);
+    }
     if (iter == 0) {
       info.outer_residual_u = std::numeric_limits<float>::max();
       info.outer_residual_p = std::numeric_limits<float>::max();
@@ -731,6 +1043,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
 
 // ------------------------------------------------------------------ debug
 void Solver::debug_prepare_assemble(bool asmb) {
+  CFD_HIP(hipSetDevice(device));
   constants.component = 0;
   prepare();
   if (asmb) assemble();
@@ -751,6 +1064,9 @@ size_t Solver::debug_len(int id) const {
 }
 
 void Solver::debug_buffer(int id, float* out) {
+  CFD_HIP(hipSetDevice(device));
+  if (dist() && (id == 0 || id == 8 || id == 9))
+    throw std::invalid_argument("debug buffers 0/8/9 use the global face/CSR layout (single GPU only)");
   const size_t n = N;
   auto d2h = [&](void* dst, const void* src, size_t bytes) {
     CFD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream));

@@ -2,13 +2,18 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "../../../include/cfd2_amd.h"
 #include "../hip/kernels.hpp"
+#include "comm.hpp"
+#include "dist.hpp"
 
 namespace cfd2 {
 
@@ -64,7 +69,20 @@ struct HostCsr {
 // factors every face sweep needs), computed once on the host in f32 with the
 // exact operation order of the WGSL expressions they replace.
 struct Topology {
-  uint32_t N = 0, F = 0;
+  uint32_t N = 0, F = 0;  // N = owned cells
+  // distributed view (one GPU: c0 = 0, c1 = NG, no ghosts)
+  uint32_t NG = 0, c0 = 0, c1 = 0;
+  uint32_t npad = 0;           // N rounded up to 64: first upper-ghost local index
+  uint32_t glo = 0, ghi = 0;   // ghosts below c0 / at or above c1
+  std::vector<uint32_t> ghost; // ghost global ids, ascending
+  // signed local index of a global cell id (owned or ghost)
+  int32_t rel(uint32_t g) const {
+    if (g >= c0 && g < c1) return (int32_t)(g - c0);
+    const auto it = std::lower_bound(ghost.begin(), ghost.end(), g);
+    if (it == ghost.end() || *it != g) throw std::logic_error("cell is neither owned nor a ghost");
+    const uint32_t k = (uint32_t)(it - ghost.begin());
+    return k < glo ? (int32_t)k - (int32_t)glo : (int32_t)(npad + (k - glo));
+  }
   int wf = 0;  // max faces per cell
   int ws = 0;  // max scalar row length (incl. diagonal)
   std::vector<float> vol;
@@ -75,13 +93,19 @@ struct Topology {
   std::vector<uint32_t> fs_face;  // host only: face index of each slot
   std::vector<float> fs_area, fs_nx, fs_ny, fs_lam_s, fs_lam_f, fs_dist_a, fs_dist_e, fs_dvx,
       fs_dvy, fs_rx, fs_ry, fs_rox, fs_roy;
-  // scalar CSR (init/mesh.rs:27-53) and its ELL image [r*N + i]
+  // scalar CSR rows of the owned cells (init/mesh.rs:27-53), global columns,
+  // and its ELL image [r*N + i] with signed local columns
   std::vector<uint32_t> srow, scol;
-  std::vector<uint32_t> ell_col, ell_len, ell_drank;
+  std::vector<int32_t> ell_col;
+  std::vector<uint32_t> ell_len, ell_drank;
 };
 
 // Throws std::invalid_argument on inconsistent meshes.
 void build_topology(const cfd_mesh_view& m, Topology& t);
+// Owned range [c0, c1) of a distributed rank, ghosts from the face neighbours.
+void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c1);
+// Global scalar CSR pattern (init/mesh.rs:27-53) of the whole mesh.
+void build_scalar_pattern(const cfd_mesh_view& m, HostCsr& out);
 
 // AMG hierarchy (linear_solver/amg.rs:84-235, 374-595) built on the host.
 struct AmgHostLevel {
@@ -90,16 +114,26 @@ struct AmgHostLevel {
   std::vector<uint32_t> r_row, r_col;  // R = P^T
   uint32_t nc = 0;
   bool has_op = false;
+  std::vector<uint64_t> part;  // row partition starts of this level (one entry per rank + 1)
 };
-std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels);
+std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
+                                               const std::vector<uint64_t>& part = {});
 
 struct AmgGpuLevel {
   AmgLevelDev dev{};
-  float* x = nullptr;   // level solution (level 0: external p_sol)
+  float* x = nullptr;   // level solution (level 0: external p_sol); owned base
   float* xt = nullptr;  // ping-pong partner for the out-of-place smoother
   float* b = nullptr;   // level rhs (level 0: external temp_p)
   float* r = nullptr;   // residual scratch
-  uint64_t nnz = 0;     // including diagonal
+  uint64_t nnz = 0;     // including diagonal (rows this rank stores)
+  uint64_t nglob = 0;   // rows of the whole level
+  // distributed level: owned rows [C0, C1) of the global level, ghosts around
+  bool dist = false;
+  HaloPlan plan;
+  uint32_t glo = 0, ghi = 0, npad = 0;
+  // this rank's rows of the level (replicated level: restriction target range)
+  uint64_t C0 = 0, C1 = 0;
+  std::vector<uint64_t> part;  // row partition of the level over the ranks
 };
 
 struct LagReader {  // async_buffer.rs restated as a deterministic lag model
@@ -114,14 +148,31 @@ struct Solver {
   hipStream_t stream = nullptr;
   DeviceArena arena;
   Topology topo;
-  uint32_t N = 0, F = 0;
+  uint32_t N = 0, F = 0;  // N: cells this rank owns
+  // ---- distribution (one GPU: R = 1, no comm, no ghosts) ----
+  std::unique_ptr<Comm> comm;
+  int R = 1, rk = 0;
+  std::vector<uint64_t> starts;  // cell partition (R + 1)
+  uint32_t NG = 0;               // cells of the whole mesh
+  uint32_t shift = 0;            // owned base offset of every per-cell vector (>= glo, 64-aligned)
+  size_t vlen = 0;               // elements per component of a per-cell vector
+  HaloPlan cell_plan;
+  HostCsr gpattern;              // global scalar pattern (distributed AMG setup)
+  float* red_local = nullptr;    // [m1] this rank's reduction results
+  float* red_gather = nullptr;   // [R * m1]
+  float* red_comb = nullptr;     // [m1]
+  uint32_t* mx_gather = nullptr; // [2R]
+  double* ev_gather = nullptr;   // [5R]
+  StateView evrec{};             // check_evolution records fetched from their owners
+  uint64_t ev_a = 0, ev_b = 0;   // record range [ev_a, ev_b) this rank's variance reads
+  int amg_g = 0;                 // first replicated AMG level (distributed)
   int m = 50, m1 = 51;
   uint32_t nchunks = 0;
 
   // static device data
   FaceSlots fs{};
   float* d_vol = nullptr;
-  uint32_t* d_scol = nullptr;
+  int32_t* d_scol = nullptr;
   uint32_t* d_slen = nullptr;
   uint32_t* d_sdrank = nullptr;
   // ring of 3 FluidState slots (SoA) + prepare's d_p / grad_p scratch
@@ -185,7 +236,8 @@ struct Solver {
   double prof_ms = 0.0;
   uint64_t prof_launches = 0;
 
-  Solver(const cfd_mesh_view& mesh, const cfd_config& cfg, int device);
+  Solver(const cfd_mesh_view& mesh, const cfd_config& cfg, int device,
+         std::unique_ptr<Comm> comm = nullptr);
   ~Solver();
   StateView& S() { return ring[i_state]; }
 
@@ -197,6 +249,7 @@ struct Solver {
   void get_p(double* p);
   void get_d_p(double* dp);
   void debug_prepare_assemble(bool assemble);
+  void get_global_ids(uint32_t* c0, uint32_t* c1) const { *c0 = topo.c0; *c1 = topo.c1; }
   size_t debug_len(int id) const;
   void debug_buffer(int id, float* out);
   double algorithmic_step_bytes() const;
@@ -217,6 +270,23 @@ struct Solver {
   void check_evolution();
   void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
   CoupledMatrix cmat() const;
+  // per-cell vectors: allocation with ghost space, owned-base pointers
+  template <class T>
+  T* valloc(int comps);
+  template <class T>
+  T* vbase(T* p, int comps) const { return p - (size_t)shift * comps; }
+  void local_image(const double* global, int comps, std::vector<float>& out) const;
+  // distributed plumbing
+  bool dist() const { return R > 1; }
+  struct HField {
+    float* ptr;
+    int comps;
+  };
+  void halo(HaloPlan& plan, std::initializer_list<HField> fields);
+  void halo_state(bool all);
+  std::pair<const float*, uint32_t> combine(const float* partial, uint32_t np, int nvec);
+  void make_plan_buffers(HaloPlan& p, int max_comps);
+  void build_dist_amg(std::vector<AmgHostLevel>& H);
 };
 
 }  // namespace cfd2

@@ -21,104 +21,158 @@ inline float wdistance(float ax, float ay, float bx, float by) {
 }
 }  // namespace
 
-void build_topology(const cfd_mesh_view& m, Topology& t) {
-  const uint32_t N = m.num_cells, F = m.num_faces;
-  if (N == 0) throw std::invalid_argument("mesh has no cells");
-  t.N = N;
-  t.F = F;
-  const uint32_t NONE = 0xFFFFFFFFu;
+void build_topology(const cfd_mesh_view& m, Topology& t) { build_topology(m, t, 0, m.num_cells); }
 
-  // f32 geometry (init/mesh.rs:93-155)
-  std::vector<float> cx(N), cy(N);
-  t.vol.resize(N);
-  for (uint32_t i = 0; i < N; ++i) {
-    cx[i] = (float)m.cell_cx[i];
-    cy[i] = (float)m.cell_cy[i];
-    t.vol[i] = (float)m.cell_vol[i];
-  }
-
-  // scalar CSR (init/mesh.rs:27-53): neighbours + diagonal, sorted, deduplicated
-  std::vector<uint32_t> deg(N + 1, 1);
+void build_scalar_pattern(const cfd_mesh_view& m, HostCsr& out) {  // init/mesh.rs:27-53
+  const uint32_t N = m.num_cells, F = m.num_faces, NONE = 0xFFFFFFFFu;
+  std::vector<uint32_t> aoff(N + 1, 0);
+  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] = 1;
+  for (uint32_t f = 0; f < F; ++f)
+    if (m.face_neighbor[f] != NONE) {
+      aoff[m.face_owner[f] + 1]++;
+      aoff[m.face_neighbor[f] + 1]++;
+    }
+  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] += aoff[i];
+  std::vector<uint32_t> adj(aoff[N]);
+  std::vector<uint32_t> pos(aoff.begin(), aoff.end() - 1);
+  for (uint32_t i = 0; i < N; ++i) adj[pos[i]++] = i;
   for (uint32_t f = 0; f < F; ++f) {
     const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
-    if (o >= N) throw std::invalid_argument("face_owner out of range");
-    if (n != NONE) {
-      if (n >= N) throw std::invalid_argument("face_neighbor out of range");
-      deg[o]++;
-      deg[n]++;
-    }
+    if (n == NONE) continue;
+    adj[pos[o]++] = n;
+    adj[pos[n]++] = o;
   }
-  std::vector<uint32_t> aoff(N + 1, 0);
-  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] = aoff[i] + deg[i];
-  std::vector<uint32_t> adj(aoff[N]);
-  {
-    std::vector<uint32_t> pos(aoff.begin(), aoff.end() - 1);
-    for (uint32_t i = 0; i < N; ++i) adj[pos[i]++] = i;
-    for (uint32_t f = 0; f < F; ++f) {
-      const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
-      if (n != NONE) {
-        adj[pos[o]++] = n;
-        adj[pos[n]++] = o;
-      }
-    }
-  }
-  t.srow.assign(N + 1, 0);
-  t.scol.clear();
-  t.scol.reserve(aoff[N]);
-  int ws = 0;
+  out.rows = out.cols = N;
+  out.row.assign(N + 1, 0);
+  out.col.clear();
+  out.col.reserve(aoff[N]);
   for (uint32_t i = 0; i < N; ++i) {
     auto b = adj.begin() + aoff[i], e = adj.begin() + aoff[i + 1];
     std::sort(b, e);
     e = std::unique(b, e);
-    t.srow[i] = (uint32_t)t.scol.size();
-    t.scol.insert(t.scol.end(), b, e);
-    ws = std::max(ws, (int)(e - b));
+    out.row[i] = (uint32_t)out.col.size();
+    out.col.insert(out.col.end(), b, e);
   }
-  t.srow[N] = (uint32_t)t.scol.size();
+  out.row[N] = (uint32_t)out.col.size();
+  out.val.clear();
+}
+
+void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c1) {
+  const uint32_t NG = m.num_cells, F = m.num_faces;
+  if (NG == 0) throw std::invalid_argument("mesh has no cells");
+  if (c0 >= c1 || c1 > NG) throw std::invalid_argument("empty or invalid owned cell range");
+  const uint32_t N = c1 - c0;
+  t.N = N;
+  t.F = F;
+  t.NG = NG;
+  t.c0 = c0;
+  t.c1 = c1;
+  t.npad = (N + 63) & ~63u;
+  const uint32_t NONE = 0xFFFFFFFFu;
+  for (uint32_t f = 0; f < F; ++f) {
+    if (m.face_owner[f] >= NG) throw std::invalid_argument("face_owner out of range");
+    if (m.face_neighbor[f] != NONE && m.face_neighbor[f] >= NG)
+      throw std::invalid_argument("face_neighbor out of range");
+  }
+
+  // f32 geometry (init/mesh.rs:93-155); centres of every cell (ghost geometry)
+  std::vector<float> cx(NG), cy(NG);
+  for (uint32_t i = 0; i < NG; ++i) {
+    cx[i] = (float)m.cell_cx[i];
+    cy[i] = (float)m.cell_cy[i];
+  }
+  t.vol.resize(N);
+  for (uint32_t li = 0; li < N; ++li) t.vol[li] = (float)m.cell_vol[c0 + li];
+
+  // scalar CSR rows of the owned cells (init/mesh.rs:27-53): adjacency from the
+  // face list, + diagonal, sorted, deduplicated; GLOBAL column ids
+  int ws = 0;
+  {
+    auto owned = [&](uint32_t c) { return c >= c0 && c < c1; };
+    std::vector<uint32_t> deg(N + 1, 1);
+    for (uint32_t f = 0; f < F; ++f) {
+      const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
+      if (n == NONE) continue;
+      if (owned(o)) deg[o - c0]++;
+      if (owned(n)) deg[n - c0]++;
+    }
+    std::vector<uint32_t> aoff(N + 1, 0);
+    for (uint32_t li = 0; li < N; ++li) aoff[li + 1] = aoff[li] + deg[li];
+    std::vector<uint32_t> adj(aoff[N]);
+    std::vector<uint32_t> pos(aoff.begin(), aoff.end() - 1);
+    for (uint32_t li = 0; li < N; ++li) adj[pos[li]++] = c0 + li;
+    for (uint32_t f = 0; f < F; ++f) {
+      const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
+      if (n == NONE) continue;
+      if (owned(o)) adj[pos[o - c0]++] = n;
+      if (owned(n)) adj[pos[n - c0]++] = o;
+    }
+    t.srow.assign(N + 1, 0);
+    t.scol.clear();
+    t.scol.reserve(aoff[N]);
+    for (uint32_t li = 0; li < N; ++li) {
+      auto bb = adj.begin() + aoff[li], ee = adj.begin() + aoff[li + 1];
+      std::sort(bb, ee);
+      ee = std::unique(bb, ee);
+      t.srow[li] = (uint32_t)t.scol.size();
+      t.scol.insert(t.scol.end(), bb, ee);
+      ws = std::max(ws, (int)(ee - bb));
+    }
+    t.srow[N] = (uint32_t)t.scol.size();
+  }
   t.ws = ws;
   if (ws > 255) throw std::invalid_argument("cell with more than 255 neighbours");
+  // ghosts: off-range neighbours, ascending global id
+  t.ghost.clear();
+  for (uint32_t c : t.scol)
+    if (c < c0 || c >= c1) t.ghost.push_back(c);
+  std::sort(t.ghost.begin(), t.ghost.end());
+  t.ghost.erase(std::unique(t.ghost.begin(), t.ghost.end()), t.ghost.end());
+  t.glo = (uint32_t)(std::lower_bound(t.ghost.begin(), t.ghost.end(), c0) - t.ghost.begin());
+  t.ghi = (uint32_t)t.ghost.size() - t.glo;
 
-  // scalar-row ELL image + diagonal rank (init/mesh.rs:201-212)
+  // scalar-row ELL image (signed local columns) + diagonal rank (init/mesh.rs:201-212)
   t.ell_col.assign((size_t)ws * N, 0);
   t.ell_len.resize(N);
   t.ell_drank.resize(N);
-  for (uint32_t i = 0; i < N; ++i) {
-    const uint32_t a = t.srow[i], b = t.srow[i + 1];
-    t.ell_len[i] = b - a;
+  for (uint32_t li = 0; li < N; ++li) {
+    const uint32_t a = t.srow[li], b = t.srow[li + 1];
+    t.ell_len[li] = b - a;
     bool found = false;
     for (uint32_t k = a; k < b; ++k) {
       const uint32_t r = k - a;
-      t.ell_col[(size_t)r * N + i] = t.scol[k];
-      if (t.scol[k] == i) {
-        t.ell_drank[i] = r;
+      t.ell_col[(size_t)r * N + li] = t.rel(t.scol[k]);
+      if (t.scol[k] == c0 + li) {
+        t.ell_drank[li] = r;
         found = true;
       }
     }
     if (!found) throw std::invalid_argument("Diagonal not found in CSR cols");
+    // unused ELL slots hold the row's own index (never read)
+    for (uint32_t r = b - a; r < (uint32_t)ws; ++r) t.ell_col[(size_t)r * N + li] = (int32_t)li;
   }
-  // pad unused ELL slots with the row's own index (never read)
-  for (uint32_t i = 0; i < N; ++i)
-    for (uint32_t r = t.ell_len[i]; r < (uint32_t)ws; ++r) t.ell_col[(size_t)r * N + i] = i;
 
   // face slots
   int wf = 0;
   t.nface.resize(N);
-  for (uint32_t i = 0; i < N; ++i) {
+  for (uint32_t li = 0; li < N; ++li) {
+    const uint32_t i = c0 + li;
     const uint32_t nfc = m.cell_face_offsets[i + 1] - m.cell_face_offsets[i];
-    t.nface[i] = nfc;
+    t.nface[li] = nfc;
     wf = std::max(wf, (int)nfc);
   }
   t.wf = wf;
   const size_t S = (size_t)wf * N;
-  t.fs_other.assign(S, -1);
+  t.fs_other.assign(S, kNoCell);
   t.fs_meta.assign(S, 0);
   t.fs_face.assign(S, NONE);
   for (auto* v : {&t.fs_area, &t.fs_nx, &t.fs_ny, &t.fs_lam_s, &t.fs_lam_f, &t.fs_dist_a,
                   &t.fs_dist_e, &t.fs_dvx, &t.fs_dvy, &t.fs_rx, &t.fs_ry, &t.fs_rox, &t.fs_roy})
     v->assign(S, 0.0f);
-  for (uint32_t i = 0; i < N; ++i) {
+  for (uint32_t li = 0; li < N; ++li) {
+    const uint32_t i = c0 + li;
     const float ci_x = cx[i], ci_y = cy[i];
-    for (uint32_t k = 0; k < t.nface[i]; ++k) {
+    for (uint32_t k = 0; k < t.nface[li]; ++k) {
       const uint32_t f = m.cell_faces[m.cell_face_offsets[i] + k];
       if (f >= F) throw std::invalid_argument("cell_faces out of range");
       const uint32_t o = m.face_owner[f], nb = m.face_neighbor[f];
@@ -158,15 +212,15 @@ void build_topology(const cfd_mesh_view& m, Topology& t) {
         const float total = d_own + d_ngh;
         if (total > 1e-6f) lam_f = d_ngh / total;
         // cell_face_matrix_indices (init/mesh.rs:157-193) as a row rank
-        const uint32_t* b = t.scol.data() + t.srow[i];
-        const uint32_t* e = t.scol.data() + t.srow[i + 1];
+        const uint32_t* b = t.scol.data() + t.srow[li];
+        const uint32_t* e = t.scol.data() + t.srow[li + 1];
         const uint32_t* it = std::lower_bound(b, e, other);
         if (it == e || *it != other) throw std::invalid_argument("neighbour missing from CSR row");
         rank = (uint32_t)(it - b);
       }
       meta |= rank << kMetaRankShift;
-      const size_t e = (size_t)k * N + i;
-      t.fs_other[e] = internal ? (int32_t)other : -1;
+      const size_t e = (size_t)k * N + li;
+      t.fs_other[e] = internal ? t.rel(other) : kNoCell;
       t.fs_meta[e] = meta;
       t.fs_face[e] = f;
       t.fs_area[e] = area;

@@ -203,6 +203,43 @@ size_t cfd_debug_buffer_len(const cfd_solver* s, int32_t id);
  * the current state without rotating the ring (kernel-level parity).        */
 cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble);
 
+/* ------------------------------------------------------------------------ */
+/* Multi-GPU (the reference is single-GPU).  The mesh is split
+ * into R contiguous cell ranges (x-major cut-cell numbering => vertical
+ * slabs), rank r owning [floor(N r/R), floor(N (r+1)/R)).  Ghost-cell halos
+ * of the state, the Krylov vectors and every distributed AMG level go to the
+ * slab neighbours; reductions all-gather per-rank partial sums and add them
+ * in rank order (deterministic, identical on every rank).  For a distributed
+ * handle: `mesh` is the WHOLE mesh on every rank; cfd_set_u/cfd_set_p take
+ * the global arrays; cfd_num_cells and cfd_get_u/p/d_p cover the owned cells.
+ *
+ * One process per GPU over RCCL (the production path): rank 0 calls
+ * cfd_dist_unique_id and broadcasts the 128 bytes (e.g. torch.distributed);
+ * every rank then calls cfd_solver_create_dist (collective) and steps with
+ * cfd_step (collective).                                                    */
+cfd_status cfd_dist_unique_id(uint8_t out[128]);
+cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg,
+                                  int32_t hip_device, int32_t nranks, int32_t rank,
+                                  const uint8_t unique_id[128], cfd_solver** out);
+/* In-process group (SURVEY §8(b) `cfd_solver_create_dist(..., nranks,
+ * devices)`): nranks handles in this process, rank r on devices[r] (devices
+ * may repeat: all ranks on one GPU is allowed).  Collective calls go through
+ * cfd_group_step / cfd_group_debug_prepare_assemble (one host thread per rank). */
+cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t nranks,
+                            const int32_t* devices, cfd_solver** out /* [nranks] */);
+cfd_status cfd_group_step(cfd_solver* const* handles, int32_t nranks);
+/* rank, rank count, owned global range [c0, c1), global cell count         */
+cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0,
+                         uint32_t* c1, uint32_t* num_global_cells);
+/* Host-only halo plan of rank `rank` (no GPU needed; for tests / tooling).
+ * First call with null arrays to get the sizes.  ghost_global: ghost cell ids
+ * (ascending); per peer: peer rank, recv count, send count; send_global: the
+ * owned cell ids sent to each peer, concatenated in peer order.            */
+cfd_status cfd_dist_plan(const cfd_mesh_view* mesh, int32_t nranks, int32_t rank, uint32_t* c0,
+                         uint32_t* c1, uint32_t* num_ghosts, uint32_t* num_peers,
+                         uint32_t* num_send, uint32_t* ghost_global, int32_t* peer_rank,
+                         uint32_t* peer_recv, uint32_t* peer_send, uint32_t* send_global);
+
 #ifdef __cplusplus
 }
 #endif

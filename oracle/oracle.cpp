@@ -91,6 +91,21 @@ float canon_dot(const float* x, const float* y, size_t ncells) {
   return canon_final(part.data(), nc);
 }
 
+// Distributed canonical order (R ranks, contiguous cell ranges starts[r]..):
+// each rank reduces its own cells in the order above (chunks restart at its
+// first cell), then the per-rank results are added in rank order from +0.
+// R = 1 is the plain canonical order.
+float dist_dot(const float* x, const float* y, const std::vector<uint64_t>& starts) {
+  const int R = (int)starts.size() - 1;
+  if (R == 1) return canon_dot(x, y, starts[1]);
+  float acc = 0.0f;
+  for (int r = 0; r < R; ++r) {
+    const size_t o = starts[r];
+    acc += canon_dot(x + 3 * o, y + 3 * o, starts[r + 1] - o);
+  }
+  return acc;
+}
+
 // WGSL builtins (WGSL spec formulas).
 inline float wdistance(float ax, float ay, float bx, float by) {
   const float dx = ax - bx, dy = ay - by;
@@ -123,19 +138,29 @@ struct AmgLevel {
   size_t n = 0;
 };
 
-void aggregate(const Csr& m, std::vector<size_t>& agg, size_t& nagg) {  // amg.rs:84-116
+// amg.rs:84-116.  Distributed: the greedy pass runs part by
+// part (the ranks' row ranges) and a neighbour joins only within its part;
+// `cpart` returns the coarse rows' partition.  One part = the reference.
+void aggregate(const Csr& m, const std::vector<uint64_t>& part, std::vector<size_t>& agg, size_t& nagg,
+               std::vector<uint64_t>& cpart) {
   const size_t n = m.rows, NONE = std::numeric_limits<size_t>::max();
   agg.assign(n, NONE);
   nagg = 0;
-  for (size_t i = 0; i < n; ++i) {
-    if (agg[i] != NONE) continue;
-    agg[i] = nagg;
-    for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
-      const size_t j = m.col[k];
-      if (j != i && agg[j] == NONE) agg[j] = nagg;
+  cpart.assign(part.size(), 0);
+  for (size_t p = 0; p + 1 < part.size(); ++p) {
+    cpart[p] = nagg;
+    const size_t lo = part[p], hi = part[p + 1];
+    for (size_t i = lo; i < hi; ++i) {
+      if (agg[i] != NONE) continue;
+      agg[i] = nagg;
+      for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
+        const size_t j = m.col[k];
+        if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = nagg;
+      }
+      ++nagg;
     }
-    ++nagg;
   }
+  cpart.back() = nagg;
 }
 
 Csr build_prolongation(const std::vector<size_t>& agg, size_t nagg, size_t nf) {  // :118-139
@@ -217,7 +242,7 @@ Csr mat_mat_mult(const Csr& a, const Csr& b) {  // :187-229, f32 accumulation in
 struct Amg {
   std::vector<AmgLevel> levels;
 
-  void build(const Csr& fine, size_t max_levels) {  // amg.rs:246-595
+  void build(const Csr& fine, size_t max_levels, std::vector<uint64_t> part) {  // amg.rs:246-595
     Csr cur = fine;
     for (size_t li = 0; li < max_levels; ++li) {
       AmgLevel L;
@@ -230,8 +255,10 @@ struct Amg {
       if (li < max_levels - 1 && L.n > 100) {
         std::vector<size_t> agg;
         size_t nagg;
-        aggregate(cur, agg, nagg);
+        std::vector<uint64_t> cpart;
+        aggregate(cur, part, agg, nagg, cpart);
         if (nagg < L.n) {
+          part = cpart;
           L.P = build_prolongation(agg, nagg, L.n);
           L.R = transpose(L.P);
           cur = mat_mat_mult(mat_mat_mult(L.R, cur), L.P);
@@ -318,6 +345,7 @@ struct Amg {
 struct oracle_solver {
   // config
   cfd_config cfg;
+  std::vector<uint64_t> starts;  // rank partition of the cells (one rank: {0, N})
   // mesh (f32 upload, init/mesh.rs)
   uint32_t N = 0, F = 0;
   std::vector<uint32_t> face_owner, face_boundary, cell_face_offsets, cell_faces;
@@ -1045,7 +1073,7 @@ float residual_into_v0(oracle_solver* s) {
   const float alpha = 1.0f, beta = -1.0f;
 #pragma omp parallel for schedule(static)
   for (long i = 0; i < (long)n; ++i) v0[i] = alpha * s->rhs[i] + beta * s->w[i];
-  return std::sqrt(canon_dot(v0, v0, s->N));
+  return std::sqrt(dist_dot(v0, v0, s->starts));
 }
 
 void scale_in_place(float* v, size_t n, float a) {
@@ -1066,9 +1094,9 @@ cfd_linear_stats solve(oracle_solver* s) {
   ensure_fgmres(s);
   if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
     s->amg.reset(new Amg);
-    s->amg->build(s->scalar, 20);
+    s->amg->build(s->scalar, 20, s->starts);
   }
-  const float rhs_norm = std::sqrt(canon_dot(s->rhs.data(), s->rhs.data(), N));
+  const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts));
   // The two early exits are kept even under the fixed schedule: the first
   // step of a run at t=0 has b == 0 (inlet ramp smoothstep(0,ramp,0) = 0).
   if (rhs_norm < abstol || !std::isfinite(rhs_norm)) {
@@ -1109,7 +1137,7 @@ cfd_linear_stats solve(oracle_solver* s) {
       spmv(s, zj, s->w.data());
       // CGS (gmres_cgs.wgsl): H[i,j] = <w, V_i>, then w -= sum_i H[i,j] V_i
       for (int i = 0; i <= j; ++i)
-        s->H[(size_t)j * m1 + i] = canon_dot(s->w.data(), s->basis.data() + (size_t)i * n, N);
+        s->H[(size_t)j * m1 + i] = dist_dot(s->w.data(), s->basis.data() + (size_t)i * n, s->starts);
       {
         const float* Hc = s->H.data() + (size_t)j * m1;
         float* wv = s->w.data();
@@ -1121,7 +1149,7 @@ cfd_linear_stats solve(oracle_solver* s) {
           wv[e] = wv[e] - corr;
         }
       }
-      const float norm = std::sqrt(canon_dot(s->w.data(), s->w.data(), N));
+      const float norm = std::sqrt(dist_dot(s->w.data(), s->w.data(), s->starts));
       s->H[(size_t)j * m1 + j + 1] = norm;
       const float inv = norm > 1e-20f ? 1.0f / norm : 0.0f;
       {
@@ -1242,44 +1270,52 @@ void check_evolution(oracle_solver* s) {
   const float* u_data = reinterpret_cast<const float*>(s->S());
   const size_t len = 8 * (size_t)N;
   const bool have = s->have_prev && s->prev_u_cpu.size() == len;
-  const size_t nc = num_chunks(N);
-  std::vector<double> part(5 * nc);
+  // per rank segment (distributed order: chunks restart at the rank's first
+  // cell, rank results added in rank order from +0; one rank = plain order)
+  const int R = (int)s->starts.size() - 1;
+  double tot[5] = {0, 0, 0, 0, 0};
+  for (int r = 0; r < R; ++r) {
+    const size_t c0 = s->starts[r], nr = s->starts[r + 1] - c0;
+    const size_t nc = num_chunks(nr);
+    std::vector<double> part(5 * nc);
 #pragma omp parallel for schedule(static)
-  for (long k = 0; k < (long)nc; ++k) {
-    double acc[5][kThreads];
-    for (int t = 0; t < kThreads; ++t) {
-      double evo = 0, su = 0, sv = 0, squ = 0, sqv = 0;
-      for (int q = 0; q < kCellsPerThread; ++q) {
-        const size_t c = (size_t)k * kChunkCells + t + (size_t)kThreads * q;
-        if (c >= N) continue;
-        if (have)
-          for (int f = 0; f < 8; ++f) {
-            const float d = u_data[8 * c + f] - s->prev_u_cpu[8 * c + f];
-            evo += (double)(d * d);
-          }
-        const double u = (double)u_data[2 * c], v = (double)u_data[2 * c + 1];
-        su += u;
-        sv += v;
-        squ += u * u;
-        sqv += v * v;
+    for (long k = 0; k < (long)nc; ++k) {
+      double acc[5][kThreads];
+      for (int t = 0; t < kThreads; ++t) {
+        double evo = 0, su = 0, sv = 0, squ = 0, sqv = 0;
+        for (int q = 0; q < kCellsPerThread; ++q) {
+          const size_t lc = (size_t)k * kChunkCells + t + (size_t)kThreads * q;
+          if (lc >= nr) continue;
+          const size_t c = c0 + lc;
+          if (have)
+            for (int f = 0; f < 8; ++f) {
+              const float d = u_data[8 * c + f] - s->prev_u_cpu[8 * c + f];
+              evo += (double)(d * d);
+            }
+          const double u = (double)u_data[2 * c], v = (double)u_data[2 * c + 1];
+          su += u;
+          sv += v;
+          squ += u * u;
+          sqv += v * v;
+        }
+        acc[0][t] = evo;
+        acc[1][t] = su;
+        acc[2][t] = sv;
+        acc[3][t] = squ;
+        acc[4][t] = sqv;
       }
-      acc[0][t] = evo;
-      acc[1][t] = su;
-      acc[2][t] = sv;
-      acc[3][t] = squ;
-      acc[4][t] = sqv;
+      for (int f = 0; f < 5; ++f) part[5 * k + f] = tree256d(acc[f]);
     }
-    for (int f = 0; f < 5; ++f) part[5 * k + f] = tree256d(acc[f]);
-  }
-  double tot[5];
-  for (int f = 0; f < 5; ++f) {
-    double acc[kThreads];
-    for (int t = 0; t < kThreads; ++t) {
-      double a = 0.0;
-      for (size_t q = t; q < nc; q += kThreads) a += part[5 * q + f];
-      acc[t] = a;
+    for (int f = 0; f < 5; ++f) {
+      double acc[kThreads];
+      for (int t = 0; t < kThreads; ++t) {
+        double a = 0.0;
+        for (size_t q = t; q < nc; q += kThreads) a += part[5 * q + f];
+        acc[t] = a;
+      }
+      const double seg = tree256d(acc);
+      tot[f] = (R == 1) ? seg : tot[f] + seg;
     }
-    tot[f] = tree256d(acc);
   }
   const double n = (double)N;
   const double mean_u = tot[1] / n, mean_v = tot[2] / n;
@@ -1395,16 +1431,22 @@ void oracle_set_threads(int n) {
 #endif
 }
 
-oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg) {
-  if (!mesh || !cfg) return nullptr;
+oracle_solver* oracle_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg, int nranks) {
+  if (!mesh || !cfg || nranks < 1 || (uint32_t)nranks > mesh->num_cells) return nullptr;
   auto* s = new oracle_solver;
   s->cfg = *cfg;
   s->m = cfg->max_restart > 0 ? cfg->max_restart : 50;
+  s->starts.resize(nranks + 1);
+  for (int r = 0; r <= nranks; ++r) s->starts[r] = (uint64_t)mesh->num_cells * (uint64_t)r / (uint64_t)nranks;
   if (!build(s, mesh)) {
     delete s;
     return nullptr;
   }
   return s;
+}
+
+oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg) {
+  return oracle_create_dist(mesh, cfg, 1);
 }
 
 void oracle_destroy(oracle_solver* s) { delete s; }

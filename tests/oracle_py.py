@@ -29,6 +29,8 @@ def olib():
         vp = C.c_void_p
         L.oracle_create.restype = vp
         L.oracle_create.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config)]
+        L.oracle_create_dist.restype = vp
+        L.oracle_create_dist.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int]
         L.oracle_destroy.argtypes = [vp]
         L.oracle_destroy.restype = None
         L.oracle_set_threads.argtypes = [C.c_int]
@@ -64,12 +66,13 @@ def _ck(st, what):
 class OracleSolver:
     """Same surface as cfd2_amd.GpuSolver, backed by the CPU oracle."""
 
-    def __init__(self, mesh, config=None, **cfg_overrides):
+    def __init__(self, mesh, config=None, nranks=1, **cfg_overrides):
+        """nranks > 1: the distributed solver's semantics on nranks cell ranges."""
         self._mesh = mesh  # keep the mesh alive (view borrows its arrays)
         cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
         self._cfg = cfg
         view = mesh.view()
-        h = olib().oracle_create(C.byref(view), C.byref(cfg))
+        h = olib().oracle_create_dist(C.byref(view), C.byref(cfg), int(nranks))
         if not h:
             raise RuntimeError("oracle_create failed: " + olib().oracle_last_error().decode())
         self._h = C.c_void_p(h)

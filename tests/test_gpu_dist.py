@@ -1,0 +1,98 @@
+"""Distributed solver vs the oracle's distributed semantics.
+
+The in-process group (cfd_group_*) runs R ranks on ONE GPU with the same
+halo / all-gather / partition-aware AMG code the RCCL path runs, so the whole
+distributed algorithm is checked bit-for-bit here against
+OracleSolver(nranks=R) (partition-aware aggregation, rank-segmented
+reductions added in rank order).  RCCL itself refuses two ranks on one device;
+its transport is exercised by bench.py --gpus N on a multi-GPU node.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from cfd2_amd import GpuGroup, default_config
+from tests.meshes import backwards_step, bench_mesh, channel_obstacle
+from tests.oracle_py import OracleSolver
+from tests.test_gpu_parity import _assert_same_fields, _assert_same_info, _setup_amg_test
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def replicate_rows():
+    """Force distributed coarse levels (and the all-gather into the replicated
+    tail) even on small meshes."""
+    old = os.environ.get("CFD_AMG_REPLICATE_ROWS")
+    yield lambda v: os.environ.__setitem__("CFD_AMG_REPLICATE_ROWS", str(v))
+    if old is None:
+        os.environ.pop("CFD_AMG_REPLICATE_ROWS", None)
+    else:
+        os.environ["CFD_AMG_REPLICATE_ROWS"] = old
+
+
+@pytest.mark.parametrize("nranks,precond,rep", [(2, 1, 32768), (2, 1, 50), (3, 1, 50), (2, 0, 32768),
+                                                (4, 1, 120)])
+def test_group_amg_test_parity(nranks, precond, rep, replicate_rows):
+    """tests/amg_test.rs setup, 4 steps, R ranks on one GPU == oracle(R), bit-exact."""
+    replicate_rows(rep)
+    mesh = backwards_step()
+    g = GpuGroup(mesh, nranks)
+    o = OracleSolver(mesh, nranks=nranks)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, precond)
+    for k in range(4):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"R={nranks} step {k}")
+        _assert_same_info(g, o, f"R={nranks} step {k}")
+    if precond == 1:  # rank 0 stores its own rows of the distributed levels
+        assert len(g.amg_levels()) == len(o.amg_levels())
+    g.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_group_fixed_schedule_schemes(nranks, replicate_rows):
+    """Fixed schedule, SOU scheme (neighbour gradients through the halo), BDF2."""
+    replicate_rows(200)
+    mesh = channel_obstacle(h=0.03)
+    cfg = dict(fixed_outer=3, fixed_inner=10)
+    g = GpuGroup(mesh, nranks, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+        s.set_scheme(1)
+        s.set_time_scheme(1)
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"R={nranks} step {k}")
+        _assert_same_info(g, o, f"R={nranks} step {k}")
+    g.close()
+
+
+def test_group_bench_geometry(replicate_rows):
+    """~100k-cell bench geometry on 4 ranks, bench physics, distributed levels down
+    to 4096 rows then the replicated tail: one fixed-schedule step bit-exact."""
+    replicate_rows(4096)
+    mesh = bench_mesh(0.0055, 30)
+    cfg = default_config(fixed_outer=2, fixed_inner=8)
+    g = GpuGroup(mesh, 4, config=cfg)
+    o = OracleSolver(mesh, config=default_config(fixed_outer=2, fixed_inner=8), nranks=4)
+    for s in (g, o):
+        s.set_dt(1e-3)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_alpha_u(0.7)
+        s.set_alpha_p(0.3)
+        s.set_precond_type(1)
+        s.initialize_history()
+        c = s.constants
+        c.time = 0.05
+        s.constants = c
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"bench geometry step {k}")
+    g.close()
