@@ -65,6 +65,7 @@ def _bind():
     L.cfd_dist_info.argtypes = [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), u32p, u32p, u32p]
     L.cfd_dist_plan.argtypes = [C.POINTER(_ffi.MeshView), C.c_int32, C.c_int32, u32p, u32p, u32p, u32p,
                                 u32p, u32p, C.POINTER(C.c_int32), u32p, u32p, u32p]
+    L.cfd_debug_rccl_selftest.argtypes = [C.c_int32]
     _bound = True
     return L
 
@@ -325,3 +326,8 @@ def dist_plan(mesh, nranks: int, rank: int) -> dict:
     n = npeer.value
     return dict(c0=c0.value, c1=c1.value, ghost=ghost[:ng.value], peers=prank[:n].tolist(),
                 recv=precv[:n].tolist(), send=psend[:n].tolist(), send_ids=sendg[:ns.value])
+
+
+def rccl_selftest(device: int = 0) -> None:
+    """RCCL transport plumbing check on one GPU (raises on failure)."""
+    _ffi.check(_bind().cfd_debug_rccl_selftest(int(device)), "cfd_debug_rccl_selftest")

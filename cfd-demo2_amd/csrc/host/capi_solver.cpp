@@ -293,6 +293,40 @@ cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
   return CFD_OK;
 }
 
+// RCCL plumbing self-test on ONE GPU (RCCL refuses two ranks per device, so
+// the multi-rank path cannot run on a one-GPU box): a 1-rank communicator,
+// a grouped send/recv to self through Comm::exchange and an all-gather.
+cfd_status cfd_debug_rccl_selftest(int32_t device) {
+  return guard([&] {
+    CFD_HIP(hipSetDevice(device));
+    uint8_t uid[128];
+    cfd2::rccl_unique_id(uid);
+    auto comm = cfd2::make_rccl_comm(1, 0, uid);
+    hipStream_t s;
+    CFD_HIP(hipStreamCreate(&s));
+    const size_t n = 4096;
+    std::vector<float> h(n), back(2 * n, 0.0f);
+    for (size_t i = 0; i < n; ++i) h[i] = (float)i * 0.5f;
+    float *a, *b;
+    CFD_HIP(hipMalloc(&a, n * sizeof(float)));
+    CFD_HIP(hipMalloc(&b, 2 * n * sizeof(float)));
+    CFD_HIP(hipMemcpyAsync(a, h.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+    CFD_HIP(hipMemsetAsync(b, 0, 2 * n * sizeof(float), s));
+    // two matched transfers to self: [0, n/2) -> b[n..], [n/2, n) -> b[n + n/2..]
+    std::vector<cfd2::Msg> msgs = {{0, a, n / 2 * sizeof(float), b + n, n / 2 * sizeof(float)},
+                                   {0, a + n / 2, n / 2 * sizeof(float), b + n + n / 2, n / 2 * sizeof(float)}};
+    comm->exchange(msgs, s);
+    comm->allgather(a, b, n * sizeof(float), s);
+    CFD_HIP(hipMemcpyAsync(back.data(), b, 2 * n * sizeof(float), hipMemcpyDeviceToHost, s));
+    CFD_HIP(hipStreamSynchronize(s));
+    (void)hipFree(a);
+    (void)hipFree(b);
+    (void)hipStreamDestroy(s);
+    for (size_t i = 0; i < n; ++i)
+      if (back[i] != h[i] || back[n + i] != h[i]) throw std::runtime_error("RCCL self-test: wrong data");
+  });
+}
+
 cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0, uint32_t* c1,
                          uint32_t* ng) {
   CHECK_S(s);

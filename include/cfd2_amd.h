@@ -228,6 +228,10 @@ cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* c
 cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t nranks,
                             const int32_t* devices, cfd_solver** out /* [nranks] */);
 cfd_status cfd_group_step(cfd_solver* const* handles, int32_t nranks);
+/* RCCL plumbing check on one GPU: 1-rank communicator, grouped send/recv to
+ * self and an all-gather through the solver's transport; CFD_OK if the data
+ * arrived intact.                                                           */
+cfd_status cfd_debug_rccl_selftest(int32_t hip_device);
 /* rank, rank count, owned global range [c0, c1), global cell count         */
 cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0,
                          uint32_t* c1, uint32_t* num_global_cells);

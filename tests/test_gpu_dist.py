@@ -96,3 +96,9 @@ def test_group_bench_geometry(replicate_rows):
         o.step()
         _assert_same_fields(g, o, f"bench geometry step {k}")
     g.close()
+
+
+def test_rccl_transport_selftest():
+    """The RCCL transport (grouped send/recv + all-gather) on a 1-rank communicator."""
+    from cfd2_amd.solver import rccl_selftest
+    rccl_selftest(0)
