@@ -30,6 +30,13 @@ __device__ __forceinline__ float safe_inverse(float v) {
   return fabsf(v) > 1e-14f ? 1.0f / v : 0.0f;
 }
 
+__device__ __forceinline__ float f4(const float4& v, int k) {
+  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ uint32_t u4(const uchar4& v, int k) {
+  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // XCD-aware block -> tile remap (cdna_hip_programming.md T1): the dispatcher
@@ -291,7 +298,7 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
       sdpp += lapl;
       const float scoeff = c.density * dp_f * area / dist;
       sdiag += scoeff;
-      const size_t slot = (size_t)rank * N + i;
+      const size_t slot = (size_t)rank * a.ld + i;
       a.cval_a[slot] = make_float2(coeff, -lapl);
       a.cval_g[slot] = make_float2(oml * pgx, oml * pgy);
       a.sval[slot] = -scoeff;
@@ -326,7 +333,7 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
     }
   }
   const uint32_t dr = a.srank_diag[i];
-  const size_t dslot = (size_t)dr * N + i;
+  const size_t dslot = (size_t)dr * a.ld + i;
   a.cval_a[dslot] = make_float2(diag_uv, 0.0f + sdpp);
   a.cval_g[dslot] = make_float2(sdup, sdvp);
   a.cdiag2[i] = make_float2(sdpu, sdpv);
@@ -448,51 +455,85 @@ __global__ void __launch_bounds__(kBlock) k_residual_axpby(const float* __restri
   if (e < n) v0[e] = 1.0f * b[e] + -1.0f * w[e];
 }
 
-struct BlockCoeffs {
-  float uu, up, vp, pu, pv, pp;
-};
-__device__ __forceinline__ BlockCoeffs load_block(const CoupledMatrix& A, uint32_t r, uint32_t dr,
-                                                  size_t slot, float2 d2) {
-  const float2 a = A.cval_a[slot];
-  const float2 g = A.cval_g[slot];
-  BlockCoeffs k;
-  k.uu = a.x;
-  k.pp = a.y;
-  k.up = g.x;
-  k.vp = g.y;
-  k.pu = (r == dr) ? d2.x : g.x;
-  k.pv = (r == dr) ? d2.y : g.y;
-  return k;
+__device__ __forceinline__ void load2x4(const float2* p, float2 v[4]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 2);
+  v[0] = make_float2(a.x, a.y);
+  v[1] = make_float2(a.z, a.w);
+  v[2] = make_float2(b.x, b.y);
+  v[3] = make_float2(b.z, b.w);
+}
+template <bool D16>
+__device__ __forceinline__ void ccols4(const CoupledMatrix& A, size_t off, uint32_t i0, int c[4]) {
+  if constexpr (D16) {
+    const short4 d = *reinterpret_cast<const short4*>(A.col16 + off);
+    c[0] = (int)i0 + (int)d.x;
+    c[1] = (int)i0 + 1 + (int)d.y;
+    c[2] = (int)i0 + 2 + (int)d.z;
+    c[3] = (int)i0 + 3 + (int)d.w;
+  } else {
+    const int4 q = *reinterpret_cast<const int4*>(A.col + off);
+    c[0] = q.x;
+    c[1] = q.y;
+    c[2] = q.z;
+    c[3] = q.w;
+  }
+}
+__device__ __forceinline__ void load12(const float* p, float v[12]) {  // 3 float4 = 4 rows x (u,v,p)
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  const float4 c = *reinterpret_cast<const float4*>(p + 8);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
+}
+__device__ __forceinline__ void store12(float* p, const float v[12]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-// spmv (gmres_ops.wgsl:63-81) on compressed blocks: one thread per cell, three
-// rows; per-row term order identical to the CSR row (neighbour-major, u,v,p).
+// spmv (gmres_ops.wgsl:63-81) on compressed blocks, 4 cells (12 rows) per
+// thread; per-row term order identical to the CSR row (neighbour-major, u,v,p).
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
-  const uint32_t i = row_id();
-  const uint32_t N = A.N;
-  if (i >= N) return;
-  const uint32_t len = A.len[i], dr = A.drank[i];
-  const float2 d2 = A.cdiag2[i];
-  float su = 0.0f, sv = 0.0f, sp = 0.0f;
-  for (uint32_t r = 0; r < len; ++r) {
-    const size_t slot = (size_t)r * N + i;
-    const int32_t j = A.col[slot];
-    const BlockCoeffs k = load_block(A, r, dr, slot, d2);
-    const float xu = x[3 * (ptrdiff_t)j], xv = x[3 * (ptrdiff_t)j + 1], xp = x[3 * (ptrdiff_t)j + 2];
-    su += k.uu * xu;
-    su += 0.0f * xv;
-    su += k.up * xp;
-    sv += 0.0f * xu;
-    sv += k.uu * xv;
-    sv += k.vp * xp;
-    sp += k.pu * xu;
-    sp += k.pv * xv;
-    sp += k.pp * xp;
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= A.N) return;
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
+  const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
+  float2 d2[4];
+  load2x4(A.cdiag2 + i0, d2);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float su[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t r = 0; r < maxlen; ++r) {
+    const size_t off = (size_t)r * A.ld + i0;
+    float2 a[4], g[4];
+    load2x4(A.cval_a + off, a);
+    load2x4(A.cval_g + off, g);
+    int c[4];
+    ccols4<D16>(A, off, i0, c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (r >= u4(ln, k)) continue;
+      const bool dg = (r == u4(dr, k));
+      const float uu = a[k].x, pp = a[k].y, up = g[k].x, vp = g[k].y;
+      const float pu = dg ? d2[k].x : g[k].x, pv = dg ? d2[k].y : g[k].y;
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[k];
+      const float xu = x[j], xv = x[j + 1], xp = x[j + 2];
+      su[k] += uu * xu;
+      su[k] += 0.0f * xv;
+      su[k] += up * xp;
+      sv[k] += 0.0f * xu;
+      sv[k] += uu * xv;
+      sv[k] += vp * xp;
+      sp[k] += pu * xu;
+      sp[k] += pv * xv;
+      sp[k] += pp * xp;
+    }
   }
-  y[3 * (size_t)i] = su;
-  y[3 * (size_t)i + 1] = sv;
-  y[3 * (size_t)i + 2] = sp;
+  const float o[12] = {su[0], sv[0], sp[0], su[1], sv[1], sp[1], su[2], sv[2], sp[2], su[3], sv[3], sp[3]};
+  store12(y + 3 * (size_t)i0, o);
 }
 
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j,
@@ -632,11 +673,13 @@ __global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict_
   resid_hist[j] = fabsf(g[j + 1]);
 }
 
-// predict_and_form_schur (schur_precond.wgsl:142-188).  z_u, z_v of the
-// prediction are recomputed by k_precond_correct (same two multiplies), so this
-// kernel writes only the Schur rhs and the first Jacobi iterate.  The term
-// `A_pp * 0.0` of the reference loop is dropped: it can only flip the sign of a
-// zero rhs_p, and its A_pp read is the largest byte cost of the row.
+// predict_and_form_schur (schur_precond.wgsl:142-188), 4 cells per thread.
+// z_u, z_v of the prediction are recomputed by k_precond_correct (same two
+// multiplies), so this kernel writes only the Schur rhs and the first Jacobi
+// iterate.  The term `A_pp * 0.0` of the reference loop is dropped: it can
+// only flip the sign of a zero rhs_p, and its A_pp read is the largest byte
+// cost of the row.
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             const float* __restrict__ w_in,
                                                             const float* __restrict__ binv, int jv,
@@ -644,32 +687,48 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             const float* __restrict__ dinv_p,
                                                             float* temp_p, float* p_sol,
                                                             float* p_prev) {
-  const uint32_t i = row_id();
-  const uint32_t N = A.N;
-  if (i >= N) return;
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= A.N) return;
   const float sc = binv[jv];
-  float rhs_p = sc * w_in[3 * (size_t)i + 2];
-  const uint32_t len = A.len[i], dr = A.drank[i];
-  const float2 d2 = A.cdiag2[i];
-  for (uint32_t r = 0; r < len; ++r) {
-    const size_t slot = (size_t)r * N + i;
-    const int32_t j = A.col[slot];
-    const float2 g = A.cval_g[slot];
-    const float pu = (r == dr) ? d2.x : g.x, pv = (r == dr) ? d2.y : g.y;
-    const float dj = dinv_uv[j];
-    const float ru = sc * w_in[3 * (ptrdiff_t)j], rv = sc * w_in[3 * (ptrdiff_t)j + 1];
-    const float zu = ru * dj;
-    const float zv = rv * dj;
-    rhs_p -= pu * zu;
-    rhs_p -= pv * zv;
+  float wo[12];
+  load12(w_in + 3 * (size_t)i0, wo);
+  float rhs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rhs[k] = sc * wo[3 * k + 2];
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
+  const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
+  float2 d2[4];
+  load2x4(A.cdiag2 + i0, d2);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  for (uint32_t r = 0; r < maxlen; ++r) {
+    const size_t off = (size_t)r * A.ld + i0;
+    float2 g[4];
+    load2x4(A.cval_g + off, g);
+    int c[4];
+    ccols4<D16>(A, off, i0, c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (r >= u4(ln, k)) continue;
+      const bool dg = (r == u4(dr, k));
+      const float pu = dg ? d2[k].x : g[k].x, pv = dg ? d2[k].y : g[k].y;
+      const float dj = dinv_uv[c[k]];
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[k];
+      const float ru = sc * w_in[j], rv = sc * w_in[j + 1];
+      const float zu = ru * dj;
+      const float zv = rv * dj;
+      rhs[k] -= pu * zu;
+      rhs[k] -= pv * zv;
+    }
   }
-  temp_p[i] = rhs_p;
-  p_sol[i] = dinv_p[i] * rhs_p;
-  if (p_prev) p_prev[i] = 0.0f;
+  const float4 dp = *reinterpret_cast<const float4*>(dinv_p + i0);
+  *reinterpret_cast<float4*>(temp_p + i0) = make_float4(rhs[0], rhs[1], rhs[2], rhs[3]);
+  *reinterpret_cast<float4*>(p_sol + i0) =
+      make_float4(dp.x * rhs[0], dp.y * rhs[1], dp.z * rhs[2], dp.w * rhs[3]);
+  if (p_prev) *reinterpret_cast<float4*>(p_prev + i0) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 // relax_pressure (schur_precond.wgsl:52-90), omega = 1.2, live scalar matrix
-__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const int32_t* __restrict__ col,
+__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t ld, const int32_t* __restrict__ col,
                                                            const uint32_t* __restrict__ len,
                                                            const float* __restrict__ sval,
                                                            const float* __restrict__ dinv_p,
@@ -681,7 +740,7 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const int
   float sigma = 0.0f;
   const uint32_t l = len[i];
   for (uint32_t r = 0; r < l; ++r) {
-    const size_t slot = (size_t)r * N + i;
+    const size_t slot = (size_t)r * ld + i;
     const int32_t cc = col[slot];
     if (cc != (int32_t)i) sigma += sval[slot] * p_sol[cc];
   }
@@ -690,33 +749,49 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, const int
 }
 
 // correct_velocity (schur_precond.wgsl:93-139) fused with the velocity
-// prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol)
+// prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol);
+// 4 cells per thread.
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
                                                             const float* __restrict__ w_in,
                                                             const float* __restrict__ binv, int jv,
                                                             const float* __restrict__ p_sol,
                                                             const float* __restrict__ dinv_uv,
                                                             float* __restrict__ z) {
-  const uint32_t i = row_id();
-  const uint32_t N = A.N;
-  if (i >= N) return;
-  const uint32_t len = A.len[i];
-  float cu = 0.0f, cv = 0.0f;
-  for (uint32_t r = 0; r < len; ++r) {
-    const size_t slot = (size_t)r * N + i;
-    const int32_t j = A.col[slot];
-    const float2 g = A.cval_g[slot];
-    const float pj = p_sol[j];
-    cu += g.x * pj;
-    cv += g.y * pj;
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= A.N) return;
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (uint32_t r = 0; r < maxlen; ++r) {
+    const size_t off = (size_t)r * A.ld + i0;
+    float2 g[4];
+    load2x4(A.cval_g + off, g);
+    int c[4];
+    ccols4<D16>(A, off, i0, c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (r >= u4(ln, k)) continue;
+      const float pj = p_sol[c[k]];
+      cu[k] += g[k].x * pj;
+      cv[k] += g[k].y * pj;
+    }
   }
   const float sc = binv[jv];
-  const float du = dinv_uv[i];
-  const float ru = sc * w_in[3 * (size_t)i], rv = sc * w_in[3 * (size_t)i + 1];
-  const float zu = du * ru, zv = du * rv;
-  z[3 * (size_t)i] = zu - du * cu;
-  z[3 * (size_t)i + 1] = zv - du * cv;
-  z[3 * (size_t)i + 2] = p_sol[i];
+  float wo[12], o[12];
+  load12(w_in + 3 * (size_t)i0, wo);
+  const float4 du4 = *reinterpret_cast<const float4*>(dinv_uv + i0);
+  const float4 ps4 = *reinterpret_cast<const float4*>(p_sol + i0);
+  const float du[4] = {du4.x, du4.y, du4.z, du4.w}, ps[4] = {ps4.x, ps4.y, ps4.z, ps4.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float ru = sc * wo[3 * k], rv = sc * wo[3 * k + 1];
+    const float zu = du[k] * ru, zv = du[k] * rv;
+    o[3 * k] = zu - du[k] * cu[k];
+    o[3 * k + 1] = zv - du[k] * cv[k];
+    o[3 * k + 2] = ps[k];
+  }
+  store12(z + 3 * (size_t)i0, o);
 }
 
 // solve_triangular (gmres_logic.wgsl:78-104), single lane
@@ -764,12 +839,6 @@ __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uin
   }
 }
 
-__device__ __forceinline__ float f4(const float4& v, int k) {
-  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-}
-__device__ __forceinline__ uint32_t u4(const uchar4& v, int k) {
-  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-}
 
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
 template <bool D16>
@@ -1129,7 +1198,12 @@ void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, 
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
 }
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
-  if (A.N) hipLaunchKernelGGL(k_spmv, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, x, y);
+  if (!A.N) return;
+  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.use16)
+    hipLaunchKernelGGL(k_spmv<true>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
+  else
+    hipLaunchKernelGGL(k_spmv<false>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      float* partial, uint32_t np, hipStream_t s) {
@@ -1153,23 +1227,30 @@ void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int 
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s) {
-  if (A.N)
-    hipLaunchKernelGGL(k_precond_predict, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv,
-                       dinv_p, temp_p, p_sol, p_prev);
+  if (!A.N) return;
+  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.use16)
+    hipLaunchKernelGGL(k_precond_predict<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
+                       temp_p, p_sol, p_prev);
+  else
+    hipLaunchKernelGGL(k_precond_predict<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
+                       temp_p, p_sol, p_prev);
 }
-void launch_relax_pressure(uint32_t N, int ws, const int32_t* col, const uint32_t* len, const float* sval,
+void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len, const float* sval,
                            const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
                            hipStream_t s) {
-  (void)ws;
   if (N)
-    hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, col, len, sval, dinv_p,
+    hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, ld, col, len, sval, dinv_p,
                        temp_p, p_sol, p_prev);
 }
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
-  if (A.N)
-    hipLaunchKernelGGL(k_precond_correct, dim3(grid_for(A.N)), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol,
-                       dinv_uv, z);
+  if (!A.N) return;
+  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.use16)
+    hipLaunchKernelGGL(k_precond_correct<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+  else
+    hipLaunchKernelGGL(k_precond_correct<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
 }
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(64), 0, s, H, g, y, k, m1);

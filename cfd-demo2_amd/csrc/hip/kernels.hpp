@@ -83,6 +83,7 @@ struct PrepareArgs {
 
 struct AssembleArgs {
   uint32_t N;
+  uint32_t ld;             // scalar-row ELL slot stride
   cfd_constants c;
   FaceSlots fs;
   const float* vol;
@@ -93,24 +94,30 @@ struct AssembleArgs {
   const float2* grad_u;
   const float2* grad_v;
   const uint32_t* srank_diag;  // [N] diagonal rank in the scalar row
-  float2* cval_a; // [r*N + i] {A_uu (=A_vv), A_pp}
-  float2* cval_g; // [r*N + i] {A_up (=A_pu), A_vp (=A_pv)}
-  float2* cdiag2; // [N] {s_pu, s_pv} of the diagonal block
-  float* sval;    // [r*N + i] scalar pressure matrix
+  float2* cval_a; // [r*ld + i] {A_uu (=A_vv), A_pp}
+  float2* cval_g; // [r*ld + i] {A_up (=A_pu), A_vp (=A_pv)}
+  float2* cdiag2; // [ld] {s_pu, s_pv} of the diagonal block
+  float* sval;    // [r*ld + i] scalar pressure matrix
   float* rhs;     // [3N]
   float* dinv_uv; // [N]
   float* dinv_p;  // [N]
 };
 
+// The Krylov kernels process 4 consecutive rows per thread: every per-slot
+// array is one 16/32-byte load per thread, columns are 16-bit deltas when the
+// whole matrix allows it, lengths / diagonal ranks u8.
 struct CoupledMatrix {
   uint32_t N;
+  uint32_t ld;            // slot stride (N rounded up to 64)
   int ws;
-  const int32_t* col;   // [r*N + i] signed local column
-  const uint32_t* len;  // [N]
-  const uint32_t* drank;  // [N]
+  int use16;
+  const int32_t* col;     // [r*ld + i] signed local column
+  const int16_t* col16;   // [r*ld + i] col - i (use16)
+  const uint8_t* len;     // [ld]
+  const uint8_t* drank;   // [ld]
   const float2* cval_a;
   const float2* cval_g;
-  const float2* cdiag2;
+  const float2* cdiag2;   // [ld]
 };
 
 // One AMG level (linear_solver/amg.rs AmgLevel) in the layout the gfx950
@@ -190,7 +197,7 @@ void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int 
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s);
-void launch_relax_pressure(uint32_t N, int ws, const int32_t* col, const uint32_t* len,
+void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,

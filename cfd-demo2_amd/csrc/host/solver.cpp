@@ -107,6 +107,9 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   d_scol = arena.upload(topo.ell_col, stream);
   d_slen = arena.upload(topo.ell_len, stream);
   d_sdrank = arena.upload(topo.ell_drank, stream);
+  if (topo.use16) d_scol16 = arena.upload(topo.ell_col16, stream);
+  d_slen8 = arena.upload(topo.ell_len8, stream);
+  d_sdrank8 = arena.upload(topo.ell_drank8, stream);
   // fields (init/fields.rs:62-139): zero-initialised, with ghost space
   auto zeros_state = [&](StateView& v) {
     v.u = valloc<float2>(1);
@@ -118,7 +121,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   zeros_state(prev);
   dp_scratch = valloc<float>(1);
   gp_scratch = valloc<float2>(1);
-  const size_t slots_f = (size_t)topo.wf * N, slots_s = (size_t)topo.ws * N;
+  const size_t slots_f = (size_t)topo.wf * N, slots_s = (size_t)topo.ws * topo.ld;
   flux_s = arena.alloc<float>(slots_f);
   CFD_HIP(hipMemsetAsync(flux_s, 0, slots_f * sizeof(float), stream));
   grad_u = valloc<float2>(1);
@@ -127,8 +130,8 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   cval_g = arena.alloc<float2>(slots_s);
   CFD_HIP(hipMemsetAsync(cval_a, 0, slots_s * sizeof(float2), stream));
   CFD_HIP(hipMemsetAsync(cval_g, 0, slots_s * sizeof(float2), stream));
-  cdiag2 = arena.alloc<float2>(N);
-  CFD_HIP(hipMemsetAsync(cdiag2, 0, N * sizeof(float2), stream));
+  cdiag2 = arena.alloc<float2>(topo.ld);
+  CFD_HIP(hipMemsetAsync(cdiag2, 0, topo.ld * sizeof(float2), stream));
   sval = arena.alloc<float>(slots_s);
   CFD_HIP(hipMemsetAsync(sval, 0, slots_s * sizeof(float), stream));
   rhs = valloc<float>(3);
@@ -173,10 +176,13 @@ Solver::~Solver() {
 CoupledMatrix Solver::cmat() const {
   CoupledMatrix A;
   A.N = N;
+  A.ld = topo.ld;
   A.ws = topo.ws;
+  A.use16 = topo.use16 ? 1 : 0;
   A.col = d_scol;
-  A.len = d_slen;
-  A.drank = d_sdrank;
+  A.col16 = d_scol16;
+  A.len = d_slen8;
+  A.drank = d_sdrank8;
   A.cval_a = cval_a;
   A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
@@ -338,6 +344,7 @@ void Solver::prepare() {
 void Solver::assemble() {
   AssembleArgs a;
   a.N = N;
+  a.ld = topo.ld;
   a.c = constants;
   a.fs = fs;
   a.vol = d_vol;
@@ -481,12 +488,13 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 // replicated on every rank.
 void Solver::ensure_amg() {
   if (amg_built) return;
-  std::vector<float> ell((size_t)topo.ws * N);
+  const size_t ld = topo.ld;
+  std::vector<float> ell((size_t)topo.ws * ld);
   CFD_HIP(hipMemcpyAsync(ell.data(), sval, ell.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   std::vector<float> own(topo.scol.size());
   for (uint32_t i = 0; i < N; ++i)
-    for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k) own[k] = ell[(size_t)(k - topo.srow[i]) * N + i];
+    for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k) own[k] = ell[(size_t)(k - topo.srow[i]) * ld + i];
   HostCsr A0;
   std::vector<AmgHostLevel> H;
   if (!dist()) {
@@ -726,7 +734,7 @@ void Solver::precondition(int j, float* z) {
       float* src = in_sol ? p_sol : temp;
       float* dst = in_sol ? temp : p_sol;
       if (dist()) halo(cell_plan, {{src, 1}});
-      launch_relax_pressure(N, topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
+      launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
       in_sol = !in_sol;
     }
     if (dist()) halo(cell_plan, {{in_sol ? p_sol : temp, 1}});
@@ -1090,14 +1098,16 @@ void Solver::debug_buffer(int id, float* out) {
     case 5: case 6: d2h(out, dinv_uv, n * 4); break;
     case 7: d2h(out, dinv_p, n * 4); break;
     case 8: {
-      std::vector<float> ell((size_t)topo.ws * n);
+      const size_t ld = topo.ld;
+      std::vector<float> ell((size_t)topo.ws * ld);
       d2h(ell.data(), sval, ell.size() * 4);
       for (uint32_t i = 0; i < N; ++i)
-        for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k) out[k] = ell[(size_t)(k - topo.srow[i]) * n + i];
+        for (uint32_t k = topo.srow[i]; k < topo.srow[i + 1]; ++k) out[k] = ell[(size_t)(k - topo.srow[i]) * ld + i];
       break;
     }
     case 9: {  // expand compressed blocks to the reference CSR (init/linear_solver/mod.rs:180-216)
-      std::vector<float2> ca((size_t)topo.ws * n), cg((size_t)topo.ws * n);
+      const size_t ld = topo.ld;
+      std::vector<float2> ca((size_t)topo.ws * ld), cg((size_t)topo.ws * ld);
       std::vector<float2> d2(n);
       d2h(ca.data(), cval_a, ca.size() * sizeof(float2));
       d2h(cg.data(), cval_g, cg.size() * sizeof(float2));
@@ -1106,7 +1116,7 @@ void Solver::debug_buffer(int id, float* out) {
         const uint32_t so = topo.srow[i], nb = topo.srow[i + 1] - so;
         const uint32_t r0 = 9 * so, r1 = r0 + 3 * nb, r2 = r0 + 6 * nb;
         for (uint32_t r = 0; r < nb; ++r) {
-          const float2 a = ca[(size_t)r * n + i], gg = cg[(size_t)r * n + i];
+          const float2 a = ca[(size_t)r * ld + i], gg = cg[(size_t)r * ld + i];
           const bool diag = (r == topo.ell_drank[i]);
           out[r0 + 3 * r + 0] = a.x;
           out[r0 + 3 * r + 1] = 0.0f;

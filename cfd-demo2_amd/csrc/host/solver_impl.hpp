@@ -96,8 +96,12 @@ struct Topology {
   // scalar CSR rows of the owned cells (init/mesh.rs:27-53), global columns,
   // and its ELL image [r*N + i] with signed local columns
   std::vector<uint32_t> srow, scol;
-  std::vector<int32_t> ell_col;
-  std::vector<uint32_t> ell_len, ell_drank;
+  uint32_t ld = 0;               // ELL slot stride (= npad)
+  std::vector<int32_t> ell_col;  // [r*ld + i]
+  std::vector<uint32_t> ell_len, ell_drank;  // [ld]
+  bool use16 = false;            // every |col - row| < 2^15: ell_col16 valid
+  std::vector<int16_t> ell_col16;
+  std::vector<uint8_t> ell_len8, ell_drank8;
 };
 
 // Throws std::invalid_argument on inconsistent meshes.
@@ -173,6 +177,9 @@ struct Solver {
   FaceSlots fs{};
   float* d_vol = nullptr;
   int32_t* d_scol = nullptr;
+  int16_t* d_scol16 = nullptr;
+  uint8_t* d_slen8 = nullptr;
+  uint8_t* d_sdrank8 = nullptr;
   uint32_t* d_slen = nullptr;
   uint32_t* d_sdrank = nullptr;
   // ring of 3 FluidState slots (SoA) + prepare's d_p / grad_p scratch

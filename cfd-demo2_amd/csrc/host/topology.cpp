@@ -131,25 +131,44 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
   t.glo = (uint32_t)(std::lower_bound(t.ghost.begin(), t.ghost.end(), c0) - t.ghost.begin());
   t.ghi = (uint32_t)t.ghost.size() - t.glo;
 
-  // scalar-row ELL image (signed local columns) + diagonal rank (init/mesh.rs:201-212)
-  t.ell_col.assign((size_t)ws * N, 0);
-  t.ell_len.resize(N);
-  t.ell_drank.resize(N);
-  for (uint32_t li = 0; li < N; ++li) {
-    const uint32_t a = t.srow[li], b = t.srow[li + 1];
+  // scalar-row ELL image (signed local columns) + diagonal rank (init/mesh.rs:201-212),
+  // slot stride ld = npad (16-byte groups of 4 rows); 16-bit column deltas and
+  // u8 lengths / ranks for the 4-rows-per-thread Krylov kernels
+  const uint32_t ld = t.npad;
+  t.ld = ld;
+  t.ell_col.assign((size_t)ws * ld, 0);
+  t.ell_len.assign(ld, 0);
+  t.ell_drank.assign(ld, 0);
+  t.ell_len8.assign(ld, 0);
+  t.ell_drank8.assign(ld, 0);
+  bool small = true;
+  for (uint32_t li = 0; li < ld; ++li) {
+    const uint32_t a = li < N ? t.srow[li] : 0, b = li < N ? t.srow[li + 1] : 0;
     t.ell_len[li] = b - a;
-    bool found = false;
+    bool found = li >= N;
     for (uint32_t k = a; k < b; ++k) {
       const uint32_t r = k - a;
-      t.ell_col[(size_t)r * N + li] = t.rel(t.scol[k]);
+      const int32_t c = t.rel(t.scol[k]);
+      t.ell_col[(size_t)r * ld + li] = c;
+      const int64_t d = (int64_t)c - (int64_t)li;
+      if (d < -32768 || d > 32767) small = false;
       if (t.scol[k] == c0 + li) {
         t.ell_drank[li] = r;
         found = true;
       }
     }
     if (!found) throw std::invalid_argument("Diagonal not found in CSR cols");
-    // unused ELL slots hold the row's own index (never read)
-    for (uint32_t r = b - a; r < (uint32_t)ws; ++r) t.ell_col[(size_t)r * N + li] = (int32_t)li;
+    // unused ELL slots / padding rows hold the row's own index (never read)
+    for (uint32_t r = b - a; r < (uint32_t)ws; ++r) t.ell_col[(size_t)r * ld + li] = (int32_t)li;
+    t.ell_len8[li] = (uint8_t)t.ell_len[li];
+    t.ell_drank8[li] = (uint8_t)t.ell_drank[li];
+  }
+  t.use16 = small;
+  t.ell_col16.clear();
+  if (small) {
+    t.ell_col16.resize(t.ell_col.size());
+    for (size_t e = 0; e < t.ell_col.size(); ++e)
+      t.ell_col16[e] = (int16_t)(t.ell_col[e] - (int32_t)(e % ld));
   }
 
   // face slots
