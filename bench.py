@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--inner", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--round", default="r01")
+    ap.add_argument("--mesh-cache", default=None,
+                    help="binary mesh file: loaded if present, else generated and saved (A/B runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,7 +122,13 @@ def main():
     h, _, cfg_idx = CONFIGS[args.config]
     h_run = h / (world ** 0.5)  # weak scaling: ~N x the 1-GPU cell count
     t0 = time.perf_counter()
-    mesh = bench_channel(h_run, 100)
+    if args.mesh_cache and os.path.exists(args.mesh_cache):
+        from cfd2_amd.mesh import Mesh
+        mesh = Mesh.load(args.mesh_cache)
+    else:
+        mesh = bench_channel(h_run, 100)
+        if args.mesh_cache and rank == 0:
+            mesh.save(args.mesh_cache)
     n_global = mesh.num_cells()
     log(f"[rank {rank}] mesh {n_global} cells / {mesh.num_faces()} faces in {time.perf_counter() - t0:.1f}s")
 

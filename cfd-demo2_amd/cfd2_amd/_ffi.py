@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libcfd2_amd.so")
+# CFD2_AMD_LIB selects an alternative build of the same library (A/B variants
+# made by tools/ab_variants.py); default: the in-tree build.
+LIB_PATH = os.environ.get("CFD2_AMD_LIB") or os.path.join(_HERE, "_lib", "libcfd2_amd.so")
 
 u32p = C.POINTER(C.c_uint32)
 f64p = C.POINTER(C.c_double)

@@ -493,11 +493,24 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
   *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
 }
 
+// Slot-group sizes of the 4-cells-per-thread kernels (all loads of a group are
+// issued before the first use).  Build-time tunables (tools/ab_variants.py).
+#ifndef CFD_SPMV_U
+#define CFD_SPMV_U 2
+#endif
+#ifndef CFD_PREDICT_U
+#define CFD_PREDICT_U 2
+#endif
+#ifndef CFD_CORRECT_U
+#define CFD_CORRECT_U 4
+#endif
+
 // spmv (gmres_ops.wgsl:63-81) on compressed blocks, 4 cells (12 rows) per
 // thread; per-row term order identical to the CSR row (neighbour-major, u,v,p).
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
+  constexpr int U = CFD_SPMV_U;
   const uint32_t i0 = 4 * row_id();
   if (i0 >= A.N) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
@@ -506,31 +519,56 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   load2x4(A.cdiag2 + i0, d2);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float su[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r = 0; r < maxlen; ++r) {
-    const size_t off = (size_t)r * A.ld + i0;
-    float2 a[4], g[4];
-    load2x4(A.cval_a + off, a);
-    load2x4(A.cval_g + off, g);
-    int c[4];
-    ccols4<D16>(A, off, i0, c);
+  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
+    float2 a[U][4], g[U][4];
+    int c[U][4];
+    float xg[U][4][3];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (r >= u4(ln, k)) continue;
-      const bool dg = (r == u4(dr, k));
-      const float uu = a[k].x, pp = a[k].y, up = g[k].x, vp = g[k].y;
-      const float pu = dg ? d2[k].x : g[k].x, pv = dg ? d2[k].y : g[k].y;
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[k];
-      const float xu = x[j], xv = x[j + 1], xp = x[j + 2];
-      su[k] += uu * xu;
-      su[k] += 0.0f * xv;
-      su[k] += up * xp;
-      sv[k] += 0.0f * xu;
-      sv[k] += uu * xv;
-      sv[k] += vp * xp;
-      sp[k] += pu * xu;
-      sp[k] += pv * xv;
-      sp[k] += pp * xp;
+    for (int u = 0; u < U; ++u) {
+      const uint32_t r = r0 + u;
+      if (U == 1 || r < maxlen) {
+        const size_t off = (size_t)r * A.ld + i0;
+        load2x4(A.cval_a + off, a[u]);
+        load2x4(A.cval_g + off, g[u]);
+        ccols4<D16>(A, off, i0, c[u]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          a[u][k] = g[u][k] = make_float2(0.0f, 0.0f);
+          c[u][k] = (int)i0 + k;
+        }
+      }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool on = r0 + u < u4(ln, k);
+        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+        xg[u][k][0] = on ? x[j] : 0.0f;
+        xg[u][k][1] = on ? x[j + 1] : 0.0f;
+        xg[u][k][2] = on ? x[j + 2] : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t r = r0 + u;
+        if (r >= u4(ln, k)) continue;
+        const bool dg = (r == u4(dr, k));
+        const float uu = a[u][k].x, pp = a[u][k].y, up = g[u][k].x, vp = g[u][k].y;
+        const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
+        const float xu = xg[u][k][0], xv = xg[u][k][1], xp = xg[u][k][2];
+        su[k] += uu * xu;
+        su[k] += 0.0f * xv;
+        su[k] += up * xp;
+        sv[k] += 0.0f * xu;
+        sv[k] += uu * xv;
+        sv[k] += vp * xp;
+        sp[k] += pu * xu;
+        sp[k] += pv * xv;
+        sp[k] += pp * xp;
+      }
   }
   const float o[12] = {su[0], sv[0], sp[0], su[1], sv[1], sp[1], su[2], sv[2], sp[2], su[3], sv[3], sp[3]};
   store12(y + 3 * (size_t)i0, o);
@@ -687,6 +725,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             const float* __restrict__ dinv_p,
                                                             float* temp_p, float* p_sol,
                                                             float* p_prev) {
+  constexpr int U = CFD_PREDICT_U;
   const uint32_t i0 = 4 * row_id();
   if (i0 >= A.N) return;
   const float sc = binv[jv];
@@ -700,25 +739,49 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
   float2 d2[4];
   load2x4(A.cdiag2 + i0, d2);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
-  for (uint32_t r = 0; r < maxlen; ++r) {
-    const size_t off = (size_t)r * A.ld + i0;
-    float2 g[4];
-    load2x4(A.cval_g + off, g);
-    int c[4];
-    ccols4<D16>(A, off, i0, c);
+  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
+    float2 g[U][4];
+    int c[U][4];
+    float gd[U][4], gu[U][4], gv[U][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (r >= u4(ln, k)) continue;
-      const bool dg = (r == u4(dr, k));
-      const float pu = dg ? d2[k].x : g[k].x, pv = dg ? d2[k].y : g[k].y;
-      const float dj = dinv_uv[c[k]];
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[k];
-      const float ru = sc * w_in[j], rv = sc * w_in[j + 1];
-      const float zu = ru * dj;
-      const float zv = rv * dj;
-      rhs[k] -= pu * zu;
-      rhs[k] -= pv * zv;
+    for (int u = 0; u < U; ++u) {
+      const uint32_t r = r0 + u;
+      if (U == 1 || r < maxlen) {
+        const size_t off = (size_t)r * A.ld + i0;
+        load2x4(A.cval_g + off, g[u]);
+        ccols4<D16>(A, off, i0, c[u]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          g[u][k] = make_float2(0.0f, 0.0f);
+          c[u][k] = (int)i0 + k;
+        }
+      }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool on = r0 + u < u4(ln, k);
+        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+        gd[u][k] = on ? dinv_uv[c[u][k]] : 0.0f;
+        gu[u][k] = on ? w_in[j] : 0.0f;
+        gv[u][k] = on ? w_in[j + 1] : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t r = r0 + u;
+        if (r >= u4(ln, k)) continue;
+        const bool dg = (r == u4(dr, k));
+        const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
+        const float ru = sc * gu[u][k], rv = sc * gv[u][k];
+        const float zu = ru * gd[u][k];
+        const float zv = rv * gd[u][k];
+        rhs[k] -= pu * zu;
+        rhs[k] -= pv * zv;
+      }
   }
   const float4 dp = *reinterpret_cast<const float4*>(dinv_p + i0);
   *reinterpret_cast<float4*>(temp_p + i0) = make_float4(rhs[0], rhs[1], rhs[2], rhs[3]);
@@ -763,19 +826,38 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r = 0; r < maxlen; ++r) {
-    const size_t off = (size_t)r * A.ld + i0;
-    float2 g[4];
-    load2x4(A.cval_g + off, g);
-    int c[4];
-    ccols4<D16>(A, off, i0, c);
+  constexpr int U = CFD_CORRECT_U;
+  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
+    float2 g[U][4];
+    int c[U][4];
+    float pj[U][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (r >= u4(ln, k)) continue;
-      const float pj = p_sol[c[k]];
-      cu[k] += g[k].x * pj;
-      cv[k] += g[k].y * pj;
+    for (int u = 0; u < U; ++u) {
+      const uint32_t r = r0 + u;
+      if (r < maxlen) {
+        const size_t off = (size_t)r * A.ld + i0;
+        load2x4(A.cval_g + off, g[u]);
+        ccols4<D16>(A, off, i0, c[u]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          g[u][k] = make_float2(0.0f, 0.0f);
+          c[u][k] = (int)i0 + k;
+        }
+      }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pj[u][k] = (r0 + u < u4(ln, k)) ? p_sol[c[u][k]] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (r0 + u >= u4(ln, k)) continue;
+        cu[k] += g[u][k].x * pj[u][k];
+        cv[k] += g[u][k].y * pj[u][k];
+      }
   }
   const float sc = binv[jv];
   float wo[12], o[12];
@@ -840,6 +922,39 @@ __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uin
 }
 
 
+// Slots are processed in groups of kU with every load of the group issued
+// before the first use (val/col, then the x gathers): ~kU x more memory-level
+// parallelism per wave than a slot-at-a-time loop.  Accumulation order per
+// row is unchanged (slot order).
+#ifndef CFD_AMG_U
+#define CFD_AMG_U 4
+#endif
+constexpr int kU = CFD_AMG_U;
+
+template <bool D16>
+__device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
+                                             uint32_t i0, uint32_t r0, uint32_t maxlen, const uchar4 ln,
+                                             float4 v[kU], float xg[kU][4]) {
+  int c[kU][4];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint32_t r = r0 + u;
+    if (r < maxlen) {
+      const size_t off = (size_t)r * L.stride + i0;
+      v[u] = *reinterpret_cast<const float4*>(L.val + off);
+      load_cols4<D16>(L, off, i0, c[u]);
+    } else {
+      v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c[u][k] = (int)i0 + k;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kU; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xg[u][k] = (r0 + u < u4(ln, k)) ? x[c[u][k]] : 0.0f;
+}
+
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
@@ -847,26 +962,45 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
                                                        float* __restrict__ x_out) {
   const uint32_t i0 = 4 * row_id();
   if (i0 >= L.n) return;
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r = 0; r < maxlen; ++r) {
-    const size_t off = (size_t)r * L.stride + i0;
-    const float4 v = *reinterpret_cast<const float4*>(L.val + off);
-    int c[4];
-    load_cols4<D16>(L, off, i0, c);
+  for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) {
+    float4 v[kU];
+    float xg[kU][4];
+    gather_group<D16>(L, x, i0, r0, maxlen, ln, v, xg);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r < u4(ln, k)) sg[k] += f4(v, k) * x[c[k]];
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (r0 + u < u4(ln, k)) sg[k] += f4(v[u], k) * xg[u][k];
   }
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
   float4 o;
   o.x = wmix(xx.x, (bb.x - sg[0]) / dd.x, 0.8f);
   o.y = wmix(xx.y, (bb.y - sg[1]) / dd.y, 0.8f);
   o.z = wmix(xx.z, (bb.z - sg[2]) / dd.z, 0.8f);
   o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
+  *reinterpret_cast<float4*>(x_out + i0) = o;
+}
+
+// smooth_op on a level whose x is identically +0 (every coarse level's
+// pre-smoother: restrict just cleared it): sigma = +0, so the sweep is the
+// elementwise x_out = mix(+0, (b - 0)/diag, 0.8) -- the same f32 operations
+// as k_amg_smooth without reading the matrix.
+__global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const float* __restrict__ b,
+                                                            float* __restrict__ x_out) {
+  const uint32_t i0 = 4 * row_id();
+  if (i0 >= L.n) return;
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
+  float4 o;
+  o.x = wmix(0.0f, (bb.x - 0.0f) / dd.x, 0.8f);
+  o.y = wmix(0.0f, (bb.y - 0.0f) / dd.y, 0.8f);
+  o.z = wmix(0.0f, (bb.z - 0.0f) / dd.z, 0.8f);
+  o.w = wmix(0.0f, (bb.w - 0.0f) / dd.w, 0.8f);
   *reinterpret_cast<float4*>(x_out + i0) = o;
 }
 
@@ -878,26 +1012,26 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
                                                          float* __restrict__ rr) {
   const uint32_t i0 = 4 * row_id();
   if (i0 >= L.n) return;
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
+  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r = 0; r <= maxlen; ++r) {
+  for (uint32_t r0 = 0; r0 <= maxlen; r0 += kU) {  // r = maxlen: a diagonal ranked last
+    float4 v[kU];
+    float xg[kU][4];
+    gather_group<D16>(L, x, i0, r0, maxlen, ln, v, xg);
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r == u4(dr, k)) ax[k] += f4(dv, k) * f4(xx, k);
-    if (r == maxlen) break;
-    const size_t off = (size_t)r * L.stride + i0;
-    const float4 v = *reinterpret_cast<const float4*>(L.val + off);
-    int c[4];
-    load_cols4<D16>(L, off, i0, c);
+    for (int u = 0; u < kU; ++u)
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (r < u4(ln, k)) ax[k] += f4(v, k) * x[c[k]];
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t r = r0 + u;
+        if (r == u4(dr, k)) ax[k] += f4(dv, k) * f4(xx, k);
+        if (r < u4(ln, k)) ax[k] += f4(v[u], k) * xg[u][k];
+      }
   }
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
   float4 o;
   o.x = bb.x - ax[0];
   o.y = bb.y - ax[1];
@@ -1266,6 +1400,9 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
     hipLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
   else
     hipLaunchKernelGGL(k_amg_smooth<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
+}
+void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
+  if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
 }
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
   if (!L.n) return;

@@ -208,6 +208,8 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
                      hipStream_t s);
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
                        hipStream_t s);
+// pre-smoother of a level whose x is identically +0 (bit-identical to launch_amg_smooth then)
+void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,
                          hipStream_t s);
 // coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused); on a

@@ -633,7 +633,7 @@ void Solver::ensure_amg() {
   amg_built = true;
 }
 
-void Solver::amg_smooth(size_t li, float*& xcur, const float* b) {
+void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {
   AmgGpuLevel& L = levels[li];
   const bool timed = prof && li == 0;
   if (timed) {
@@ -653,7 +653,10 @@ void Solver::amg_smooth(size_t li, float*& xcur, const float* b) {
     }
     CFD_HIP(hipEventRecord(prof_ev[prof_used], stream));
   }
-  launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
+  if (x_zero)
+    launch_amg_smooth_zero(L.dev, b, L.xt, stream);
+  else
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
   if (timed) {
     CFD_HIP(hipEventRecord(prof_ev[prof_used + 1], stream));
     prof_used += 2;
@@ -682,7 +685,7 @@ void Solver::v_cycle() {
   if (D > 0) hx(0);
   for (int i = 0; i < down; ++i) {
     AmgGpuLevel& Lv = levels[i];
-    amg_smooth(i, Lv.x, Lv.b);
+    amg_smooth(i, Lv.x, Lv.b, i > 0);  // coarse x was cleared by the restriction
     hx(i);
     launch_amg_residual(Lv.dev, Lv.x, Lv.b, Lv.r, stream);
     AmgGpuLevel& C = levels[i + 1];

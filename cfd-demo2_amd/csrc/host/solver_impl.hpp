@@ -271,7 +271,7 @@ struct Solver {
   void ensure_amg();
   void precondition(int j, float* z);
   void v_cycle();
-  void amg_smooth(size_t li, float*& x, const float* b);
+  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);
   float norm_blocking(const float* v, int mode, int slot);
   float residual_into_v0_blocking();
   void check_evolution();
