@@ -496,10 +496,10 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
 // Slot-group sizes of the 4-cells-per-thread kernels (all loads of a group are
 // issued before the first use).  Build-time tunables (tools/ab_variants.py).
 #ifndef CFD_SPMV_U
-#define CFD_SPMV_U 2
+#define CFD_SPMV_U 4
 #endif
 #ifndef CFD_PREDICT_U
-#define CFD_PREDICT_U 2
+#define CFD_PREDICT_U 4
 #endif
 #ifndef CFD_CORRECT_U
 #define CFD_CORRECT_U 4
@@ -511,8 +511,8 @@ template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
   constexpr int U = CFD_SPMV_U;
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= A.N) return;
+  const uint32_t i0 = A.r0 + 4 * row_id();
+  if (i0 >= A.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
   float2 d2[4];
@@ -726,8 +726,8 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             float* temp_p, float* p_sol,
                                                             float* p_prev) {
   constexpr int U = CFD_PREDICT_U;
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= A.N) return;
+  const uint32_t i0 = A.r0 + 4 * row_id();
+  if (i0 >= A.r1) return;
   const float sc = binv[jv];
   float wo[12];
   load12(w_in + 3 * (size_t)i0, wo);
@@ -821,8 +821,8 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
                                                             const float* __restrict__ p_sol,
                                                             const float* __restrict__ dinv_uv,
                                                             float* __restrict__ z) {
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= A.N) return;
+  const uint32_t i0 = A.r0 + 4 * row_id();
+  if (i0 >= A.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -960,8 +960,8 @@ template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= L.n) return;
+  const uint32_t i0 = L.r0 + 4 * row_id();
+  if (i0 >= L.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1010,8 +1010,8 @@ template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= L.n) return;
+  const uint32_t i0 = L.r0 + 4 * row_id();
+  if (i0 >= L.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
@@ -1332,8 +1332,8 @@ void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, 
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
 }
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
-  if (!A.N) return;
-  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.r1 <= A.r0) return;
+  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
   if (A.use16)
     hipLaunchKernelGGL(k_spmv<true>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
   else
@@ -1361,8 +1361,8 @@ void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int 
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s) {
-  if (!A.N) return;
-  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.r1 <= A.r0) return;
+  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_predict<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
                        temp_p, p_sol, p_prev);
@@ -1379,8 +1379,8 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
 }
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
-  if (!A.N) return;
-  const unsigned nb = grid_for((A.N + 3) / 4);
+  if (A.r1 <= A.r0) return;
+  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_correct<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
   else
@@ -1394,8 +1394,8 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for(n)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s) {
-  if (!L.n) return;
-  const unsigned nb = grid_for((L.n + 3) / 4);
+  if (L.r1 <= L.r0) return;
+  const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
   if (L.use16)
     hipLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
   else
@@ -1405,8 +1405,8 @@ void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, 
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
 }
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
-  if (!L.n) return;
-  const unsigned nb = grid_for((L.n + 3) / 4);
+  if (L.r1 <= L.r0) return;
+  const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
   if (L.use16)
     hipLaunchKernelGGL(k_amg_residual<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
   else

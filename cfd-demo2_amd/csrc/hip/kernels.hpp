@@ -108,6 +108,7 @@ struct AssembleArgs {
 // whole matrix allows it, lengths / diagonal ranks u8.
 struct CoupledMatrix {
   uint32_t N;
+  uint32_t r0, r1;        // rows this launch processes (multiples of 4 except r1 = N)
   uint32_t ld;            // slot stride (N rounded up to 64)
   int ws;
   int use16;
@@ -129,6 +130,7 @@ struct CoupledMatrix {
 // row sum accumulates in the reference order.
 struct AmgLevelDev {
   uint32_t n;
+  uint32_t r0, r1;       // rows a smoother / residual launch processes (default 0, n)
   uint32_t stride;       // row stride of the ELL slots (n rounded up to 64)
   int w;                 // ELL width (max off-diagonals per row)
   int use16;             // 1: col16 holds deltas; 0: col32 holds absolute columns

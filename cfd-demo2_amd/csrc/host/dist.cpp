@@ -45,6 +45,18 @@ HaloPlan build_halo_plan(const std::vector<uint64_t>& starts, int rank, const ui
     }
   }
   HaloPlan P;
+  {  // boundary row ranges (columns ascend: a row's first / last column decide)
+    int64_t last_lo = -1, first_hi = n;
+    for (uint32_t li = 0; li < n; ++li) {
+      if (row[li + 1] == row[li]) continue;
+      if (col[row[li]] < c0) last_lo = li;
+      if (col[row[li + 1] - 1] >= starts[rank + 1] && first_hi == (int64_t)n) first_hi = li;
+    }
+    P.lo_end = (uint32_t)((last_lo + 1 + 3) & ~(int64_t)3);
+    P.hi_begin = (uint32_t)(first_hi & ~(int64_t)3);
+    if (P.lo_end > n) P.lo_end = n;
+    if (P.hi_begin < P.lo_end) P.hi_begin = P.lo_end;
+  }
   for (int q = 0; q < R; ++q) {
     if (q == rank) continue;
     const auto lo = std::lower_bound(ghost.begin(), ghost.end(), (uint32_t)starts[q]);

@@ -29,6 +29,9 @@ struct HaloPlan {
   int32_t* d_send_idx = nullptr;
   float* d_stage = nullptr;       // pack buffer (send_idx.size() x max comps)
   int max_comps = 0;
+  // rows reading ghosts: [0, lo_end) (lower ghosts) and [hi_begin, n) (upper);
+  // the rows between are interior and overlap the exchange (multiples of 4)
+  uint32_t lo_end = 0, hi_begin = 0;
 };
 
 // Ghost list (ascending) of owned rows [c0, c1) whose global CSR pattern is

@@ -67,6 +67,9 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   CFD_HIP(hipSetDevice(device));
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
+    CFD_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    CFD_HIP(hipEventCreateWithFlags(&hev_pack, hipEventDisableTiming));
+    CFD_HIP(hipEventCreateWithFlags(&hev_done, hipEventDisableTiming));
     cell_plan = build_halo_plan(starts, rk, topo.srow.data(), N, topo.scol.data(), topo.ghost, topo.glo,
                                 topo.npad);
     make_plan_buffers(cell_plan, 8);
@@ -169,13 +172,20 @@ Solver::~Solver() {
     if (e) (void)hipEventDestroy(e);
   for (auto e : prof_ev) (void)hipEventDestroy(e);
   if (h_pin) (void)hipHostFree(h_pin);
+  if (cstream) (void)hipStreamSynchronize(cstream);
+  if (hev_pack) (void)hipEventDestroy(hev_pack);
+  if (hev_done) (void)hipEventDestroy(hev_done);
+  comm.reset();
   arena.release();
+  if (cstream) (void)hipStreamDestroy(cstream);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
 CoupledMatrix Solver::cmat() const {
   CoupledMatrix A;
   A.N = N;
+  A.r0 = 0;
+  A.r1 = N;
   A.ld = topo.ld;
   A.ws = topo.ws;
   A.use16 = topo.use16 ? 1 : 0;
@@ -264,6 +274,13 @@ void Solver::get_d_p(double* out) {
 // then one grouped transfer per (peer, field) straight into the ghost slots.
 void Solver::halo(HaloPlan& plan, std::initializer_list<HField> fields) {
   if (!dist()) return;
+  halo_begin(plan, fields);
+  halo_end();
+}
+
+void Solver::halo_end() { CFD_HIP(hipStreamWaitEvent(stream, hev_done, 0)); }
+
+void Solver::halo_begin(HaloPlan& plan, std::initializer_list<HField> fields) {
   const uint32_t ns = (uint32_t)plan.send_idx.size();
   PackArgs pa{};
   int tot = 0;
@@ -290,7 +307,10 @@ void Solver::halo(HaloPlan& plan, std::initializer_list<HField> fields) {
       msgs.push_back(mm);
     }
   }
-  comm->exchange(msgs, stream);
+  CFD_HIP(hipEventRecord(hev_pack, stream));
+  CFD_HIP(hipStreamWaitEvent(cstream, hev_pack, 0));
+  comm->exchange(msgs, cstream);
+  CFD_HIP(hipEventRecord(hev_done, cstream));
 }
 
 // ghosts of the current FluidState slot: u, p (all = also d_p, grad_p)
@@ -466,6 +486,8 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
   }
   G.nnz = nnz;
   G.dev.n = n;
+  G.dev.r0 = 0;
+  G.dev.r1 = n;
   G.dev.stride = st;
   G.dev.w = wmax;
   G.dev.use16 = small_delta ? 1 : 0;
@@ -484,7 +506,7 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 // scalar matrix, build the frozen hierarchy on the host, upload it.  A
 // distributed rank all-gathers the scalar matrix, builds the same partition-
 // aware hierarchy as every other rank, and keeps its rows of the levels with
-// more than CFD_AMG_REPLICATE_ROWS rows (default 32768); the small levels are
+// more than CFD_AMG_REPLICATE_ROWS rows (default 262144); the small levels are
 // replicated on every rank.
 void Solver::ensure_amg() {
   if (amg_built) return;
@@ -523,7 +545,7 @@ void Solver::ensure_amg() {
   amg_g = 0;
   if (dist()) {
     const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
-    const uint64_t rep = ev ? std::strtoull(ev, nullptr, 10) : 32768u;
+    const uint64_t rep = ev ? std::strtoull(ev, nullptr, 10) : 262144u;
     amg_g = L;
     for (int li = 1; li < L; ++li)
       if (H[li].A.rows <= rep) {
@@ -679,15 +701,38 @@ void Solver::v_cycle() {
   // while the level-0 smoother is being timed on a one-level hierarchy
   const int tf = (prof && L == 1) ? L : std::max({tail_first, 1, D});
   const int down = std::min(tf, L - 1);
-  auto hx = [&](int i) {
-    if (levels[i].dist) halo(levels[i].plan, {{levels[i].x, 1}});
+  // smoother sweep; on a distributed level the x halo overlaps the interior rows
+  auto sm = [&](int i, bool x_zero) {
+    AmgGpuLevel& Lv = levels[i];
+    if (!Lv.dist || x_zero) {
+      amg_smooth(i, Lv.x, Lv.b, x_zero);
+      return;
+    }
+    overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b) {
+      AmgLevelDev d = Lv.dev;
+      d.r0 = a;
+      d.r1 = b;
+      launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream);
+    });
+    std::swap(Lv.x, Lv.xt);
   };
-  if (D > 0) hx(0);
+  auto res = [&](int i) {
+    AmgGpuLevel& Lv = levels[i];
+    auto f = [&](uint32_t a, uint32_t b) {
+      AmgLevelDev d = Lv.dev;
+      d.r0 = a;
+      d.r1 = b;
+      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream);
+    };
+    if (Lv.dist)
+      overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, f);
+    else
+      f(0, Lv.dev.n);
+  };
   for (int i = 0; i < down; ++i) {
     AmgGpuLevel& Lv = levels[i];
-    amg_smooth(i, Lv.x, Lv.b, i > 0);  // coarse x was cleared by the restriction
-    hx(i);
-    launch_amg_residual(Lv.dev, Lv.x, Lv.b, Lv.r, stream);
+    sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
+    res(i);
     AmgGpuLevel& C = levels[i + 1];
     if (!Lv.dist) {
       launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream);
@@ -704,17 +749,12 @@ void Solver::v_cycle() {
   if (tf < L) {
     launch_amg_tail(d_tail, tf, L, stream);
   } else {
-    for (int s = 0; s < 10; ++s) {
-      if (s > 0) hx(L - 1);
-      amg_smooth(L - 1, levels[L - 1].x, levels[L - 1].b);
-    }
+    for (int s = 0; s < 10; ++s) sm(L - 1, s == 0 && L > 1);
   }
   for (int ii = down - 1; ii >= 0; --ii) {
     launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
-    hx(ii);
-    amg_smooth(ii, levels[ii].x, levels[ii].b);
+    sm(ii, false);
   }
-  if (D > 0) hx(0);  // the velocity correction reads neighbours' p_sol
   // every level performs an even number of sweeps, so level 0 ends in p_sol
   if (levels[0].x != p_sol) throw std::logic_error("AMG level-0 ping-pong parity");
 }
@@ -724,8 +764,13 @@ void Solver::precondition(int j, float* z) {
   const CoupledMatrix A = cmat();
   const bool jacobi = constants.precond_type != 1;
   float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
-  if (dist()) halo(cell_plan, {{v, 3}});  // the prediction reads neighbours' r_u, r_v
-  launch_precond_predict(A, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
+  // the prediction reads neighbours' r_u, r_v
+  overlapped(cell_plan, {{v, 3}}, N, [&](uint32_t a, uint32_t b) {
+    CoupledMatrix Ar = A;
+    Ar.r0 = a;
+    Ar.r1 = b;
+    launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
+  });
   bool in_sol = true;
   if (!jacobi) {
     v_cycle();
@@ -740,9 +785,15 @@ void Solver::precondition(int j, float* z) {
       launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
       in_sol = !in_sol;
     }
-    if (dist()) halo(cell_plan, {{in_sol ? p_sol : temp, 1}});
   }
-  launch_precond_correct(A, v, binv, j, in_sol ? p_sol : temp, dinv_uv, z, stream);
+  float* ps = in_sol ? p_sol : temp;
+  // the velocity correction reads neighbours' p_sol
+  overlapped(cell_plan, {{ps, 1}}, N, [&](uint32_t a, uint32_t b) {
+    CoupledMatrix Ar = A;
+    Ar.r0 = a;
+    Ar.r1 = b;
+    launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream);
+  });
 }
 
 float Solver::norm_blocking(const float* v, int mode, int slot) {
@@ -759,8 +810,12 @@ float Solver::norm_blocking(const float* v, int mode, int slot) {
 // g = [||r||, 0, ...] (coupled_solver_fgmres.rs:1880-1890, 2380-2392).
 float Solver::residual_into_v0_blocking() {
   CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
-  if (dist()) halo(cell_plan, {{x, 3}});
-  launch_spmv(cmat(), x, w, stream);
+  overlapped(cell_plan, {{x, 3}}, N, [&](uint32_t a, uint32_t b) {
+    CoupledMatrix A = cmat();
+    A.r0 = a;
+    A.r1 = b;
+    launch_spmv(A, x, w, stream);
+  });
   launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
   return norm_blocking(basis, 2, 1);
 }
@@ -801,8 +856,12 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       ++total;
       float* zj = zvec + (size_t)j * stride;
       precondition(j, zj);
-      if (dist()) halo(cell_plan, {{zj, 3}});
-      launch_spmv(cmat(), zj, w, stream);
+      overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b) {
+        CoupledMatrix A = cmat();
+        A.r0 = a;
+        A.r1 = b;
+        launch_spmv(A, zj, w, stream);
+      });
       launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);
       const auto rd = combine(partial, nchunks, j + 1);
       launch_cgs_reduce(rd.first, rd.second, j, H, m1, stream);

@@ -290,6 +290,26 @@ struct Solver {
     int comps;
   };
   void halo(HaloPlan& plan, std::initializer_list<HField> fields);
+  // exchange on the comm stream; halo_end makes the compute stream wait for it
+  void halo_begin(HaloPlan& plan, std::initializer_list<HField> fields);
+  void halo_end();
+  // launch(r0, r1) over rows [0, n): interior rows overlap the halo exchange,
+  // boundary rows run after it (one GPU: a single launch over all rows)
+  template <class F>
+  void overlapped(HaloPlan& plan, std::initializer_list<HField> fields, uint32_t n, F&& launch) {
+    if (!dist()) {
+      launch(0u, n);
+      return;
+    }
+    halo_begin(plan, fields);
+    if (plan.hi_begin > plan.lo_end) launch(plan.lo_end, plan.hi_begin);
+    halo_end();
+    if (plan.lo_end > 0) launch(0u, plan.lo_end);
+    const uint32_t hb = plan.hi_begin > plan.lo_end ? plan.hi_begin : plan.lo_end;
+    if (n > hb) launch(hb, n);
+  }
+  hipStream_t cstream = nullptr;  // RCCL / peer-copy stream of the halo exchanges
+  hipEvent_t hev_pack = nullptr, hev_done = nullptr;
   void halo_state(bool all);
   std::pair<const float*, uint32_t> combine(const float* partial, uint32_t np, int nvec);
   void make_plan_buffers(HaloPlan& p, int max_comps);
