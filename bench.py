@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--inner", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--round", default="r01")
+    ap.add_argument("--inproc-ranks", type=int, default=0,
+                    help="test mode: run the distributed solver as R in-process ranks on GPU 0 "
+                         "(not a bench line; exercises the multi-GPU code path at scale on one GPU)")
     ap.add_argument("--mesh-cache", default=None,
                     help="binary mesh file: loaded if present, else generated and saved (A/B runs)")
     args = ap.parse_args()
@@ -121,6 +124,8 @@ def main():
 
     h, _, cfg_idx = CONFIGS[args.config]
     h_run = h / (world ** 0.5)  # weak scaling: ~N x the 1-GPU cell count
+    if args.inproc_ranks > 1:
+        h_run = h / (args.inproc_ranks ** 0.5)
     t0 = time.perf_counter()
     if args.mesh_cache and os.path.exists(args.mesh_cache):
         from cfd2_amd.mesh import Mesh
@@ -138,10 +143,21 @@ def main():
         uid = [dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         solver = GpuSolver.create_dist(mesh, world, rank, uid[0], device=local_rank, config=cfg)
+    elif args.inproc_ranks > 1:
+        from cfd2_amd import GpuGroup
+        solver = GpuGroup(mesh, args.inproc_ranks, config=cfg)
+        solver.num_cells = solver.ranks[0].num_cells
+        solver.profile_smoother = solver.ranks[0].profile_smoother
+        solver.step_algorithmic_bytes = solver.ranks[0].step_algorithmic_bytes
     else:
         solver = GpuSolver(mesh, config=cfg, device=0)
     n_cells = solver.num_cells  # cells this rank owns
     setup_solver(solver)
+    if world > 1 or args.inproc_ranks > 1:
+        del mesh  # the solver keeps what it needs; free the global mesh
+        import gc
+        gc.collect()
+        mesh = None
     log(f"[rank {rank}] solver created in {time.perf_counter() - t0:.1f}s (owns {n_cells} cells)")
 
     def barrier_sync():
@@ -222,7 +238,7 @@ def main():
         "step_algorithmic_gbs": step_bytes / (ms_per_step / 1e3) / 1e9,
         "linear_iterations_last_step": int(info.total_linear_iterations),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and mesh is not None and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(mesh, n_cells, args.outer, args.inner)
         except Exception as e:  # the baseline is reported, never the target

@@ -655,33 +655,41 @@ void Solver::ensure_amg() {
   amg_built = true;
 }
 
+// HIP events around level-0 smoother launches (bench roofline); the pool is
+// drained into prof_ms when full.
+void Solver::prof_begin() {
+  if (prof_used + 2 > prof_ev.size()) {
+    CFD_HIP(hipStreamSynchronize(stream));
+    for (size_t k = 0; k + 1 < prof_used; k += 2) {
+      float ms = 0.0f;
+      CFD_HIP(hipEventElapsedTime(&ms, prof_ev[k], prof_ev[k + 1]));
+      prof_ms += ms;
+    }
+    prof_used = 0;
+    while (prof_ev.size() < 512) {
+      hipEvent_t e;
+      CFD_HIP(hipEventCreate(&e));
+      prof_ev.push_back(e);
+    }
+  }
+  CFD_HIP(hipEventRecord(prof_ev[prof_used], stream));
+}
+
+void Solver::prof_end() {
+  CFD_HIP(hipEventRecord(prof_ev[prof_used + 1], stream));
+  prof_used += 2;
+}
+
 void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {
   AmgGpuLevel& L = levels[li];
   const bool timed = prof && li == 0;
-  if (timed) {
-    if (prof_used + 2 > prof_ev.size()) {  // drain the pool
-      CFD_HIP(hipStreamSynchronize(stream));
-      for (size_t k = 0; k + 1 < prof_used; k += 2) {
-        float ms = 0.0f;
-        CFD_HIP(hipEventElapsedTime(&ms, prof_ev[k], prof_ev[k + 1]));
-        prof_ms += ms;
-      }
-      prof_used = 0;
-      while (prof_ev.size() < 512) {
-        hipEvent_t e;
-        CFD_HIP(hipEventCreate(&e));
-        prof_ev.push_back(e);
-      }
-    }
-    CFD_HIP(hipEventRecord(prof_ev[prof_used], stream));
-  }
+  if (timed) prof_begin();
   if (x_zero)
     launch_amg_smooth_zero(L.dev, b, L.xt, stream);
   else
     launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
   if (timed) {
-    CFD_HIP(hipEventRecord(prof_ev[prof_used + 1], stream));
-    prof_used += 2;
+    prof_end();
     prof_launches++;
   }
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
@@ -708,12 +716,16 @@ void Solver::v_cycle() {
       amg_smooth(i, Lv.x, Lv.b, x_zero);
       return;
     }
+    const bool timed = prof && i == 0;  // kernel time only: each part timed separately
     overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b) {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;
       d.r1 = b;
+      if (timed) prof_begin();
       launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream);
+      if (timed) prof_end();
     });
+    if (timed) prof_launches++;
     std::swap(Lv.x, Lv.xt);
   };
   auto res = [&](int i) {

@@ -272,6 +272,8 @@ struct Solver {
   void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);
+  void prof_begin();
+  void prof_end();
   float norm_blocking(const float* v, int mode, int slot);
   float residual_into_v0_blocking();
   void check_evolution();
