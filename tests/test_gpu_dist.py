@@ -102,3 +102,27 @@ def test_rccl_transport_selftest():
     """The RCCL transport (grouped send/recv + all-gather) on a 1-rank communicator."""
     from cfd2_amd.solver import rccl_selftest
     rccl_selftest(0)
+
+
+def test_group_c1_scale(replicate_rows):
+    """BASELINE configs[1] scale (~1M cells) on 4 in-process ranks, default
+    replication threshold: one real fixed-schedule step bit-exact vs oracle(4)."""
+    replicate_rows(262144)
+    mesh = bench_mesh(0.001723, 100)
+    cfg = dict(fixed_outer=1, fixed_inner=6)
+    g = GpuGroup(mesh, 4, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=4)
+    for s in (g, o):
+        s.set_dt(1e-3)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_alpha_u(0.7)
+        s.set_alpha_p(0.3)
+        s.set_precond_type(1)
+        s.initialize_history()
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"C1 R=4 step {k}")
+        _assert_same_info(g, o, f"C1 R=4 step {k}")
+    g.close()
