@@ -74,9 +74,19 @@ __device__ __forceinline__ float block_tree(float v, float* lds) {
 }
 
 // Canonical stage 2 over `np` partials by one 256-thread block.
+// (loads issued 8 at a time ahead of the sequential adds: same order, more
+// memory-level parallelism for the single-block stage-2 kernels)
 __device__ __forceinline__ float block_final(const float* partial, uint32_t np, float* lds) {
   float acc = 0.0f;
-  for (uint32_t q = threadIdx.x; q < np; q += kBlock) acc += partial[q];
+  uint32_t q = threadIdx.x;
+  for (; q + 7 * kBlock < np; q += 8 * kBlock) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = partial[q + u * kBlock];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; q < np; q += kBlock) acc += partial[q];
   return block_tree(acc, lds);
 }
 
@@ -391,8 +401,9 @@ __global__ void __launch_bounds__(kBlock) k_maxdiff_final(const uint32_t* __rest
   __shared__ uint32_t su[4], sp[4];
   uint32_t bu = 0, bp = 0;
   for (uint32_t q = threadIdx.x; q < nb; q += kBlock) {
-    bu = max(bu, blockmax[2 * q]);
-    bp = max(bp, blockmax[2 * q + 1]);
+    const uint2 v = *reinterpret_cast<const uint2*>(blockmax + 2 * (size_t)q);
+    bu = max(bu, v.x);
+    bp = max(bp, v.y);
   }
   for (int o = 32; o >= 1; o >>= 1) {
     bu = max(bu, (uint32_t)__shfl_xor((int)bu, o));
@@ -892,11 +903,40 @@ __global__ void k_solve_triangular(const float* H, const float* g, float* y, int
 __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __restrict__ z,
                                                      size_t stride, const float* __restrict__ y,
                                                      int k, size_t n) {
-  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t e = 4 * ((size_t)blockIdx.x * kBlock + threadIdx.x);
   if (e >= n) return;
-  float xv = x[e];
-  for (int ii = 0; ii < k; ++ii) xv = y[ii] * z[(size_t)ii * stride + e] + xv;
-  x[e] = xv;
+  if (e + 3 < n) {  // 4 elements per thread, 16-byte loads (slots are 256-byte aligned)
+    float4 xv = *reinterpret_cast<const float4*>(x + e);
+    int ii = 0;
+    for (; ii + 1 < k; ii += 2) {
+      const float4 z0 = *reinterpret_cast<const float4*>(z + (size_t)ii * stride + e);
+      const float4 z1 = *reinterpret_cast<const float4*>(z + (size_t)(ii + 1) * stride + e);
+      const float y0 = y[ii], y1 = y[ii + 1];
+      xv.x = y0 * z0.x + xv.x;
+      xv.y = y0 * z0.y + xv.y;
+      xv.z = y0 * z0.z + xv.z;
+      xv.w = y0 * z0.w + xv.w;
+      xv.x = y1 * z1.x + xv.x;
+      xv.y = y1 * z1.y + xv.y;
+      xv.z = y1 * z1.z + xv.z;
+      xv.w = y1 * z1.w + xv.w;
+    }
+    if (ii < k) {
+      const float4 z0 = *reinterpret_cast<const float4*>(z + (size_t)ii * stride + e);
+      const float y0 = y[ii];
+      xv.x = y0 * z0.x + xv.x;
+      xv.y = y0 * z0.y + xv.y;
+      xv.z = y0 * z0.z + xv.z;
+      xv.w = y0 * z0.w + xv.w;
+    }
+    *reinterpret_cast<float4*>(x + e) = xv;
+    return;
+  }
+  for (size_t f = e; f < n; ++f) {
+    float xv = x[f];
+    for (int ii = 0; ii < k; ++ii) xv = y[ii] * z[(size_t)ii * stride + f] + xv;
+    x[f] = xv;
+  }
 }
 
 // ------------------------------- AMG ---------------------------------------
@@ -1391,7 +1431,7 @@ void launch_solve_triangular(const float* H, const float* g, float* y, int k, in
 }
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
                      hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for(n)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
+  if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s) {
   if (L.r1 <= L.r0) return;
