@@ -1195,6 +1195,86 @@ __global__ void __launch_bounds__(1024) k_amg_tail(const AmgTailLevel* __restric
   }
 }
 
+// The same V-cycle tail with every vector of the tail levels in LDS (x, xt,
+// b, r per level; the matrices stay in L2): each phase is one global-latency
+// round (matrix row) + LDS gathers + a barrier.  Entry: b of `first` in global
+// memory, x of every tail level known zero (cleared by the restriction), so
+// each pre-smoother is the elementwise zero-x sweep.  Exit: x of `first`
+// written back for the host-side prolongation.
+__device__ __forceinline__ uint32_t r4(uint32_t n) { return (n + 3) & ~3u; }
+
+__global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __restrict__ tail, int first,
+                                                       int nlev) {
+  extern __shared__ float sm[];
+  const uint32_t t = threadIdx.x, nt = blockDim.x;
+  auto base = [&](int l) {
+    uint32_t o = 0;
+    for (int k = first; k < l; ++k) o += 4 * r4(tail[k].L.n);
+    return sm + o;
+  };
+  {
+    const AmgTailLevel T = tail[first];
+    float* B0 = base(first) + 2 * r4(T.L.n);
+    for (uint32_t i = t; i < T.L.n; i += nt) B0[i] = T.b[i];
+  }
+  __syncthreads();
+  for (int l = first; l + 1 < nlev; ++l) {
+    const AmgLevelDev L = tail[l].L;
+    const uint32_t nr = r4(L.n);
+    float* X = base(l);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    float* Rr = B + nr;
+    for (uint32_t i = t; i < L.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / L.de[i], 0.8f);
+    __syncthreads();
+    for (uint32_t i = t; i < L.n; i += nt) Rr[i] = residual_row(L, XT, B, i);
+    __syncthreads();
+    float* CB = base(l + 1) + 2 * r4(tail[l + 1].L.n);
+    for (uint32_t I = t; I < L.nc; I += nt) {
+      float sum = 0.0f;
+      for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * Rr[L.r_col[k]];
+      CB[I] = sum;
+    }
+    __syncthreads();
+  }
+  {
+    const AmgLevelDev L = tail[nlev - 1].L;
+    const uint32_t nr = r4(L.n);
+    float* X = base(nlev - 1);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    for (int s = 0; s < 10; ++s) {
+      if (s == 0) {
+        for (uint32_t i = t; i < L.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / L.de[i], 0.8f);
+      } else {
+        const float* xin = (s & 1) ? XT : X;
+        float* xout = (s & 1) ? X : XT;
+        for (uint32_t i = t; i < L.n; i += nt) xout[i] = smooth_row(L, xin, B, i);
+      }
+      __syncthreads();
+    }
+  }
+  for (int l = nlev - 2; l >= first; --l) {
+    const AmgLevelDev L = tail[l].L;
+    const uint32_t nr = r4(L.n);
+    float* X = base(l);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    const float* XC = base(l + 1);
+    for (uint32_t i = t; i < L.n; i += nt) {
+      float corr = 0.0f;
+      corr += 1.0f * XC[L.agg[i]];
+      XT[i] += corr;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < L.n; i += nt) X[i] = smooth_row(L, XT, B, i);
+    __syncthreads();
+  }
+  const AmgTailLevel T = tail[first];
+  const float* X0 = base(first);
+  for (uint32_t i = t; i < T.L.n; i += nt) T.x[i] = X0[i];
+}
+
 __global__ void __launch_bounds__(kBlock) k_fill(float* x, float v, size_t n) {
   const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (e < n) x[e] = v;
@@ -1460,8 +1540,18 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float*
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, x, xc);
 }
-void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, hipStream_t s) {
-  hipLaunchKernelGGL(k_amg_tail, dim3(1), dim3(1024), 0, s, tail, first, nlev);
+void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s) {
+  if (lds_bytes == 0) {
+    hipLaunchKernelGGL(k_amg_tail, dim3(1), dim3(1024), 0, s, tail, first, nlev);
+    return;
+  }
+  static bool attr = false;
+  if (!attr) {  // allow up to the whole 160 KiB LDS of a CU for this kernel
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_lds),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_amg_tail_lds, dim3(1), dim3(1024), lds_bytes, s, tail, first, nlev);
 }
 void launch_fill(float* x, float v, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);

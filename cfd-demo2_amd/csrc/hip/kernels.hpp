@@ -221,7 +221,9 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, 
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).
-void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, hipStream_t s);
+// lds_bytes > 0: the LDS-resident version (needs every tail vector in <= kTailLdsMax bytes)
+constexpr size_t kTailLdsMax = 160 * 1024 - 1024;
+void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
 void launch_fill(float* x, float v, size_t n, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:

@@ -637,6 +637,8 @@ void Solver::ensure_amg() {
     }
   }
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
+  const char* tl_env = std::getenv("CFD_AMG_TAIL_LDS");
+  tail_lds = !(tl_env && tl_env[0] == '0');
   const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
   const uint32_t tail_rows = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 4096u;
   const int lo = std::max(amg_g, 1);
@@ -759,7 +761,10 @@ void Solver::v_cycle() {
     }
   }
   if (tf < L) {
-    launch_amg_tail(d_tail, tf, L, stream);
+    size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL_LDS=0 disables)
+    for (int l = tf; l < L; ++l) lds += 4 * (((size_t)levels[l].dev.n + 3) & ~(size_t)3) * sizeof(float);
+    if (lds > kTailLdsMax || !tail_lds) lds = 0;
+    launch_amg_tail(d_tail, tf, L, lds, stream);
   } else {
     for (int s = 0; s < 10; ++s) sm(L - 1, s == 0 && L > 1);
   }

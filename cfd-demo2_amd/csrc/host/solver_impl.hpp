@@ -230,6 +230,7 @@ struct Solver {
   // AMG
   bool amg_built = false;
   int tail_first = 1;              // first AMG level handled by k_amg_tail
+  bool tail_lds = true;            // LDS-resident tail kernel when it fits
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   std::vector<AmgGpuLevel> levels;
   // host-side state
