@@ -79,7 +79,7 @@ class GpuSolver:
     def __init__(self, mesh, config: _ffi.Config | None = None, device: int = 0, _handle=None,
                   **cfg_overrides):
         L = _bind()
-        self._mesh = mesh
+        # the library copies what it needs at creation: no reference to the mesh is kept
         cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
         self._cfg = cfg
         if _handle is None:
