@@ -293,3 +293,71 @@ def _scalar_csr_fast(mesh):
     srow = np.zeros(n + 1, dtype=np.int64)
     np.add.at(srow, rr + 1, 1)
     return np.cumsum(srow), cc
+
+
+def test_reproduce_divergence_gpu():
+    """tests/reproduce_divergence.rs: BackwardsStep h=0.025, water, alpha 0.7/0.3,
+    adaptive dt (CFL 0.2, growth <= 1.2, dt <= 0.1), 50 steps: outer residuals
+    finite and < 1e10.  The first 10 steps are also checked bit-exact vs the
+    oracle (same host-side dt sequence)."""
+    from tests.meshes import STEP
+    from cfd2_amd.mesh import generate_cut_cell_mesh
+    mesh = generate_cut_cell_mesh(STEP, 0.025, 0.025, 1.2, (3.5, 1.0))
+    mesh.smooth(STEP, 0.3, 50)
+    min_cell = float(np.sqrt(mesh.arrays()["cell_vol"]).min())
+    g, o = _pair(mesh)
+    sols = [g, o]
+    dts = {}
+    for s in sols:
+        s.set_density(1000.0)
+        s.set_viscosity(0.001)
+        s.set_scheme(0)
+        s.set_alpha_u(0.7)
+        s.set_alpha_p(0.3)
+        n = mesh.num_cells()
+        s.set_u(np.zeros((n, 2)))
+        s.set_p(np.zeros(n))
+        s.set_dt(0.001)
+        dts[id(s)] = np.float32(0.001)
+    for step in range(50):
+        active = sols if step < 10 else [g]
+        for s in active:
+            s.step()
+            assert not (s.should_stop and s.degenerate_count > 10)
+            i = s.step_info()
+            for r in (i.outer_residual_u, i.outer_residual_p):
+                assert np.isfinite(r) and r <= 1e10, (step, r)
+            u = s.get_u()
+            vmax = float(np.sqrt((u ** 2).sum(1)).max())
+            if vmax > 1e-6:
+                dt = float(dts[id(s)])
+                new_dt = dt * 0.2 / (vmax * dt / min_cell)
+                new_dt = min(new_dt, dt * 1.2, 0.1)
+                s.set_dt(new_dt)
+                dts[id(s)] = np.float32(new_dt)
+        if step < 10:
+            _assert_same_fields(g, o, f"reproduce_divergence step {step}")
+
+
+def test_fine_mesh_obstacle_gpu():
+    """tests/gpu_fine_mesh_obstacle.rs (#[ignore] in the reference: beyond its
+    dispatch limit): ChannelWithObstacle r=0.2, h=0.001 (~2.87 M cells), dt 1e-4,
+    nu 1e-3, u = (1, 0) for cx < 0.01, Jacobi preconditioner, natural
+    convergence, 10 steps: no NaN, no degenerate stop."""
+    mesh = channel_obstacle(h=0.001, smooth_iters=50)
+    n = mesh.num_cells()
+    assert 2.7e6 < n < 3.0e6
+    g = GpuSolver(mesh)
+    g.set_dt(1e-4)
+    g.set_density(1.0)
+    g.set_viscosity(0.001)
+    u = np.zeros((n, 2))
+    u[mesh.arrays()["cell_cx"] < 0.01, 0] = 1.0
+    g.set_u(u)
+    for _ in range(10):
+        g.step()
+        if g.should_stop:
+            assert g.degenerate_count <= 10
+            break
+        uu = g.get_u()
+        assert np.all(np.isfinite(uu))
