@@ -240,7 +240,7 @@ def main():
         "step_algorithmic_gbs": step_bytes / (ms_per_step / 1e3) / 1e9,
         "linear_iterations_last_step": int(info.total_linear_iterations),
     }
-    if rank == 0 and world == 1 and mesh is not None and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and mesh is not None and args.outer > 0 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(mesh, n_cells, args.outer, args.inner)
         except Exception as e:  # the baseline is reported, never the target
