@@ -1086,15 +1086,21 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
 __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
                                                          float* __restrict__ cb,
                                                          float* __restrict__ cx, uint32_t stride_c,
-                                                         uint32_t glo, uint32_t ghi) {
+                                                         uint32_t glo, uint32_t ghi,
+                                                         float* __restrict__ sm_out,
+                                                         const float* __restrict__ sm_de) {
   const uint32_t I = row_id();
   if (I < L.nc) {
     float sum = 0.0f;
     for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
     cb[I] = sum;
-    cx[I] = 0.0f;
+    if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
+      sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
+    else
+      cx[I] = 0.0f;
     return;
   }
+  if (sm_out) return;
   const uint32_t g = I - L.nc;
   if (g < glo)
     cx[-1 - (int)g] = 0.0f;
@@ -1533,9 +1539,11 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
     hipLaunchKernelGGL(k_amg_residual<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
-                         uint32_t glo, uint32_t ghi, hipStream_t s) {
-  const size_t n = (size_t)L.nc + glo + ghi;
-  if (n) hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi);
+                         uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de) {
+  const size_t n = (size_t)L.nc + (sm_out ? 0 : (size_t)glo + ghi);
+  if (n)
+    hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
+                       sm_out, sm_de);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, x, xc);

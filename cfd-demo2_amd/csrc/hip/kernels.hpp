@@ -216,8 +216,11 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
                          hipStream_t s);
 // coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused); on a
 // distributed coarse level also clears its ghosts: [-glo, 0) and [stride_c, stride_c + ghi)
+// sm_out != null: instead of clearing coarse_x, write the coarse level's
+// zero-x pre-smoother result (mix(0, (b - 0)/de, 0.8), de = sm_de) to sm_out.
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
-                         uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s);
+                         uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s,
+                         float* sm_out = nullptr, const float* sm_de = nullptr);
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).

@@ -637,6 +637,8 @@ void Solver::ensure_amg() {
     }
   }
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
+  const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
+  fuse_presmooth = !(fz_env && fz_env[0] == '0');
   const char* tl_env = std::getenv("CFD_AMG_TAIL_LDS");
   tail_lds = !(tl_env && tl_env[0] == '0');
   const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
@@ -743,15 +745,22 @@ void Solver::v_cycle() {
     else
       f(0, Lv.dev.n);
   };
+  bool presmoothed = false;  // level i's zero-x pre-smoother already ran inside the restriction
   for (int i = 0; i < down; ++i) {
     AmgGpuLevel& Lv = levels[i];
-    sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
+    if (presmoothed)
+      std::swap(Lv.x, Lv.xt);
+    else
+      sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
     res(i);
     AmgGpuLevel& C = levels[i + 1];
+    // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
+    presmoothed = fuse_presmooth && (i + 1 < down) && (!Lv.dist || C.dist);
+    float* smo = presmoothed ? C.xt : nullptr;
     if (!Lv.dist) {
-      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream);
+      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream, smo, C.dev.de);
     } else if (C.dist) {
-      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, C.npad, C.glo, C.ghi, stream);
+      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, C.npad, C.glo, C.ghi, stream, smo, C.dev.de);
     } else {  // into the first replicated level: own slice, clear all, all-gather
       launch_amg_restrict(Lv.dev, Lv.r, C.b + C.C0, C.x + C.C0, Lv.dev.nc, (uint32_t)C.C0,
                           (uint32_t)(C.nglob - C.C1), stream);

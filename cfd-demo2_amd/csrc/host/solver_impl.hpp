@@ -231,6 +231,7 @@ struct Solver {
   bool amg_built = false;
   int tail_first = 1;              // first AMG level handled by k_amg_tail
   bool tail_lds = true;            // LDS-resident tail kernel when it fits
+  bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   std::vector<AmgGpuLevel> levels;
   // host-side state
