@@ -10,7 +10,13 @@
 // The hierarchy is built once (first AMG solve) and frozen.
 // P and R hold only 1.0 values, so they are stored as index arrays.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "solver_impl.hpp"
 
@@ -18,40 +24,63 @@ namespace cfd2 {
 
 namespace {
 
-// C = A * B for general CSR, per-row dense accumulator visited in the same
-// order as the reference's HashMap accumulation, then columns sorted.
+// C = A * B for general CSR.  Per row, products are accumulated per output
+// column in visit order (the reference's HashMap accumulation: first touch
+// starts at 0, then += a*b), then the row's columns are sorted.  Rows are
+// independent, so they are built in parallel (OpenMP, contiguous row chunks
+// concatenated in order) with a small per-row accumulator instead of a dense
+// one: identical arithmetic, O(nnz) memory.
 HostCsr spgemm(const HostCsr& a, const HostCsr& b) {
   HostCsr c;
   c.rows = a.rows;
   c.cols = b.cols;
   c.row.assign(a.rows + 1, 0);
-  std::vector<float> acc(b.cols, 0.0f);
-  std::vector<uint8_t> seen(b.cols, 0);
-  std::vector<uint32_t> touched;
-  for (size_t i = 0; i < a.rows; ++i) {
-    c.row[i] = (uint32_t)c.col.size();
-    touched.clear();
+  // visit-order accumulation of row i into acc (first touch = 0, then += a*b)
+  auto row_product = [&](size_t i, std::vector<std::pair<uint32_t, float>>& acc) {
+    acc.clear();
     for (uint32_t ka = a.row[i]; ka < a.row[i + 1]; ++ka) {
       const uint32_t j = a.col[ka];
       const float va = a.val[ka];
       for (uint32_t kb = b.row[j]; kb < b.row[j + 1]; ++kb) {
         const uint32_t k = b.col[kb];
-        if (!seen[k]) {
-          seen[k] = 1;
-          acc[k] = 0.0f;
-          touched.push_back(k);
-        }
-        acc[k] += va * b.val[kb];
+        size_t q = 0;
+        while (q < acc.size() && acc[q].first != k) ++q;
+        if (q == acc.size()) acc.push_back({k, 0.0f});
+        acc[q].second += va * b.val[kb];
       }
     }
-    std::sort(touched.begin(), touched.end());
-    for (uint32_t k : touched) {
-      c.col.push_back(k);
-      c.val.push_back(acc[k]);
-      seen[k] = 0;
+  };
+  // pass 1: row lengths (parallel, no allocation), pass 2: fill in place
+#pragma omp parallel
+  {
+    std::vector<std::pair<uint32_t, float>> acc;
+#pragma omp for schedule(static)
+    for (long i = 0; i < (long)a.rows; ++i) {
+      row_product(i, acc);
+      c.row[i + 1] = (uint32_t)acc.size();
     }
   }
-  c.row[a.rows] = (uint32_t)c.col.size();
+  for (size_t i = 0; i < a.rows; ++i) c.row[i + 1] += c.row[i];
+  c.col.resize(c.row[a.rows]);
+  c.val.resize(c.row[a.rows]);
+#pragma omp parallel
+  {
+    std::vector<std::pair<uint32_t, float>> acc;
+#pragma omp for schedule(static)
+    for (long i = 0; i < (long)a.rows; ++i) {
+      row_product(i, acc);
+      std::sort(acc.begin(), acc.end(),
+                [](const std::pair<uint32_t, float>& x, const std::pair<uint32_t, float>& y) {
+                  return x.first < y.first;
+                });
+      uint32_t o = c.row[i];
+      for (const auto& e : acc) {
+        c.col[o] = e.first;
+        c.val[o] = e.second;
+        ++o;
+      }
+    }
+  }
   return c;
 }
 
@@ -73,21 +102,35 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
       const uint32_t NONE = std::numeric_limits<uint32_t>::max();
       std::vector<uint32_t> agg(n, NONE);
       std::vector<uint64_t> cpart(part.size(), 0);
-      uint32_t nagg = 0;
-      for (size_t p = 0; p + 1 < part.size(); ++p) {
-        cpart[p] = nagg;
+      const size_t nparts = part.size() - 1;
+      std::vector<uint32_t> pcount(nparts, 0);
+      // greedy index-order aggregation, part by part: parts are independent
+      // (neighbours outside the part never join), so they run in parallel with
+      // local numbering, then are offset by the aggregates of earlier parts
+#pragma omp parallel for schedule(dynamic, 1)
+      for (long p = 0; p < (long)nparts; ++p) {
         const uint64_t lo = part[p], hi = part[p + 1];
+        uint32_t na = 0;
         for (size_t i = lo; i < hi; ++i) {
           if (agg[i] != NONE) continue;
-          agg[i] = nagg;
+          agg[i] = na;
           for (uint32_t k = cur.row[i]; k < cur.row[i + 1]; ++k) {
             const uint32_t j = cur.col[k];
-            if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = nagg;
+            if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = na;
           }
-          ++nagg;
+          ++na;
         }
+        pcount[p] = na;
+      }
+      uint32_t nagg = 0;
+      for (size_t p = 0; p < nparts; ++p) {
+        cpart[p] = nagg;
+        nagg += pcount[p];
       }
       cpart.back() = nagg;
+#pragma omp parallel for schedule(dynamic, 1)
+      for (long p = 0; p < (long)nparts; ++p)
+        for (size_t i = part[p]; i < part[p + 1]; ++i) agg[i] += (uint32_t)cpart[p];
       if (nagg < n) {
         // P (n x nagg) and R = P^T as CSR with unit values
         HostCsr P, R;
@@ -112,7 +155,14 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
           std::vector<uint32_t> pos(R.row.begin(), R.row.end() - 1);
           for (size_t i = 0; i < n; ++i) R.col[pos[agg[i]]++] = (uint32_t)i;  // ascending i
         }
-        HostCsr next = spgemm(spgemm(R, cur), P);
+        const auto t0 = std::chrono::steady_clock::now();
+        HostCsr RA = spgemm(R, cur);
+        const auto t1 = std::chrono::steady_clock::now();
+        HostCsr next = spgemm(RA, P);
+        const auto t2 = std::chrono::steady_clock::now();
+        if (std::getenv("CFD_AMG_SETUP_TIMING"))
+          std::fprintf(stderr, "[amg setup] level %zu: n=%zu nagg=%u  R*A %.3fs  (RA)*P %.3fs\n", li, n, nagg,
+                       std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
         L.agg = std::move(agg);
         L.r_row = R.row;
         L.r_col = R.col;
