@@ -7,6 +7,7 @@
 // each kernel) and is compiled with -ffp-contract=off, so results are
 // bit-identical to the CPU oracle; reductions follow the canonical order of
 // kernels.hpp (256 threads x 4 cells per chunk, halving tree).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -1519,9 +1520,17 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
                      hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
-void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s) {
+void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
+                       hipEvent_t ev0, hipEvent_t ev1) {
   if (L.r1 <= L.r0) return;
   const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
+  if (ev0) {  // timed launch: events recorded by the GPU at kernel start / end
+    if (L.use16)
+      hipExtLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
+    else
+      hipExtLaunchKernelGGL(k_amg_smooth<false>, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
+    return;
+  }
   if (L.use16)
     hipLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
   else

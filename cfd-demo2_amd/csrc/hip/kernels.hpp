@@ -208,8 +208,9 @@ void launch_solve_triangular(const float* H, const float* g, float* y, int k, in
                              hipStream_t s);
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
                      hipStream_t s);
+// ev0/ev1 (optional): timing events recorded by the GPU at kernel start / end
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
-                       hipStream_t s);
+                       hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // pre-smoother of a level whose x is identically +0 (bit-identical to launch_amg_smooth then)
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,

@@ -661,7 +661,10 @@ void Solver::ensure_amg() {
 
 // HIP events around level-0 smoother launches (bench roofline); the pool is
 // drained into prof_ms when full.
-void Solver::prof_begin() {
+// Timing of level-0 smoother launches (bench roofline): a pair of pool events
+// per launch, recorded by the GPU at kernel start / end (hipExtLaunchKernel);
+// the pool is drained into prof_ms when full.
+std::pair<hipEvent_t, hipEvent_t> Solver::prof_pair() {
   if (prof_used + 2 > prof_ev.size()) {
     CFD_HIP(hipStreamSynchronize(stream));
     for (size_t k = 0; k + 1 < prof_used; k += 2) {
@@ -676,25 +679,20 @@ void Solver::prof_begin() {
       prof_ev.push_back(e);
     }
   }
-  CFD_HIP(hipEventRecord(prof_ev[prof_used], stream));
-}
-
-void Solver::prof_end() {
-  CFD_HIP(hipEventRecord(prof_ev[prof_used + 1], stream));
   prof_used += 2;
+  return {prof_ev[prof_used - 2], prof_ev[prof_used - 1]};
 }
 
 void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {
   AmgGpuLevel& L = levels[li];
-  const bool timed = prof && li == 0;
-  if (timed) prof_begin();
-  if (x_zero)
+  if (x_zero) {
     launch_amg_smooth_zero(L.dev, b, L.xt, stream);
-  else
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
-  if (timed) {
-    prof_end();
+  } else if (prof && li == 0) {
+    const auto ev = prof_pair();
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second);
     prof_launches++;
+  } else {
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
   }
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
@@ -725,9 +723,12 @@ void Solver::v_cycle() {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;
       d.r1 = b;
-      if (timed) prof_begin();
-      launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream);
-      if (timed) prof_end();
+      if (timed) {
+        const auto ev = prof_pair();
+        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second);
+      } else {
+        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream);
+      }
     });
     if (timed) prof_launches++;
     std::swap(Lv.x, Lv.xt);

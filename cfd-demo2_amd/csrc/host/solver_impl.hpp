@@ -274,8 +274,7 @@ struct Solver {
   void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);
-  void prof_begin();
-  void prof_end();
+  std::pair<hipEvent_t, hipEvent_t> prof_pair();
   float norm_blocking(const float* v, int mode, int slot);
   float residual_into_v0_blocking();
   void check_evolution();
