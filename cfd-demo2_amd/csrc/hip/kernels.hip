@@ -1282,10 +1282,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
   for (uint32_t i = t; i < T.L.n; i += nt) T.x[i] = X0[i];
 }
 
-__global__ void __launch_bounds__(kBlock) k_fill(float* x, float v, size_t n) {
-  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e < n) x[e] = v;
-}
 
 // ---------------------- check_evolution statistics --------------------------
 // AoS view of the reference FluidState (coupled_solver.rs:504 reads the 32-byte
@@ -1569,9 +1565,6 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
     attr = true;
   }
   hipLaunchKernelGGL(k_amg_tail_lds, dim3(1), dim3(1024), lds_bytes, s, tail, first, nlev);
-}
-void launch_fill(float* x, float v, size_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);
 }
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
                               uint64_t gbase, uint64_t rec0, double* partial, hipStream_t s) {

@@ -229,7 +229,6 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, 
 constexpr size_t kTailLdsMax = 160 * 1024 - 1024;
 void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
-void launch_fill(float* x, float v, size_t n, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
 // partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
 // The variance part reads record ((gbase + c) >> 2) - rec0 of `var` (stride bug, §0.1-12).
