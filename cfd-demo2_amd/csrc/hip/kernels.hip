@@ -586,6 +586,25 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   store12(y + 3 * (size_t)i0, o);
 }
 
+#ifndef CFD_CGS_NT
+#define CFD_CGS_NT 1
+#endif
+// streamed-once basis reads / new basis vector stores (nontemporal when CFD_CGS_NT)
+__device__ __forceinline__ float ld_stream(const float* p) {
+#if CFD_CGS_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(float* p, float v) {
+#if CFD_CGS_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j,
 // V_ii = binv[ii] * W_ii
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
@@ -613,7 +632,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
       if (ok[q]) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const float vv = sc * v[3 * c + s];
+          const float vv = sc * ld_stream(v + 3 * c + s);
           acc += wv[q][s] * vv;
         }
       }
@@ -663,7 +682,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
       if (c < N) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          const float vv = sc * v[3 * c + s];
+          const float vv = sc * ld_stream(v + 3 * c + s);
           corr[q][s] += h * vv;
         }
       }
@@ -678,7 +697,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
         const float wn = w[3 * c + s] - corr[q][s];
-        out[3 * c + s] = wn;
+        st_stream(out + 3 * c + s, wn);
         acc += wn * wn;
       }
     }
