@@ -505,6 +505,28 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
   *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
 }
 
+// Gathers of the 4-cells-per-thread kernels.  Unused ELL slots and padding
+// rows hold the row's own (valid) index, so a gather can be issued
+// unconditionally (ALWAYS): no branch per load, and the three loads of one
+// cell's (u, v, p) merge into one dwordx3; the value of an unused slot is
+// never consumed (every accumulation skips r >= len), so results are
+// unchanged.  Same-box A/B (tools/gpu_ab_prof.sh, C2): a win for k_spmv
+// (253 -> 246 us) and k_amg_smooth (84 -> 81 us), a loss for the Schur
+// kernels and k_amg_residual (whose extra diagonal pass would load a whole
+// unused slot group), so those keep the predicated form.
+#ifndef CFD_GATHER_ALWAYS
+#define CFD_GATHER_ALWAYS 1
+#endif
+template <bool ALWAYS = false>
+__device__ __forceinline__ float gat(bool on, const float* p) {
+  if constexpr (ALWAYS && CFD_GATHER_ALWAYS) {
+    (void)on;
+    return *p;
+  } else {
+    return on ? *p : 0.0f;
+  }
+}
+
 // Slot-group sizes of the 4-cells-per-thread kernels (all loads of a group are
 // issued before the first use).  Build-time tunables (tools/ab_variants.py).
 #ifndef CFD_SPMV_U
@@ -517,12 +539,71 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
 #define CFD_CORRECT_U 4
 #endif
 
+// Slot loads of the row kernels are unconditional: slot r reads ELL slot
+// min(r, ws - 1) (ws = the matrix's ELL width, kernel-uniform), which always
+// exists; unused slots hold value 0 and the row's own column, and every
+// accumulation skips r >= len, so results are unchanged.  Without a branch
+// per slot the compiler issues a whole group's matrix loads back to back
+// (a predicated load per slot made it wait for each slot's column load
+// before issuing the next slot), and the first group does not wait for the
+// row lengths.  The first group is sized to cover a whole interior row
+// (5 entries of a quad cell's coupled row).
+#ifndef CFD_SPMV_U1
+#define CFD_SPMV_U1 5
+#endif
+
 // spmv (gmres_ops.wgsl:63-81) on compressed blocks, 4 cells (12 rows) per
 // thread; per-row term order identical to the CSR row (neighbour-major, u,v,p).
+template <bool D16, int U>
+__device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
+                                           uint32_t r0, uint32_t rmax, const uchar4 ln, const uchar4 dr,
+                                           const float2 d2[4], float su[4], float sv[4], float sp[4]) {
+  float2 a[U][4], g[U][4];
+  int c[U][4];
+  float xg[U][4][3];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
+    load2x4(A.cval_a + off, a[u]);
+    load2x4(A.cval_g + off, g[u]);
+    ccols4<D16>(A, off, i0, c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool on = r0 + u < u4(ln, k);
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+      xg[u][k][0] = gat<true>(on, x + j);
+      xg[u][k][1] = gat<true>(on, x + j + 1);
+      xg[u][k][2] = gat<true>(on, x + j + 2);
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t r = r0 + u;
+      if (r >= u4(ln, k)) continue;
+      const bool dg = (r == u4(dr, k));
+      const float uu = a[u][k].x, pp = a[u][k].y, up = g[u][k].x, vp = g[u][k].y;
+      const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
+      const float xu = xg[u][k][0], xv = xg[u][k][1], xp = xg[u][k][2];
+      su[k] += uu * xu;
+      su[k] += 0.0f * xv;
+      su[k] += up * xp;
+      sv[k] += 0.0f * xu;
+      sv[k] += uu * xv;
+      sv[k] += vp * xp;
+      sp[k] += pu * xu;
+      sp[k] += pv * xv;
+      sp[k] += pp * xp;
+    }
+}
+
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
-  constexpr int U = CFD_SPMV_U;
+  constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   const uint32_t i0 = A.r0 + 4 * row_id();
   if (i0 >= A.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
@@ -531,57 +612,8 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   load2x4(A.cdiag2 + i0, d2);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float su[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
-    float2 a[U][4], g[U][4];
-    int c[U][4];
-    float xg[U][4][3];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t r = r0 + u;
-      if (U == 1 || r < maxlen) {
-        const size_t off = (size_t)r * A.ld + i0;
-        load2x4(A.cval_a + off, a[u]);
-        load2x4(A.cval_g + off, g[u]);
-        ccols4<D16>(A, off, i0, c[u]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          a[u][k] = g[u][k] = make_float2(0.0f, 0.0f);
-          c[u][k] = (int)i0 + k;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool on = r0 + u < u4(ln, k);
-        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-        xg[u][k][0] = on ? x[j] : 0.0f;
-        xg[u][k][1] = on ? x[j + 1] : 0.0f;
-        xg[u][k][2] = on ? x[j + 2] : 0.0f;
-      }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t r = r0 + u;
-        if (r >= u4(ln, k)) continue;
-        const bool dg = (r == u4(dr, k));
-        const float uu = a[u][k].x, pp = a[u][k].y, up = g[u][k].x, vp = g[u][k].y;
-        const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
-        const float xu = xg[u][k][0], xv = xg[u][k][1], xp = xg[u][k][2];
-        su[k] += uu * xu;
-        su[k] += 0.0f * xv;
-        su[k] += up * xp;
-        sv[k] += 0.0f * xu;
-        sv[k] += uu * xv;
-        sv[k] += vp * xp;
-        sp[k] += pu * xu;
-        sp[k] += pv * xv;
-        sp[k] += pp * xp;
-      }
-  }
+  spmv_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, su, sv, sp);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv_group<D16, U>(A, x, i0, r0, maxlen - 1u, ln, dr, d2, su, sv, sp);
   const float o[12] = {su[0], sv[0], sp[0], su[1], sv[1], sp[1], su[2], sv[2], sp[2], su[3], sv[3], sp[3]};
   store12(y + 3 * (size_t)i0, o);
 }
@@ -748,6 +780,52 @@ __global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict_
 // iterate.  The term `A_pp * 0.0` of the reference loop is dropped: it can
 // only flip the sign of a zero rhs_p, and its A_pp read is the largest byte
 // cost of the row.
+#ifndef CFD_SCHUR_GATHER_ALWAYS
+#define CFD_SCHUR_GATHER_ALWAYS 1
+#endif
+#ifndef CFD_PREDICT_U1
+#define CFD_PREDICT_U1 5
+#endif
+template <bool D16, int U>
+__device__ __forceinline__ void predict_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
+                                              const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
+                                              uint32_t rmax, const uchar4 ln, const uchar4 dr, const float2 d2[4],
+                                              float rhs[4]) {
+  float2 g[U][4];
+  int c[U][4];
+  float gd[U][4], gu[U][4], gv[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
+    load2x4(A.cval_g + off, g[u]);
+    ccols4<D16>(A, off, i0, c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool on = r0 + u < u4(ln, k);
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+      gd[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, dinv_uv + c[u][k]);
+      gu[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j);
+      gv[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j + 1);
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t r = r0 + u;
+      if (r >= u4(ln, k)) continue;
+      const bool dg = (r == u4(dr, k));
+      const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
+      const float ru = sc * gu[u][k], rv = sc * gv[u][k];
+      const float zu = ru * gd[u][k];
+      const float zv = rv * gd[u][k];
+      rhs[k] -= pu * zu;
+      rhs[k] -= pv * zv;
+    }
+}
+
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             const float* __restrict__ w_in,
@@ -756,7 +834,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             const float* __restrict__ dinv_p,
                                                             float* temp_p, float* p_sol,
                                                             float* p_prev) {
-  constexpr int U = CFD_PREDICT_U;
+  constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
   const uint32_t i0 = A.r0 + 4 * row_id();
   if (i0 >= A.r1) return;
   const float sc = binv[jv];
@@ -770,50 +848,9 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
   float2 d2[4];
   load2x4(A.cdiag2 + i0, d2);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
-  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
-    float2 g[U][4];
-    int c[U][4];
-    float gd[U][4], gu[U][4], gv[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t r = r0 + u;
-      if (U == 1 || r < maxlen) {
-        const size_t off = (size_t)r * A.ld + i0;
-        load2x4(A.cval_g + off, g[u]);
-        ccols4<D16>(A, off, i0, c[u]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          g[u][k] = make_float2(0.0f, 0.0f);
-          c[u][k] = (int)i0 + k;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool on = r0 + u < u4(ln, k);
-        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-        gd[u][k] = on ? dinv_uv[c[u][k]] : 0.0f;
-        gu[u][k] = on ? w_in[j] : 0.0f;
-        gv[u][k] = on ? w_in[j + 1] : 0.0f;
-      }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t r = r0 + u;
-        if (r >= u4(ln, k)) continue;
-        const bool dg = (r == u4(dr, k));
-        const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
-        const float ru = sc * gu[u][k], rv = sc * gv[u][k];
-        const float zu = ru * gd[u][k];
-        const float zv = rv * gd[u][k];
-        rhs[k] -= pu * zu;
-        rhs[k] -= pv * zv;
-      }
-  }
+  predict_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, rhs);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
+    predict_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, ln, dr, d2, rhs);
   const float4 dp = *reinterpret_cast<const float4*>(dinv_p + i0);
   *reinterpret_cast<float4*>(temp_p + i0) = make_float4(rhs[0], rhs[1], rhs[2], rhs[3]);
   *reinterpret_cast<float4*>(p_sol + i0) =
@@ -845,6 +882,36 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 // correct_velocity (schur_precond.wgsl:93-139) fused with the velocity
 // prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol);
 // 4 cells per thread.
+#ifndef CFD_CORRECT_U1
+#define CFD_CORRECT_U1 5
+#endif
+template <bool D16, int U>
+__device__ __forceinline__ void correct_group(const CoupledMatrix& A, const float* __restrict__ p_sol,
+                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln, float cu[4],
+                                              float cv[4]) {
+  float2 g[U][4];
+  int c[U][4];
+  float pj[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
+    load2x4(A.cval_g + off, g[u]);
+    ccols4<D16>(A, off, i0, c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(r0 + u < u4(ln, k), p_sol + c[u][k]);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (r0 + u >= u4(ln, k)) continue;
+      cu[k] += g[u][k].x * pj[u][k];
+      cv[k] += g[u][k].y * pj[u][k];
+    }
+}
+
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
                                                             const float* __restrict__ w_in,
@@ -852,44 +919,14 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
                                                             const float* __restrict__ p_sol,
                                                             const float* __restrict__ dinv_uv,
                                                             float* __restrict__ z) {
+  constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
   const uint32_t i0 = A.r0 + 4 * row_id();
   if (i0 >= A.r1) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  constexpr int U = CFD_CORRECT_U;
-  for (uint32_t r0 = 0; r0 < maxlen; r0 += U) {
-    float2 g[U][4];
-    int c[U][4];
-    float pj[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t r = r0 + u;
-      if (r < maxlen) {
-        const size_t off = (size_t)r * A.ld + i0;
-        load2x4(A.cval_g + off, g[u]);
-        ccols4<D16>(A, off, i0, c[u]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          g[u][k] = make_float2(0.0f, 0.0f);
-          c[u][k] = (int)i0 + k;
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pj[u][k] = (r0 + u < u4(ln, k)) ? p_sol[c[u][k]] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (r0 + u >= u4(ln, k)) continue;
-        cu[k] += g[u][k].x * pj[u][k];
-        cv[k] += g[u][k].y * pj[u][k];
-      }
-  }
+  correct_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, ln, cu, cv);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, ln, cu, cv);
   const float sc = binv[jv];
   float wo[12], o[12];
   load12(w_in + 3 * (size_t)i0, wo);
@@ -991,16 +1028,20 @@ __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uin
 #endif
 constexpr int kU = CFD_AMG_U;
 
-template <bool D16>
+// FULL levels (rows nearly as long as the ELL width, e.g. level 0 of a quad
+// mesh): slot loads unconditional, clamped to rmax, and the first group
+// peeled so its loads do not wait for the row lengths.  Other levels predicate
+// each slot load on the thread's longest row, which avoids reading the padding
+// of short rows.
+template <bool D16, bool FULL, bool ALWAYS = false>
 __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
-                                             uint32_t i0, uint32_t r0, uint32_t maxlen, const uchar4 ln,
+                                             uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln,
                                              float4 v[kU], float xg[kU][4]) {
   int c[kU][4];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
-    const uint32_t r = r0 + u;
-    if (r < maxlen) {
-      const size_t off = (size_t)r * L.stride + i0;
+    if (FULL || r0 + u <= rmax) {
+      const size_t off = (size_t)min(r0 + u, rmax) * L.stride + i0;
       v[u] = *reinterpret_cast<const float4*>(L.val + off);
       load_cols4<D16>(L, off, i0, c[u]);
     } else {
@@ -1012,11 +1053,11 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 #pragma unroll
   for (int u = 0; u < kU; ++u)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) xg[u][k] = (r0 + u < u4(ln, k)) ? x[c[u][k]] : 0.0f;
+    for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && FULL>(r0 + u < u4(ln, k), x + c[u][k]);
 }
 
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
-template <bool D16>
+template <bool D16, bool FULL>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
@@ -1025,15 +1066,22 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) {
+  auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16>(L, x, i0, r0, maxlen, ln, v, xg);
+    gather_group<D16, FULL, true>(L, x, i0, r0, rmax, ln, v, xg);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (r0 + u < u4(ln, k)) sg[k] += f4(v[u], k) * xg[u][k];
+  };
+  if constexpr (FULL) {
+    // first slot group peeled: its loads (clamped to the ELL width) do not wait for the lengths
+    step(0, (uint32_t)max(L.w, 1) - 1u);
+    for (uint32_t r0 = kU; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
+  } else {
+    for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
   }
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
@@ -1064,9 +1112,12 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
   *reinterpret_cast<float4*>(x_out + i0) = o;
 }
 
+#ifndef CFD_RESID_GATHER_ALWAYS
+#define CFD_RESID_GATHER_ALWAYS 1
+#endif
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
-template <bool D16>
+template <bool D16, bool FULL>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
@@ -1078,10 +1129,10 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
   const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (uint32_t r0 = 0; r0 <= maxlen; r0 += kU) {  // r = maxlen: a diagonal ranked last
+  auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16>(L, x, i0, r0, maxlen, ln, v, xg);
+    gather_group<D16, FULL, CFD_RESID_GATHER_ALWAYS>(L, x, i0, r0, rmax, ln, v, xg);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -1090,7 +1141,17 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
         if (r == u4(dr, k)) ax[k] += f4(dv, k) * f4(xx, k);
         if (r < u4(ln, k)) ax[k] += f4(v[u], k) * xg[u][k];
       }
+  };
+  uint32_t r0 = 0;
+  if constexpr (FULL) {
+    step(0, (uint32_t)max(L.w, 1) - 1u);  // peeled first group (see k_amg_smooth)
+    r0 = kU;
   }
+  for (; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
+  // a diagonal ranked after every visited slot (rank = len >= r0) comes last
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (u4(dr, k) >= r0) ax[k] += f4(dv, k) * f4(xx, k);
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
   float4 o;
   o.x = bb.x - ax[0];
@@ -1535,21 +1596,19 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
                      hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
+// instance for a level: 16/32-bit columns x FULL (see gather_group)
+#define CFD_AMG_INSTANCE(kern, L) \
+  ((L).use16 ? ((L).full ? kern<true, true> : kern<true, false>) : ((L).full ? kern<false, true> : kern<false, false>))
+
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
                        hipEvent_t ev0, hipEvent_t ev1) {
   if (L.r1 <= L.r0) return;
   const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
-  if (ev0) {  // timed launch: events recorded by the GPU at kernel start / end
-    if (L.use16)
-      hipExtLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
-    else
-      hipExtLaunchKernelGGL(k_amg_smooth<false>, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
-    return;
-  }
-  if (L.use16)
-    hipLaunchKernelGGL(k_amg_smooth<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
+  auto fn = CFD_AMG_INSTANCE(k_amg_smooth, L);
+  if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
+    hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
   else
-    hipLaunchKernelGGL(k_amg_smooth<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
+    hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
 }
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
@@ -1557,10 +1616,8 @@ void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, 
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
   if (L.r1 <= L.r0) return;
   const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
-  if (L.use16)
-    hipLaunchKernelGGL(k_amg_residual<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
-  else
-    hipLaunchKernelGGL(k_amg_residual<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
+  auto fn = CFD_AMG_INSTANCE(k_amg_residual, L);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
                          uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de) {

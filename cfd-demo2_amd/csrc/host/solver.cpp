@@ -611,6 +611,14 @@ void Solver::ensure_amg() {
         G.b = zeroed(G.npad);
       }
     }
+    // unconditional slot loads (kernels.hip gather_group) on level 0 (the
+    // face stencil: rows fill the ELL width) and on latency-bound small levels;
+    // predicated loads on the big coarse levels, whose row lengths vary
+    // (same-box A/B at C2: level 1 smoother 58 vs 66 us, small-level residual 6 vs 8.5 us)
+    {
+      const char* fe = std::getenv("CFD_AMG_FULL");
+      G.dev.full = fe ? (fe[0] == '1') : (li == 0 || G.dev.n <= (1u << 19));
+    }
     // coarsening operators: P as an aggregate index per stored fine row, R = P^T
     if (HL.has_op) {
       const AmgHostLevel& HC = H[li + 1];
