@@ -54,6 +54,7 @@ def _bind():
     L.cfd_debug_buffer_len.restype = C.c_size_t
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
     L.cfd_debug_prepare_assemble.argtypes = [_vp, C.c_int32]
+    L.cfd_debug_amg_info.argtypes = [_vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
     u8p = C.POINTER(C.c_uint8)
     u32p = C.POINTER(C.c_uint32)
     L.cfd_dist_unique_id.argtypes = [u8p]
@@ -215,6 +216,16 @@ class GpuSolver:
         nnz = (C.c_uint64 * 20)()
         self._call("cfd_amg_levels", C.byref(nl), rows, nnz)
         return [(int(rows[i]), int(nnz[i])) for i in range(nl.value)]
+
+    def amg_setup_info(self):
+        """(setup path: 0 not built / 1 host / 2 device, [digest of every level image])."""
+        path = C.c_int32()
+        dig = []
+        for li in range(len(self.amg_levels())):
+            d = C.c_uint64()
+            self._call("cfd_debug_amg_info", li, C.byref(path), C.byref(d))
+            dig.append(int(d.value))
+        return int(path.value), dig
 
     def step_algorithmic_bytes(self) -> float:
         return float(_ffi.lib().cfd_step_algorithmic_bytes(self._h))

@@ -1,0 +1,34 @@
+// Device-side AMG setup (amg_setup.hip): Galerkin product and level packing.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace cfd2 {
+
+// A fine level as the setup kernels read it: ELL slot-major (level 0, the
+// assembled scalar matrix: entry k of row i at k*ld + i, columns int32) or
+// CSR (coarse levels: rowptr, columns u32 stored as int32 bits).  Columns are
+// sorted ascending within each row.
+struct SetupMatrix {
+  int ell;
+  uint32_t ld;               // ELL slot stride
+  const uint32_t* len;       // ELL row lengths
+  const uint32_t* rowptr;    // CSR
+  const int32_t* col;
+  const float* val;
+};
+
+// per-thread capacities of k_galerkin; overflow (flag bit 1: members, bit 2:
+// coarse columns) makes the host fall back to its own setup
+constexpr int kSetupMaxMembers = 64;
+constexpr int kSetupMaxCoarse = 128;
+
+// rowptr_c == nullptr: count pass (cnt[I] = coarse row length); else fill pass.
+void launch_galerkin(const SetupMatrix& A, const uint32_t* agg, const uint32_t* r_row, const uint32_t* r_col,
+                     uint32_t nc, uint32_t* cnt, const uint32_t* rowptr_c, uint32_t* col_c, float* val_c,
+                     uint32_t* overflow, hipStream_t s);
+// AmgLevelDev arrays (val, col16 | col32, len, drank, dv, de) of rows [0, n), stride st, ELL width w
+void launch_amg_pack(const SetupMatrix& A, uint32_t n, uint32_t st, int w, int use16, float* val, int16_t* col16,
+                     int32_t* col32, uint8_t* len, uint8_t* drank, float* dv, float* de, hipStream_t s);
+
+}  // namespace cfd2

@@ -86,6 +86,54 @@ HostCsr spgemm(const HostCsr& a, const HostCsr& b) {
 
 }  // namespace
 
+uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, const std::vector<uint64_t>& part,
+                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart) {
+  const uint32_t NONE = std::numeric_limits<uint32_t>::max();
+  agg.assign(n, NONE);
+  cpart.assign(part.size(), 0);
+  const size_t nparts = part.size() - 1;
+  std::vector<uint32_t> pcount(nparts, 0);
+  // greedy index-order aggregation, part by part: parts are independent
+  // (neighbours outside the part never join), so they run in parallel with
+  // local numbering, then are offset by the aggregates of earlier parts
+#pragma omp parallel for schedule(dynamic, 1)
+  for (long p = 0; p < (long)nparts; ++p) {
+    const uint64_t lo = part[p], hi = part[p + 1];
+    uint32_t na = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      if (agg[i] != NONE) continue;
+      agg[i] = na;
+      for (uint32_t k = row[i]; k < row[i + 1]; ++k) {
+        const uint32_t j = col[k];
+        if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = na;
+      }
+      ++na;
+    }
+    pcount[p] = na;
+  }
+  uint32_t nagg = 0;
+  for (size_t p = 0; p < nparts; ++p) {
+    cpart[p] = nagg;
+    nagg += pcount[p];
+  }
+  cpart.back() = nagg;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (long p = 0; p < (long)nparts; ++p)
+    for (size_t i = part[p]; i < part[p + 1]; ++i) agg[i] += (uint32_t)cpart[p];
+  return nagg;
+}
+
+void transpose_aggregates(const std::vector<uint32_t>& agg, uint32_t nagg, std::vector<uint32_t>& r_row,
+                          std::vector<uint32_t>& r_col) {
+  const size_t n = agg.size();
+  r_row.assign(nagg + 1, 0);
+  for (size_t i = 0; i < n; ++i) r_row[agg[i] + 1]++;
+  for (uint32_t I = 0; I < nagg; ++I) r_row[I + 1] += r_row[I];
+  r_col.resize(n);
+  std::vector<uint32_t> pos(r_row.begin(), r_row.end() - 1);
+  for (size_t i = 0; i < n; ++i) r_col[pos[agg[i]]++] = (uint32_t)i;  // ascending i
+}
+
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
                                                const std::vector<uint64_t>& part0) {
   std::vector<AmgHostLevel> levels;
@@ -99,38 +147,9 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
     const size_t n = cur.rows;
     bool coarsened = false;
     if (li < max_levels - 1 && n > 100) {
-      const uint32_t NONE = std::numeric_limits<uint32_t>::max();
-      std::vector<uint32_t> agg(n, NONE);
-      std::vector<uint64_t> cpart(part.size(), 0);
-      const size_t nparts = part.size() - 1;
-      std::vector<uint32_t> pcount(nparts, 0);
-      // greedy index-order aggregation, part by part: parts are independent
-      // (neighbours outside the part never join), so they run in parallel with
-      // local numbering, then are offset by the aggregates of earlier parts
-#pragma omp parallel for schedule(dynamic, 1)
-      for (long p = 0; p < (long)nparts; ++p) {
-        const uint64_t lo = part[p], hi = part[p + 1];
-        uint32_t na = 0;
-        for (size_t i = lo; i < hi; ++i) {
-          if (agg[i] != NONE) continue;
-          agg[i] = na;
-          for (uint32_t k = cur.row[i]; k < cur.row[i + 1]; ++k) {
-            const uint32_t j = cur.col[k];
-            if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = na;
-          }
-          ++na;
-        }
-        pcount[p] = na;
-      }
-      uint32_t nagg = 0;
-      for (size_t p = 0; p < nparts; ++p) {
-        cpart[p] = nagg;
-        nagg += pcount[p];
-      }
-      cpart.back() = nagg;
-#pragma omp parallel for schedule(dynamic, 1)
-      for (long p = 0; p < (long)nparts; ++p)
-        for (size_t i = part[p]; i < part[p + 1]; ++i) agg[i] += (uint32_t)cpart[p];
+      std::vector<uint32_t> agg;
+      std::vector<uint64_t> cpart;
+      const uint32_t nagg = aggregate_greedy(n, cur.row.data(), cur.col.data(), part, agg, cpart);
       if (nagg < n) {
         // P (n x nagg) and R = P^T as CSR with unit values
         HostCsr P, R;
@@ -146,15 +165,8 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
         P.row[n] = (uint32_t)n;
         R.rows = nagg;
         R.cols = n;
-        R.row.assign(nagg + 1, 0);
-        for (size_t i = 0; i < n; ++i) R.row[agg[i] + 1]++;
-        for (uint32_t I = 0; I < nagg; ++I) R.row[I + 1] += R.row[I];
-        R.col.resize(n);
+        transpose_aggregates(agg, nagg, R.row, R.col);
         R.val.assign(n, 1.0f);
-        {
-          std::vector<uint32_t> pos(R.row.begin(), R.row.end() - 1);
-          for (size_t i = 0; i < n; ++i) R.col[pos[agg[i]]++] = (uint32_t)i;  // ascending i
-        }
         const auto t0 = std::chrono::steady_clock::now();
         HostCsr RA = spgemm(R, cur);
         const auto t1 = std::chrono::steady_clock::now();

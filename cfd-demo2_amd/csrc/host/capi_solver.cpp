@@ -211,6 +211,13 @@ cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* ro
   }
   return CFD_OK;
 }
+cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path, uint64_t* digest) {
+  CHECK_S(s);
+  return guard([&] {
+    if (setup_path) *setup_path = s->s->amg_setup_path;
+    if (digest) *digest = s->s->amg_level_digest(level);
+  });
+}
 double cfd_step_algorithmic_bytes(const cfd_solver* s) {
   return (s && s->s) ? s->s->algorithmic_step_bytes() : 0.0;
 }

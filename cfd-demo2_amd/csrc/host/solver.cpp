@@ -8,6 +8,7 @@
 // (blocking norms at solve start / restart, lagged residual reads), and none
 // under the fixed benchmark schedule except the two early-exit norms.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -508,8 +509,20 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 // aware hierarchy as every other rank, and keeps its rows of the levels with
 // more than CFD_AMG_REPLICATE_ROWS rows (default 262144); the small levels are
 // replicated on every rank.
-void Solver::ensure_amg() {
-  if (amg_built) return;
+// Unconditional slot loads (kernels.hip gather_group) on level 0 (the face
+// stencil: rows fill the ELL width) and on latency-bound small levels;
+// predicated loads on the big coarse levels, whose row lengths vary (same-box
+// A/B at C2: level 1 smoother 58 vs 66 us, small-level residual 6 vs 8.5 us).
+void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
+  const char* fe = std::getenv("CFD_AMG_FULL");
+  G.dev.full = fe ? (fe[0] == '1') : (li == 0 || G.dev.n <= (1u << 19));
+}
+
+// Host AMG setup (amg_setup.cpp): the assembled scalar matrix is downloaded,
+// the whole hierarchy is built on the host and every level image uploaded.
+// Distributed solvers always take this path (partition-aware hierarchy,
+// replicated coarse levels).
+void Solver::build_amg_host() {
   const size_t ld = topo.ld;
   std::vector<float> ell((size_t)topo.ws * ld);
   CFD_HIP(hipMemcpyAsync(ell.data(), sval, ell.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
@@ -611,14 +624,7 @@ void Solver::ensure_amg() {
         G.b = zeroed(G.npad);
       }
     }
-    // unconditional slot loads (kernels.hip gather_group) on level 0 (the
-    // face stencil: rows fill the ELL width) and on latency-bound small levels;
-    // predicated loads on the big coarse levels, whose row lengths vary
-    // (same-box A/B at C2: level 1 smoother 58 vs 66 us, small-level residual 6 vs 8.5 us)
-    {
-      const char* fe = std::getenv("CFD_AMG_FULL");
-      G.dev.full = fe ? (fe[0] == '1') : (li == 0 || G.dev.n <= (1u << 19));
-    }
+    set_amg_full_policy(G, li);
     // coarsening operators: P as an aggregate index per stored fine row, R = P^T
     if (HL.has_op) {
       const AmgHostLevel& HC = H[li + 1];
@@ -644,6 +650,23 @@ void Solver::ensure_amg() {
       G.dev.r_col = arena.upload(r_col, stream);
     }
   }
+}
+
+void Solver::ensure_amg() {
+  if (amg_built) return;
+  const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  const char* se = std::getenv("CFD_AMG_SETUP");
+  const bool device_setup = !dist() && !(se && std::string(se) == "host");
+  const char* how = "device";
+  amg_setup_path = 2;
+  if (!(device_setup && build_amg_device())) {
+    how = "host";
+    amg_setup_path = 1;
+    levels.clear();
+    build_amg_host();
+  }
+  const int L = (int)levels.size();
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
   fuse_presmooth = !(fz_env && fz_env[0] == '0');
@@ -665,6 +688,9 @@ void Solver::ensure_amg() {
   d_tail = arena.upload(tl, stream);
   sync();
   amg_built = true;
+  if (timing)
+    std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s\n", how, L,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
 }
 
 // HIP events around level-0 smoother launches (bench roofline); the pool is
@@ -1153,6 +1179,43 @@ void Solver::debug_prepare_assemble(bool asmb) {
   prepare();
   if (asmb) assemble();
   sync();
+}
+
+uint64_t Solver::amg_level_digest(int li) {
+  if (li < 0 || li >= (int)levels.size()) throw std::invalid_argument("no such AMG level");
+  CFD_HIP(hipSetDevice(device));
+  const AmgLevelDev& d = levels[li].dev;
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t bytes) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t k = 0; k < bytes; ++k) h = (h ^ b[k]) * 1099511628211ull;
+  };
+  auto dev = [&](const void* src, size_t bytes) {
+    if (!src || !bytes) return;
+    std::vector<unsigned char> tmp(bytes);
+    CFD_HIP(hipMemcpyAsync(tmp.data(), src, bytes, hipMemcpyDeviceToHost, stream));
+    sync();
+    mix(tmp.data(), bytes);
+  };
+  const uint32_t hdr[6] = {d.n, d.stride, (uint32_t)d.w, (uint32_t)d.use16, d.nc, (uint32_t)levels[li].nnz};
+  mix(hdr, sizeof(hdr));
+  const size_t slots = (size_t)std::max(d.w, 1) * d.stride;
+  dev(d.val, slots * 4);
+  dev(d.col16, d.use16 ? slots * 2 : 0);
+  dev(d.col32, d.use16 ? 0 : slots * 4);
+  dev(d.len, d.stride);
+  dev(d.drank, d.stride);
+  dev(d.dv, (size_t)d.stride * 4);
+  dev(d.de, (size_t)d.stride * 4);
+  if (d.nc) {
+    dev(d.agg, (size_t)d.stride * 4);
+    std::vector<uint32_t> rr((size_t)d.nc + 1);
+    CFD_HIP(hipMemcpyAsync(rr.data(), d.r_row, rr.size() * 4, hipMemcpyDeviceToHost, stream));
+    sync();
+    mix(rr.data(), rr.size() * 4);
+    dev(d.r_col, (size_t)rr[d.nc] * 4);
+  }
+  return h;
 }
 
 size_t Solver::debug_len(int id) const {

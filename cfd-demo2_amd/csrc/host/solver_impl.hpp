@@ -122,6 +122,14 @@ struct AmgHostLevel {
 };
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
                                                const std::vector<uint64_t>& part = {});
+// Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
+// n rows, part by part (aggregates never cross a part); returns the aggregate
+// count, agg[i] = aggregate of row i, cpart = aggregate partition.
+uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, const std::vector<uint64_t>& part,
+                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart);
+// R = P^T of piecewise-constant P: rows = aggregates, fine indices ascending
+void transpose_aggregates(const std::vector<uint32_t>& agg, uint32_t nagg, std::vector<uint32_t>& r_row,
+                          std::vector<uint32_t>& r_col);
 
 struct AmgGpuLevel {
   AmgLevelDev dev{};
@@ -229,6 +237,7 @@ struct Solver {
   LagReader inner;
   // AMG
   bool amg_built = false;
+  int amg_setup_path = 0;          // 0 not built, 1 host, 2 device (build_amg_device)
   int tail_first = 1;              // first AMG level handled by k_amg_tail
   bool tail_lds = true;            // LDS-resident tail kernel when it fits
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
@@ -263,6 +272,7 @@ struct Solver {
   void debug_buffer(int id, float* out);
   double algorithmic_step_bytes() const;
   double smoother_bytes() const;
+  uint64_t amg_level_digest(int li);  // FNV-1a over every byte of level li's device image
 
  private:
   void rotate();
@@ -271,6 +281,9 @@ struct Solver {
   cfd_linear_stats solve();
   void ensure_fgmres();
   void ensure_amg();
+  void build_amg_host();
+  bool build_amg_device();  // single GPU; false: a per-thread capacity overflowed (host path then)
+  void set_amg_full_policy(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);

@@ -189,6 +189,11 @@ cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t*
 /* AMG hierarchy summary: number of levels and rows/nnz per level.            */
 cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* rows /*[20]*/,
                           uint64_t* nnz /*[20]*/);
+/* AMG setup path taken (0 not built yet, 1 host, 2 device; SURVEY §8(f)
+ * rank 3) and an FNV-1a digest of every byte of level `level`'s device image
+ * (matrix, diagonal, P, R) -- host and device setups must agree bit-for-bit.
+ * Debug/parity only; not part of the reference surface.                     */
+cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path, uint64_t* digest);
 /* Algorithmic bytes of one step under the fixed schedule.    */
 double cfd_step_algorithmic_bytes(const cfd_solver* s);
 

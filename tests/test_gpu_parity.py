@@ -361,3 +361,55 @@ def test_fine_mesh_obstacle_gpu():
             break
         uu = g.get_u()
         assert np.all(np.isfinite(uu))
+
+
+def _amg_setup_pair(mesh, monkeypatch, **cfg):
+    """The same AMG problem solved with the device setup (default on one GPU)
+    and with CFD_AMG_SETUP=host; both after one step at t = 0.05 (inlet on)."""
+    out = []
+    for path in ("device", "host"):
+        if path == "host":
+            monkeypatch.setenv("CFD_AMG_SETUP", "host")
+        else:
+            monkeypatch.delenv("CFD_AMG_SETUP", raising=False)
+        s = GpuSolver(mesh, config=default_config(**cfg))
+        s.set_dt(1e-3)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_alpha_u(0.7)
+        s.set_alpha_p(0.3)
+        s.set_precond_type(1)
+        s.initialize_history()
+        c = s.constants
+        c.time = 0.05
+        s.constants = c
+        s.step()
+        out.append(s)
+    monkeypatch.delenv("CFD_AMG_SETUP", raising=False)
+    return out
+
+
+@pytest.mark.parametrize("which", ["amg_test", "bench_100k", "c1", "voronoi"])
+def test_amg_device_setup_matches_host(which, monkeypatch):
+    """the device-side AMG setup (Galerkin product and
+    level packing on the GPU, aggregation on the host) builds a hierarchy
+    byte-identical to the host setup -- every level's matrix, diagonal, P and
+    R -- so the steps that follow are bit-identical too."""
+    if which == "amg_test":
+        mesh = backwards_step()
+    elif which == "bench_100k":
+        mesh = bench_mesh(0.0055, 30)
+    elif which == "c1":
+        mesh = bench_mesh(0.001723, 100)
+    else:
+        from tests.voronoi import voronoi_channel
+        mesh = voronoi_channel(4000, seed=12345)
+    dev, host = _amg_setup_pair(mesh, monkeypatch, fixed_outer=1, fixed_inner=4)
+    pd, dd = dev.amg_setup_info()
+    ph, dh = host.amg_setup_info()
+    assert (pd, ph) == (2, 1), "device setup must be the path taken on one GPU"
+    assert dev.amg_levels() == host.amg_levels()
+    assert len(dd) >= (3 if which in ("bench_100k", "c1") else 1)
+    assert dd == dh, [i for i, (a, b) in enumerate(zip(dd, dh)) if a != b]
+    _assert_same_fields(dev, host, f"{which} device vs host AMG setup")
+    _assert_same_info(dev, host, which)
