@@ -44,12 +44,14 @@ struct Rows {
     else
       return (size_t)m.rowptr[i] + k;
   }
-  __device__ __forceinline__ uint32_t col(uint32_t i, uint32_t k) const { return (uint32_t)m.col[at(i, k)]; }
+  __device__ __forceinline__ int32_t col(uint32_t i, uint32_t k) const { return m.col[at(i, k)]; }
   __device__ __forceinline__ float val(uint32_t i, uint32_t k) const { return m.val[at(i, k)]; }
 };
 
 // FILL = false: cnt[I] = number of distinct coarse columns of row I.
-// FILL = true: the sorted row written at rowptr_c[I].
+// FILL = true: the sorted row written at rowptr_c[I].  `agg` is indexed by
+// the (signed local) fine column: on a distributed level it holds the global
+// aggregate ids of the owned rows and of the ghosts (halo-exchanged).
 template <bool ELL, bool FILL>
 __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32_t* __restrict__ agg,
                                                      const uint32_t* __restrict__ r_row,
@@ -76,10 +78,11 @@ __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32
   float cv[kSetupMaxCoarse];
   uint32_t nl = 0;
   for (;;) {
-    uint32_t jmin = 0xFFFFFFFFu;
+    // columns are signed local indices (ghosts of lower ranks < 0): local order == global order
+    int32_t jmin = INT32_MAX;
     for (uint32_t t = 0; t < m; ++t)
       if (cur[t] < end[t]) jmin = min(jmin, a.col(mem[t], cur[t]));
-    if (jmin == 0xFFFFFFFFu) break;
+    if (jmin == INT32_MAX) break;
     float ra = 0.0f;  // RA[I, jmin], members in ascending order (first touch: 0 + ...)
     for (uint32_t t = 0; t < m; ++t)
       if (cur[t] < end[t] && a.col(mem[t], cur[t]) == jmin) {
@@ -142,9 +145,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_pack(SetupMatrix A, uint32_t n, 
     bool has = false;
     const uint32_t l = a.len(i);
     for (uint32_t k = 0; k < l; ++k) {
-      const uint32_t c = a.col(i, k);
+      const int32_t c = a.col(i, k);
       const float v = a.val(i, k);
-      if (c == i) {
+      if (c == (int32_t)i) {
         has = true;
         raw = v;
         diag = raw;
@@ -153,9 +156,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_pack(SetupMatrix A, uint32_t n, 
         const size_t o = (size_t)off * st + i;
         val[o] = v;
         if (use16)
-          col16[o] = (int16_t)((int32_t)c - (int32_t)i);
+          col16[o] = (int16_t)(c - (int32_t)i);
         else
-          col32[o] = (int32_t)c;
+          col32[o] = c;
         ++off;
       }
     }

@@ -6,9 +6,10 @@
 namespace cfd2 {
 
 // A fine level as the setup kernels read it: ELL slot-major (level 0, the
-// assembled scalar matrix: entry k of row i at k*ld + i, columns int32) or
-// CSR (coarse levels: rowptr, columns u32 stored as int32 bits).  Columns are
-// sorted ascending within each row.
+// assembled scalar matrix: entry k of row i at k*ld + i) or CSR (coarse
+// levels).  Columns are signed local indices (global ids on one GPU and on
+// replicated levels; owned-relative with ghosts below 0 / above npad on a
+// distributed rank), sorted ascending within each row.
 struct SetupMatrix {
   int ell;
   uint32_t ld;               // ELL slot stride

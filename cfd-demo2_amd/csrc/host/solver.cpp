@@ -74,7 +74,6 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
     cell_plan = build_halo_plan(starts, rk, topo.srow.data(), N, topo.scol.data(), topo.ghost, topo.glo,
                                 topo.npad);
     make_plan_buffers(cell_plan, 8);
-    build_scalar_pattern(mesh, gpattern);
     red_local = arena.alloc<float>(m1 + 1);
     red_gather = arena.alloc<float>((size_t)R * (m1 + 1));
     red_comb = arena.alloc<float>(m1 + 1);
@@ -513,6 +512,17 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 // stencil: rows fill the ELL width) and on latency-bound small levels;
 // predicated loads on the big coarse levels, whose row lengths vary (same-box
 // A/B at C2: level 1 smoother 58 vs 66 us, small-level residual 6 vs 8.5 us).
+std::vector<uint64_t> Solver::allgather_u64(uint64_t mine) {
+  std::vector<uint64_t> all(R, mine);
+  if (!dist()) return all;
+  if (!d_u64) d_u64 = arena.alloc<uint64_t>((size_t)R + 1);
+  CFD_HIP(hipMemcpyAsync(d_u64, &mine, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+  comm->allgather(d_u64, d_u64 + 1, sizeof(uint64_t), stream);
+  CFD_HIP(hipMemcpyAsync(all.data(), d_u64 + 1, (size_t)R * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+  sync();
+  return all;
+}
+
 void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
   const char* fe = std::getenv("CFD_AMG_FULL");
   G.dev.full = fe ? (fe[0] == '1') : (li == 0 || G.dev.n <= (1u << 19));
@@ -539,18 +549,36 @@ void Solver::build_amg_host() {
     A0.val = std::move(own);
     H = build_amg_hierarchy(A0, kMaxAmgLevels);
   } else {
-    // all-gather the matrix values (row order = global order, rank by rank)
-    A0 = gpattern;
-    std::vector<size_t> off(R + 1);
-    for (int q = 0; q <= R; ++q) off[q] = (size_t)A0.row[starts[q]] * sizeof(float);
-    if (off[rk + 1] - off[rk] != own.size() * sizeof(float)) throw std::logic_error("AMG gather: row mismatch");
-    float* dbuf = arena.alloc<float>(A0.col.size());
-    CFD_HIP(hipMemcpyAsync((char*)dbuf + off[rk], own.data(), own.size() * sizeof(float), hipMemcpyHostToDevice,
-                           stream));
-    comm->allgatherv_inplace(dbuf, off, stream);
-    A0.val.resize(A0.col.size());
-    CFD_HIP(hipMemcpyAsync(A0.val.data(), dbuf, A0.col.size() * sizeof(float), hipMemcpyDeviceToHost, stream));
+    // all-gather the global pattern and the values (row order = global order, rank by rank)
+    const std::vector<uint64_t> nz = allgather_u64(topo.scol.size());
+    std::vector<uint64_t> eoff(R + 1, 0);
+    for (int q = 0; q < R; ++q) eoff[q + 1] = eoff[q] + nz[q];
+    std::vector<size_t> roff(R + 1), coff(R + 1);
+    for (int q = 0; q <= R; ++q) {
+      roff[q] = starts[q] * sizeof(uint32_t);
+      coff[q] = eoff[q] * sizeof(uint32_t);
+    }
+    const size_t nnz_all = eoff[R];
+    std::vector<uint32_t> lens(NG, 0);
+    for (uint32_t i = 0; i < N; ++i) lens[starts[rk] + i] = topo.srow[i + 1] - topo.srow[i];
+    uint32_t* d_lens = arena.alloc<uint32_t>(NG);
+    uint32_t* d_cols = arena.alloc<uint32_t>(nnz_all);
+    float* d_vals = arena.alloc<float>(nnz_all);
+    CFD_HIP(hipMemcpyAsync(d_lens, lens.data(), (size_t)NG * 4, hipMemcpyHostToDevice, stream));
+    CFD_HIP(hipMemcpyAsync(d_cols + eoff[rk], topo.scol.data(), topo.scol.size() * 4, hipMemcpyHostToDevice, stream));
+    CFD_HIP(hipMemcpyAsync(d_vals + eoff[rk], own.data(), own.size() * 4, hipMemcpyHostToDevice, stream));
+    comm->allgatherv_inplace(d_lens, roff, stream);
+    comm->allgatherv_inplace(d_cols, coff, stream);
+    comm->allgatherv_inplace(d_vals, coff, stream);
+    A0.rows = A0.cols = NG;
+    A0.row.assign((size_t)NG + 1, 0);
+    A0.col.resize(nnz_all);
+    A0.val.resize(nnz_all);
+    CFD_HIP(hipMemcpyAsync(lens.data(), d_lens, (size_t)NG * 4, hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(A0.col.data(), d_cols, nnz_all * 4, hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(A0.val.data(), d_vals, nnz_all * 4, hipMemcpyDeviceToHost, stream));
     sync();
+    for (uint32_t i = 0; i < NG; ++i) A0.row[i + 1] = A0.row[i] + lens[i];
     H = build_amg_hierarchy(A0, kMaxAmgLevels, starts);
   }
   const int L = (int)H.size();
@@ -657,7 +685,7 @@ void Solver::ensure_amg() {
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
   const auto t_start = std::chrono::steady_clock::now();
   const char* se = std::getenv("CFD_AMG_SETUP");
-  const bool device_setup = !dist() && !(se && std::string(se) == "host");
+  const bool device_setup = !(se && std::string(se) == "host");
   const char* how = "device";
   amg_setup_path = 2;
   if (!(device_setup && build_amg_device())) {

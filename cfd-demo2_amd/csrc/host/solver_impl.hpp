@@ -108,8 +108,6 @@ struct Topology {
 void build_topology(const cfd_mesh_view& m, Topology& t);
 // Owned range [c0, c1) of a distributed rank, ghosts from the face neighbours.
 void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c1);
-// Global scalar CSR pattern (init/mesh.rs:27-53) of the whole mesh.
-void build_scalar_pattern(const cfd_mesh_view& m, HostCsr& out);
 
 // AMG hierarchy (linear_solver/amg.rs:84-235, 374-595) built on the host.
 struct AmgHostLevel {
@@ -169,7 +167,7 @@ struct Solver {
   uint32_t shift = 0;            // owned base offset of every per-cell vector (>= glo, 64-aligned)
   size_t vlen = 0;               // elements per component of a per-cell vector
   HaloPlan cell_plan;
-  HostCsr gpattern;              // global scalar pattern (distributed AMG setup)
+  uint64_t* d_u64 = nullptr;     // [R + 1] all-gather scratch of allgather_u64
   float* red_local = nullptr;    // [m1] this rank's reduction results
   float* red_gather = nullptr;   // [R * m1]
   float* red_comb = nullptr;     // [m1]
@@ -282,8 +280,9 @@ struct Solver {
   void ensure_fgmres();
   void ensure_amg();
   void build_amg_host();
-  bool build_amg_device();  // single GPU; false: a per-thread capacity overflowed (host path then)
+  bool build_amg_device();  // false: a per-thread capacity overflowed on some rank (host path then)
   void set_amg_full_policy(AmgGpuLevel& G, int li);
+  std::vector<uint64_t> allgather_u64(uint64_t mine);  // every rank's value (collective)
   void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);

@@ -23,40 +23,6 @@ inline float wdistance(float ax, float ay, float bx, float by) {
 
 void build_topology(const cfd_mesh_view& m, Topology& t) { build_topology(m, t, 0, m.num_cells); }
 
-void build_scalar_pattern(const cfd_mesh_view& m, HostCsr& out) {  // init/mesh.rs:27-53
-  const uint32_t N = m.num_cells, F = m.num_faces, NONE = 0xFFFFFFFFu;
-  std::vector<uint32_t> aoff(N + 1, 0);
-  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] = 1;
-  for (uint32_t f = 0; f < F; ++f)
-    if (m.face_neighbor[f] != NONE) {
-      aoff[m.face_owner[f] + 1]++;
-      aoff[m.face_neighbor[f] + 1]++;
-    }
-  for (uint32_t i = 0; i < N; ++i) aoff[i + 1] += aoff[i];
-  std::vector<uint32_t> adj(aoff[N]);
-  std::vector<uint32_t> pos(aoff.begin(), aoff.end() - 1);
-  for (uint32_t i = 0; i < N; ++i) adj[pos[i]++] = i;
-  for (uint32_t f = 0; f < F; ++f) {
-    const uint32_t o = m.face_owner[f], n = m.face_neighbor[f];
-    if (n == NONE) continue;
-    adj[pos[o]++] = n;
-    adj[pos[n]++] = o;
-  }
-  out.rows = out.cols = N;
-  out.row.assign(N + 1, 0);
-  out.col.clear();
-  out.col.reserve(aoff[N]);
-  for (uint32_t i = 0; i < N; ++i) {
-    auto b = adj.begin() + aoff[i], e = adj.begin() + aoff[i + 1];
-    std::sort(b, e);
-    e = std::unique(b, e);
-    out.row[i] = (uint32_t)out.col.size();
-    out.col.insert(out.col.end(), b, e);
-  }
-  out.row[N] = (uint32_t)out.col.size();
-  out.val.clear();
-}
-
 void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c1) {
   const uint32_t NG = m.num_cells, F = m.num_faces;
   if (NG == 0) throw std::invalid_argument("mesh has no cells");

@@ -126,3 +126,46 @@ def test_group_c1_scale(replicate_rows):
         _assert_same_fields(g, o, f"C1 R=4 step {k}")
         _assert_same_info(g, o, f"C1 R=4 step {k}")
     g.close()
+
+
+@pytest.mark.parametrize("nranks,rep,which", [(2, 50, "amg_test"), (3, 50, "amg_test"), (4, 4096, "bench_100k"),
+                                              (4, 262144, "c1")])
+def test_group_amg_device_setup_matches_host(nranks, rep, which, replicate_rows, monkeypatch):
+    """Distributed device-side AMG setup: every rank
+    builds its rows of the distributed levels and the replicated tail on the
+    GPU (aggregate ids of ghost columns by halo exchange, first replicated
+    level all-gathered) -- byte-identical, rank by rank and level by level, to
+    the host setup that all-gathers the whole fine matrix."""
+    replicate_rows(rep)
+    mesh = {"amg_test": backwards_step, "bench_100k": lambda: bench_mesh(0.0055, 30),
+            "c1": lambda: bench_mesh(0.001723, 100)}[which]()
+    groups = []
+    for path in ("device", "host"):
+        if path == "host":
+            monkeypatch.setenv("CFD_AMG_SETUP", "host")
+        else:
+            monkeypatch.delenv("CFD_AMG_SETUP", raising=False)
+        g = GpuGroup(mesh, nranks, config=default_config(fixed_outer=1, fixed_inner=4))
+        g.set_dt(1e-3)
+        g.set_viscosity(0.01)
+        g.set_density(1.0)
+        g.set_alpha_u(0.7)
+        g.set_alpha_p(0.3)
+        g.set_precond_type(1)
+        g.initialize_history()
+        c = g.constants
+        c.time = 0.05
+        g.constants = c
+        g.step()
+        groups.append(g)
+    monkeypatch.delenv("CFD_AMG_SETUP", raising=False)
+    dev, host = groups
+    for r in range(nranks):
+        pd, dd = dev.ranks[r].amg_setup_info()
+        ph, dh = host.ranks[r].amg_setup_info()
+        assert (pd, ph) == (2, 1), f"rank {r}"
+        assert dev.ranks[r].amg_levels() == host.ranks[r].amg_levels(), f"rank {r}"
+        assert dd == dh, f"rank {r} levels differ: {[i for i, (a, b) in enumerate(zip(dd, dh)) if a != b]}"
+    _assert_same_fields(dev, host, f"{which} R={nranks} device vs host setup")
+    dev.close()
+    host.close()
