@@ -16,3 +16,8 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_amg_smooth
   python3 $ROOT/bench.py --config $CFG --no-cpu-baseline --steps 1 --warmup 2 > $OUT/bench_write.json 2> $OUT/bench_write.log && \
 python3 $ROOT/tools/summarize_stats.py $OUT/trace > $OUT/kernel_top.txt && \
 python3 $ROOT/tools/pmc_summary.py $OUT $OUT/smoother_pmc.json $CFG
+
+# Per-kernel HBM traffic of every kernel (profiles/r01/c2_kernel_traffic.txt):
+#   bash tools/gpu_pmc_all.sh c2   (FETCH_SIZE and WRITE_SIZE passes, no kernel filter)
+# Default bench line with the CPU baseline (profiles/r01/bench_c2.json):
+#   python bench.py
