@@ -527,6 +527,31 @@ __device__ __forceinline__ float gat(bool on, const float* p) {
   }
 }
 
+// Vector gathers: the columns of one slot for 4 consecutive rows are, for
+// every interior row of a face stencil, 4 consecutive cells (c, c+1, c+2,
+// c+3): one 16-byte load (dword-aligned: gfx950 global loads need only
+// 4-byte alignment for multi-dword accesses) fetches all four, and only
+// threads whose slot is not consecutive (boundary / cut cells) issue the
+// per-row loads.  Cuts the gather instructions per wave ~4x for scalar
+// vectors (the row kernels are VMEM-issue bound: SQ_WAIT_INST_ANY ~0.5-0.7
+// of wave cycles, tools/gpu_sq.sh).  Every vector read this
+// way has >= 64 floats of padding past its last (ghost) entry.
+#ifndef CFD_VGATHER
+#define CFD_VGATHER 1
+#endif
+// k_spmv keeps one dwordx3 per (cell, slot): its 12-float vector form was
+// slower in the same-box A/B (234 -> 250 us) while the scalar-vector kernels
+// gained (level-0 smoother 84 -> 78 us, Schur predict 198 -> 185, correct
+// 166 -> 159)
+#ifndef CFD_VGATHER_SPMV
+#define CFD_VGATHER_SPMV 0
+#endif
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ f4u ld4u(const float* p) { return *reinterpret_cast<const f4u*>(p); }
+__device__ __forceinline__ bool consec4(const int c[4]) {
+  return c[1] == c[0] + 1 && c[2] == c[0] + 2 && c[3] == c[0] + 3;
+}
+
 // Slot-group sizes of the 4-cells-per-thread kernels (all loads of a group are
 // issued before the first use).  Build-time tunables (tools/ab_variants.py).
 #ifndef CFD_SPMV_U
@@ -568,16 +593,40 @@ __device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* 
     load2x4(A.cval_g + off, g[u]);
     ccols4<D16>(A, off, i0, c[u]);
   }
+  if constexpr (CFD_VGATHER_SPMV) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {  // 12 consecutive floats = (u, v, p) of cells c0..c0+3
+      const float* b = x + 3 * (ptrdiff_t)c[u][0];
+      const f4u q0 = ld4u(b), q1 = ld4u(b + 4), q2 = ld4u(b + 8);
+      const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool on = r0 + u < u4(ln, k);
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-      xg[u][k][0] = gat<true>(on, x + j);
-      xg[u][k][1] = gat<true>(on, x + j + 1);
-      xg[u][k][2] = gat<true>(on, x + j + 2);
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) xg[u][k][t] = f[3 * k + t];
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (!consec4(c[u])) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+          xg[u][k][0] = x[j];
+          xg[u][k][1] = x[j + 1];
+          xg[u][k][2] = x[j + 2];
+        }
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool on = r0 + u < u4(ln, k);
+        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+        xg[u][k][0] = gat<true>(on, x + j);
+        xg[u][k][1] = gat<true>(on, x + j + 1);
+        xg[u][k][2] = gat<true>(on, x + j + 2);
+      }
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -800,16 +849,44 @@ __device__ __forceinline__ void predict_group(const CoupledMatrix& A, const floa
     load2x4(A.cval_g + off, g[u]);
     ccols4<D16>(A, off, i0, c[u]);
   }
+  if constexpr (CFD_VGATHER) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      const f4u d = ld4u(dinv_uv + c[u][0]);
+      const float* b = w_in + 3 * (ptrdiff_t)c[u][0];
+      const f4u q0 = ld4u(b), q1 = ld4u(b + 4), q2 = ld4u(b + 8);
+      const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+      const float dd[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool on = r0 + u < u4(ln, k);
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-      gd[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, dinv_uv + c[u][k]);
-      gu[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j);
-      gv[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j + 1);
+      for (int k = 0; k < 4; ++k) {
+        gd[u][k] = dd[k];
+        gu[u][k] = f[3 * k];
+        gv[u][k] = f[3 * k + 1];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (!consec4(c[u])) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+          gd[u][k] = dinv_uv[c[u][k]];
+          gu[u][k] = w_in[j];
+          gv[u][k] = w_in[j + 1];
+        }
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool on = r0 + u < u4(ln, k);
+        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+        gd[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, dinv_uv + c[u][k]);
+        gu[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j);
+        gv[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j + 1);
+      }
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -898,10 +975,27 @@ __device__ __forceinline__ void correct_group(const CoupledMatrix& A, const floa
     load2x4(A.cval_g + off, g[u]);
     ccols4<D16>(A, off, i0, c[u]);
   }
+  if constexpr (CFD_VGATHER) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      const f4u q = ld4u(p_sol + c[u][0]);
+      pj[u][0] = q.x;
+      pj[u][1] = q.y;
+      pj[u][2] = q.z;
+      pj[u][3] = q.w;
+    }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(r0 + u < u4(ln, k), p_sol + c[u][k]);
+    for (int u = 0; u < U; ++u)
+      if (!consec4(c[u])) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) pj[u][k] = p_sol[c[u][k]];
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(r0 + u < u4(ln, k), p_sol + c[u][k]);
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -956,6 +1050,20 @@ __global__ void k_solve_triangular(const float* H, const float* g, float* y, int
   }
 }
 
+// the preconditioned vectors Z_i are read once per restart cycle here (nontemporal, CFD_UPDX_NT)
+#ifndef CFD_UPDX_NT
+#define CFD_UPDX_NT 1
+#endif
+__device__ __forceinline__ float4 ld4_upd(const float* p) {
+#if CFD_UPDX_NT
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+
 // basis_size x axpy_from_y (gmres_ops.wgsl:96-105) fused: x = y_i * z_i + x, i ascending
 __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __restrict__ z,
                                                      size_t stride, const float* __restrict__ y,
@@ -966,8 +1074,8 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
     float4 xv = *reinterpret_cast<const float4*>(x + e);
     int ii = 0;
     for (; ii + 1 < k; ii += 2) {
-      const float4 z0 = *reinterpret_cast<const float4*>(z + (size_t)ii * stride + e);
-      const float4 z1 = *reinterpret_cast<const float4*>(z + (size_t)(ii + 1) * stride + e);
+      const float4 z0 = ld4_upd(z + (size_t)ii * stride + e);
+      const float4 z1 = ld4_upd(z + (size_t)(ii + 1) * stride + e);
       const float y0 = y[ii], y1 = y[ii + 1];
       xv.x = y0 * z0.x + xv.x;
       xv.y = y0 * z0.y + xv.y;
@@ -979,7 +1087,7 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
       xv.w = y1 * z1.w + xv.w;
     }
     if (ii < k) {
-      const float4 z0 = *reinterpret_cast<const float4*>(z + (size_t)ii * stride + e);
+      const float4 z0 = ld4_upd(z + (size_t)ii * stride + e);
       const float y0 = y[ii];
       xv.x = y0 * z0.x + xv.x;
       xv.y = y0 * z0.y + xv.y;
@@ -1050,10 +1158,27 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       for (int k = 0; k < 4; ++k) c[u][k] = (int)i0 + k;
     }
   }
+  if constexpr (ALWAYS && FULL && CFD_VGATHER) {
 #pragma unroll
-  for (int u = 0; u < kU; ++u)
+    for (int u = 0; u < kU; ++u) {
+      const f4u q = ld4u(x + c[u][0]);
+      xg[u][0] = q.x;
+      xg[u][1] = q.y;
+      xg[u][2] = q.z;
+      xg[u][3] = q.w;
+    }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && FULL>(r0 + u < u4(ln, k), x + c[u][k]);
+    for (int u = 0; u < kU; ++u)
+      if (!consec4(c[u])) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) xg[u][k] = x[c[u][k]];
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && FULL>(r0 + u < u4(ln, k), x + c[u][k]);
+  }
 }
 
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
