@@ -1488,6 +1488,122 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 }
 
 
+// The LDS tail with every matrix of the tail levels in LDS as well (the blob
+// built once by the host from the level images: off-diagonal CSR with u16
+// columns, dv/de, drank, P and R).  Each phase is then LDS reads + one
+// barrier instead of a global (L2) round trip per matrix slot.  Same row
+// arithmetic, in the same order, as smooth_row / residual_row.
+__global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __restrict__ tail,
+                                                        const TailBlobLevel* __restrict__ desc,
+                                                        const uint32_t* __restrict__ blob, uint32_t blob_words,
+                                                        uint32_t vec_floats, int first, int nlev) {
+  extern __shared__ float sm[];
+  const uint32_t t = threadIdx.x, nt = blockDim.x;
+  uint32_t* bw = reinterpret_cast<uint32_t*>(sm + vec_floats);
+  for (uint32_t w = 4 * t; w < blob_words; w += 4 * nt)
+    *reinterpret_cast<uint4*>(bw + w) = *reinterpret_cast<const uint4*>(blob + w);
+  auto base = [&](int l) {
+    uint32_t o = 0;
+    for (int k = first; k < l; ++k) o += 4 * r4(desc[k].n);
+    return sm + o;
+  };
+  {
+    const uint32_t n = desc[first].n;
+    float* B0 = base(first) + 2 * r4(n);
+    const float* gb = tail[first].b;
+    for (uint32_t i = t; i < n; i += nt) B0[i] = gb[i];
+  }
+  __syncthreads();
+  auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
+  auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
+  auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
+    const uint32_t* ro = bw + D.rowoff;
+    const float* val = fw(D.val);
+    const uint16_t* col = hw(D.col);
+    float sigma = 0.0f;
+    for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) sigma += val[e] * xin[col[e]];
+    return wmix(xin[i], (B[i] - sigma) / fw(D.de)[i], 0.8f);
+  };
+  for (int l = first; l + 1 < nlev; ++l) {
+    const TailBlobLevel D = desc[l];
+    const uint32_t nr = r4(D.n);
+    float* X = base(l);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    float* Rr = B + nr;
+    const float* de = fw(D.de);
+    for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
+    __syncthreads();
+    {
+      const uint32_t* ro = bw + D.rowoff;
+      const float* val = fw(D.val);
+      const float* dv = fw(D.dv);
+      const uint16_t* col = hw(D.col);
+      const uint8_t* drank = reinterpret_cast<const uint8_t*>(bw + D.drank);
+      for (uint32_t i = t; i < D.n; i += nt) {
+        const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
+        float ax = 0.0f;
+        for (uint32_t r = 0; r <= len; ++r) {
+          if (r == dr) ax += dv[i] * XT[i];
+          if (r == len) break;
+          ax += val[e0 + r] * XT[col[e0 + r]];
+        }
+        Rr[i] = B[i] - ax;
+      }
+    }
+    __syncthreads();
+    float* CB = base(l + 1) + 2 * r4(desc[l + 1].n);
+    {
+      const uint16_t* rrow = hw(D.r_row);
+      const uint16_t* rcol = hw(D.r_col);
+      for (uint32_t I = t; I < D.nc; I += nt) {
+        float sum = 0.0f;
+        for (uint32_t k = rrow[I]; k < rrow[I + 1]; ++k) sum += 1.0f * Rr[rcol[k]];
+        CB[I] = sum;
+      }
+    }
+    __syncthreads();
+  }
+  {
+    const TailBlobLevel D = desc[nlev - 1];
+    const uint32_t nr = r4(D.n);
+    float* X = base(nlev - 1);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    const float* de = fw(D.de);
+    for (int s = 0; s < 10; ++s) {
+      if (s == 0) {
+        for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
+      } else {
+        const float* xin = (s & 1) ? XT : X;
+        float* xout = (s & 1) ? X : XT;
+        for (uint32_t i = t; i < D.n; i += nt) xout[i] = smooth(D, xin, B, i);
+      }
+      __syncthreads();
+    }
+  }
+  for (int l = nlev - 2; l >= first; --l) {
+    const TailBlobLevel D = desc[l];
+    const uint32_t nr = r4(D.n);
+    float* X = base(l);
+    float* XT = X + nr;
+    float* B = XT + nr;
+    const float* XC = base(l + 1);
+    const uint16_t* agg = hw(D.agg);
+    for (uint32_t i = t; i < D.n; i += nt) {
+      float corr = 0.0f;
+      corr += 1.0f * XC[agg[i]];
+      XT[i] += corr;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < D.n; i += nt) X[i] = smooth(D, XT, B, i);
+    __syncthreads();
+  }
+  const float* X0 = base(first);
+  float* gx = tail[first].x;
+  for (uint32_t i = t; i < desc[first].n; i += nt) gx[i] = X0[i];
+}
+
 // ---------------------- check_evolution statistics --------------------------
 // AoS view of the reference FluidState (coupled_solver.rs:504 reads the 32-byte
 // records as a flat f32 array): record r = {u.x, u.y, p, d_p, gp.x, gp.y, 0, 0}.
@@ -1766,6 +1882,18 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
     attr = true;
   }
   hipLaunchKernelGGL(k_amg_tail_lds, dim3(1), dim3(1024), lds_bytes, s, tail, first, nlev);
+}
+void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
+                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax);
+    attr = true;
+  }
+  const size_t lds = 4 * ((size_t)vec_floats + blob_words);
+  hipLaunchKernelGGL(k_amg_tail_blob, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats, first,
+                     nlev);
 }
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
                               uint64_t gbase, uint64_t rec0, double* partial, hipStream_t s) {

@@ -173,6 +173,14 @@ struct AmgTailLevel {
 };
 constexpr int kMaxAmgLevels = 20;
 
+// One tail level inside the LDS blob of k_amg_tail_blob (offsets in 32-bit
+// words from the blob start, each array 16-byte aligned): off-diagonal CSR
+// with u16 columns, diagonal data, P (agg, u16) and R (u16 CSR).
+struct TailBlobLevel {
+  uint32_t n, nc;
+  uint32_t de, dv, rowoff, drank, val, col, agg, r_row, r_col;
+};
+
 // ---------------- launch wrappers (kernels.hip) ----------------
 void launch_prepare(const PrepareArgs& a, hipStream_t s);
 void launch_assemble(const AssembleArgs& a, hipStream_t s);
@@ -229,6 +237,11 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, 
 // lds_bytes > 0: the LDS-resident version (needs every tail vector in <= kTailLdsMax bytes)
 constexpr size_t kTailLdsMax = 160 * 1024 - 1024;
 void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s);
+// The LDS tail with the matrices in LDS too: `blob` (blob_words 32-bit words,
+// a multiple of 4) is copied into LDS after the vectors (vec_floats floats);
+// desc[l] describes level l (l in [first, nlev)).  lds_bytes = 4 * (vec_floats + blob_words).
+void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
+                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
 // partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}

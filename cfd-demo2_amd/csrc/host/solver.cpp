@@ -714,11 +714,125 @@ void Solver::ensure_amg() {
     tl[li].r = levels[li].r;
   }
   d_tail = arena.upload(tl, stream);
+  const char* tb_env = std::getenv("CFD_AMG_TAIL_BLOB");
+  if (tail_lds && !(tb_env && tb_env[0] == '0')) build_tail_blob(std::max({tail_first, 1, dist() ? amg_g : 0}));
   sync();
   amg_built = true;
   if (timing)
     std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s\n", how, L,
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+}
+
+// LDS image of the tail levels [tf, L) for k_amg_tail_blob: every array the
+// tail V-cycle reads, compacted (off-diagonal CSR, u16 indices) from the
+// level images, when vectors + blob fit in one CU's LDS.
+void Solver::build_tail_blob(int tf) {
+  tail_blob_first = -1;
+  const int L = (int)levels.size();
+  if (tf >= L) return;
+  std::vector<uint32_t> blob;
+  std::vector<TailBlobLevel> desc(L);
+  auto align4 = [&] {
+    while (blob.size() % 4) blob.push_back(0);
+    return (uint32_t)blob.size();
+  };
+  auto put_f = [&](const float* v, size_t n) {
+    const uint32_t o = align4();
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t w;
+      std::memcpy(&w, v + i, 4);
+      blob.push_back(w);
+    }
+    return o;
+  };
+  auto put_u32 = [&](const std::vector<uint32_t>& v) {
+    const uint32_t o = align4();
+    blob.insert(blob.end(), v.begin(), v.end());
+    return o;
+  };
+  auto put_u16 = [&](const std::vector<uint32_t>& v) {
+    const uint32_t o = align4();
+    for (size_t i = 0; i < v.size(); i += 2)
+      blob.push_back((v[i] & 0xFFFFu) | ((i + 1 < v.size() ? v[i + 1] & 0xFFFFu : 0u) << 16));
+    return o;
+  };
+  auto put_u8 = [&](const std::vector<uint8_t>& v) {
+    const uint32_t o = align4();
+    for (size_t i = 0; i < v.size(); i += 4) {
+      uint32_t w = 0;
+      for (size_t b = 0; b < 4 && i + b < v.size(); ++b) w |= (uint32_t)v[i + b] << (8 * b);
+      blob.push_back(w);
+    }
+    return o;
+  };
+  auto d2h = [&](void* dst, const void* src, size_t bytes) {
+    if (bytes) CFD_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream));
+  };
+  uint32_t vec = 0;
+  for (int l = tf; l < L; ++l) {
+    const AmgLevelDev& d = levels[l].dev;
+    const uint32_t n = d.n, st = d.stride;
+    if (n > 65535 || d.nc > 65535) return;
+    const size_t slots = (size_t)std::max(d.w, 1) * st;
+    std::vector<uint8_t> len(n), drank(n);
+    std::vector<float> dv(n), de(n), val(slots);
+    std::vector<int16_t> c16(d.use16 ? slots : 0);
+    std::vector<int32_t> c32(d.use16 ? 0 : slots);
+    d2h(len.data(), d.len, n);
+    d2h(drank.data(), d.drank, n);
+    d2h(dv.data(), d.dv, (size_t)n * 4);
+    d2h(de.data(), d.de, (size_t)n * 4);
+    d2h(val.data(), d.val, slots * 4);
+    if (d.use16) d2h(c16.data(), d.col16, slots * 2);
+    else d2h(c32.data(), d.col32, slots * 4);
+    std::vector<uint32_t> agg, rrow, rcol;
+    if (d.nc) {
+      agg.resize(n);
+      rrow.resize((size_t)d.nc + 1);
+      d2h(agg.data(), d.agg, (size_t)n * 4);
+      d2h(rrow.data(), d.r_row, rrow.size() * 4);
+    }
+    sync();
+    if (d.nc) {
+      rcol.resize(rrow[d.nc]);
+      d2h(rcol.data(), d.r_col, rcol.size() * 4);
+      sync();
+    }
+    std::vector<uint32_t> ro(n + 1, 0), cols;
+    std::vector<float> vals;
+    for (uint32_t i = 0; i < n; ++i) {
+      ro[i + 1] = ro[i] + len[i];
+      for (uint32_t r = 0; r < len[i]; ++r) {
+        const size_t o = (size_t)r * st + i;
+        const int64_t c = d.use16 ? (int64_t)i + c16[o] : (int64_t)c32[o];
+        if (c < 0 || c >= (int64_t)n) return;  // tail levels are replicated: global columns
+        cols.push_back((uint32_t)c);
+        vals.push_back(val[o]);
+      }
+    }
+    TailBlobLevel& D = desc[l];
+    D.n = n;
+    D.nc = d.nc;
+    D.de = put_f(de.data(), n);
+    D.dv = put_f(dv.data(), n);
+    D.rowoff = put_u32(ro);
+    D.drank = put_u8(drank);
+    D.val = put_f(vals.data(), vals.size());
+    D.col = put_u16(cols);
+    if (d.nc) {
+      D.agg = put_u16(agg);
+      D.r_row = put_u16(rrow);
+      D.r_col = put_u16(rcol);
+    }
+    vec += 4 * ((n + 3) & ~3u);
+  }
+  align4();
+  if (4 * ((size_t)vec + blob.size()) > kTailLdsMax) return;
+  d_tail_blob = arena.upload(blob, stream);
+  d_tail_desc = arena.upload(desc, stream);
+  tail_blob_words = (uint32_t)blob.size();
+  tail_vec_floats = vec;
+  tail_blob_first = tf;
 }
 
 // HIP events around level-0 smoother launches (bench roofline); the pool is
@@ -832,7 +946,9 @@ void Solver::v_cycle() {
       comm->allgatherv_inplace(C.b, off, stream);
     }
   }
-  if (tf < L) {
+  if (tf < L && tf == tail_blob_first) {
+    launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf, L, stream);
+  } else if (tf < L) {
     size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL_LDS=0 disables)
     for (int l = tf; l < L; ++l) lds += 4 * (((size_t)levels[l].dev.n + 3) & ~(size_t)3) * sizeof(float);
     if (lds > kTailLdsMax || !tail_lds) lds = 0;

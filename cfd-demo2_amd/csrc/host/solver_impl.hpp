@@ -240,6 +240,12 @@ struct Solver {
   bool tail_lds = true;            // LDS-resident tail kernel when it fits
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
+  // k_amg_tail_blob: LDS image of the tail levels [tail_blob_first, L) (-1: none)
+  int tail_blob_first = -1;
+  uint32_t* d_tail_blob = nullptr;
+  TailBlobLevel* d_tail_desc = nullptr;
+  uint32_t tail_blob_words = 0, tail_vec_floats = 0;
+  void build_tail_blob(int tf);
   std::vector<AmgGpuLevel> levels;
   // host-side state
   cfd_constants constants{};
