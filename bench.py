@@ -84,13 +84,17 @@ def cpu_baseline(mesh, n_cells, outer_fixed, inner_fixed, sample_outer=3):
     }
 
 
-def load_traffic(round_tag):
+def load_traffic(round_tag, config, world):
     """HBM bytes per level-0 smoother launch from the committed rocprofv3 PMC
-    summary (profiles/<round>/smoother_pmc.json), or None."""
+    summary (profiles/<round>/smoother_pmc.json) when it was measured on this
+    workload (its config, one GPU), else None."""
     p = os.path.join(ROOT, "profiles", round_tag, "smoother_pmc.json")
     try:
         with open(p) as f:
-            return float(json.load(f)["hbm_bytes_per_launch"])
+            d = json.load(f)
+        if world != 1 or not d["kernel"].endswith(f"config {config}"):
+            return None
+        return float(d["hbm_bytes_per_launch"])
     except (OSError, KeyError, ValueError):
         return None
 
@@ -141,10 +145,16 @@ def main():
 
     cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner)
     t0 = time.perf_counter()
-    if world > 1:
+    # test / rehearsal mode: CFD_DIST_TRANSPORT=host stages every exchange through
+    # the gloo process group (several ranks may then share one GPU: CFD_BENCH_DEVICE)
+    transport = os.environ.get("CFD_DIST_TRANSPORT", "rccl")
+    device = int(os.environ.get("CFD_BENCH_DEVICE", local_rank))
+    if world > 1 and transport == "host":
+        solver = GpuSolver.create_dist_host(mesh, world, rank, device=device, config=cfg)
+    elif world > 1:
         uid = [dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        solver = GpuSolver.create_dist(mesh, world, rank, uid[0], device=local_rank, config=cfg)
+        solver = GpuSolver.create_dist(mesh, world, rank, uid[0], device=device, config=cfg)
     elif args.inproc_ranks > 1:
         from cfd2_amd import GpuGroup
         solver = GpuGroup(mesh, args.inproc_ranks, config=cfg)
@@ -223,7 +233,9 @@ def main():
             "cells_total": n_global,
             "cells_per_gpu": n_cells,
             "h": h_run,
-            "parallelism": f"slab{world} (RCCL halo + all-gather)" if world > 1 else "single",
+            "parallelism": (f"slab{world} (RCCL halo + all-gather)" if transport != "host" else
+                            f"slab{world} (host-staged gloo transport: test mode, not a bench line)")
+                           if world > 1 else "single",
         },
         "roofline": {
             "bound": "hbm",
@@ -232,7 +244,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_traffic(args.round),
+            "traffic": load_traffic(args.round, args.config, world if args.inproc_ranks <= 1 else args.inproc_ranks),
             "bytes_per_launch": sm_bytes,
             "avg_launch_us": sm_avg_s * 1e6,
             "launches": sm_n,

@@ -15,6 +15,12 @@ _vp = C.c_void_p
 _bound = False
 
 
+# cfd_exchange_fn / cfd_allgather_fn (include/cfd2_amd.h)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_void_p),
+                          C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64))
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+
+
 def _bind():
     global _bound
     if _bound:
@@ -60,6 +66,9 @@ def _bind():
     L.cfd_dist_unique_id.argtypes = [u8p]
     L.cfd_solver_create_dist.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
                                          C.c_int32, C.c_int32, u8p, C.POINTER(_vp)]
+    L.cfd_solver_create_dist_host.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
+                                              C.c_int32, C.c_int32, EXCHANGE_FN, ALLGATHER_FN, _vp,
+                                              C.POINTER(_vp)]
     L.cfd_group_create.argtypes = [C.POINTER(_ffi.MeshView), C.POINTER(_ffi.Config), C.c_int32,
                                    C.POINTER(C.c_int32), C.POINTER(_vp)]
     L.cfd_group_step.argtypes = [C.POINTER(_vp), C.c_int32]
@@ -112,6 +121,58 @@ class GpuSolver:
         _ffi.check(L.cfd_solver_create_dist(C.byref(view), C.byref(cfg), int(device), int(nranks), int(rank),
                                             uid, C.byref(h)), "cfd_solver_create_dist")
         return cls(mesh, config=cfg, _handle=h)
+
+    @classmethod
+    def create_dist_host(cls, mesh, nranks: int, rank: int, device: int = 0,
+                         config: _ffi.Config | None = None, **cfg_overrides):
+        """One rank of the distributed solver over the host-staged transport
+        (test / rehearsal mode: torch.distributed's process group -- gloo --
+        carries every halo and all-gather; several ranks may share one GPU).
+        torch.distributed must be initialised.  Collective."""
+        import torch
+        import torch.distributed as dist
+        L = _bind()
+        cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
+        view = mesh.view()
+
+        def buf(addr, nbytes):
+            return torch.frombuffer((C.c_uint8 * int(nbytes)).from_address(addr), dtype=torch.uint8)
+
+        def exchange(_user, n, peer, send, sbytes, recv, rbytes):
+            try:
+                reqs, ks, kr = [], {}, {}
+                for i in range(n):
+                    q = int(peer[i])
+                    if sbytes[i]:
+                        reqs.append(dist.isend(buf(send[i], sbytes[i]), q, tag=ks.setdefault(q, 0)))
+                        ks[q] += 1
+                    if rbytes[i]:
+                        reqs.append(dist.irecv(buf(recv[i], rbytes[i]), q, tag=kr.setdefault(q, 0)))
+                        kr[q] += 1
+                for r in reqs:
+                    r.wait()
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the status code
+                print("cfd2 host transport exchange failed:", e, flush=True)
+                return 1
+
+        def allgather(_user, send, recv, nbytes):
+            try:
+                out = [buf(recv + r * nbytes, nbytes) for r in range(nranks)] if nbytes else None
+                if nbytes:
+                    dist.all_gather(out, buf(send, nbytes).clone())
+                return 0
+            except Exception as e:  # noqa: BLE001
+                print("cfd2 host transport allgather failed:", e, flush=True)
+                return 1
+
+        ex_cb, ag_cb = EXCHANGE_FN(exchange), ALLGATHER_FN(allgather)
+        h = _vp()
+        _ffi.check(L.cfd_solver_create_dist_host(C.byref(view), C.byref(cfg), int(device), int(nranks), int(rank),
+                                                 ex_cb, ag_cb, None, C.byref(h)), "cfd_solver_create_dist_host")
+        s = cls(mesh, config=cfg, _handle=h)
+        s._transport = (ex_cb, ag_cb)  # the callbacks must outlive the handle
+        return s
 
     def close(self):
         h = getattr(self, "_h", None)

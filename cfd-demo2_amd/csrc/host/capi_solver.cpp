@@ -259,6 +259,27 @@ cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* c
   return CFD_OK;
 }
 
+cfd_status cfd_solver_create_dist_host(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
+                                       int32_t nranks, int32_t rank, cfd_exchange_fn exchange,
+                                       cfd_allgather_fn allgather, void* user, cfd_solver** out) {
+  if (!mesh || !out || !exchange || !allgather) return set_error(CFD_ERR_INVALID, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(CFD_ERR_INVALID, "bad rank / nranks");
+  cfd_config c;
+  if (cfg)
+    c = *cfg;
+  else
+    cfd_config_default(&c);
+  cfd2::Solver* sp = nullptr;
+  const cfd_status st = guard([&] {
+    CFD_HIP(hipSetDevice(hip_device));
+    auto comm = cfd2::make_host_comm(nranks, rank, exchange, allgather, user);
+    sp = new cfd2::Solver(*mesh, c, hip_device, std::move(comm));
+  });
+  if (st != CFD_OK) return st;
+  *out = new cfd_solver{sp};
+  return CFD_OK;
+}
+
 cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t nranks,
                             const int32_t* devices, cfd_solver** out) {
   if (!mesh || !out || !devices || nranks < 1) return set_error(CFD_ERR_INVALID, "bad argument");

@@ -73,6 +73,62 @@ std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUn
   return std::make_unique<RcclComm>(nranks, rank, uid);
 }
 
+// ------------------------------------------------------ host-staged callbacks
+namespace {
+
+// Every transfer goes device -> host staging -> caller callback -> host
+// staging -> device, after the stream has drained (test transport only).
+class HostComm final : public Comm {
+ public:
+  HostComm(int nranks, int r, HostExchangeFn ex, HostAllgatherFn ag, void* user)
+      : ex_(ex), ag_(ag), user_(user) {
+    rank = r;
+    size = nranks;
+  }
+  void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    if (msgs.empty()) return;
+    CFD_HIP(hipStreamSynchronize(s));
+    const size_t n = msgs.size();
+    std::vector<std::vector<char>> sb(n), rb(n);
+    std::vector<int32_t> peer(n);
+    std::vector<void*> sp(n), rp(n);
+    std::vector<uint64_t> sn(n), rn(n);
+    for (size_t i = 0; i < n; ++i) {
+      const Msg& m = msgs[i];
+      peer[i] = m.peer;
+      sb[i].resize(m.sbytes + 1);
+      rb[i].resize(m.rbytes + 1);
+      if (m.sbytes) CFD_HIP(hipMemcpy(sb[i].data(), m.sbuf, m.sbytes, hipMemcpyDeviceToHost));
+      sp[i] = sb[i].data();
+      rp[i] = rb[i].data();
+      sn[i] = m.sbytes;
+      rn[i] = m.rbytes;
+    }
+    if (ex_(user_, (int32_t)n, peer.data(), sp.data(), sn.data(), rp.data(), rn.data()) != 0)
+      throw std::runtime_error("host transport: exchange callback failed");
+    for (size_t i = 0; i < n; ++i)
+      if (msgs[i].rbytes) CFD_HIP(hipMemcpy(msgs[i].rbuf, rb[i].data(), msgs[i].rbytes, hipMemcpyHostToDevice));
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    CFD_HIP(hipStreamSynchronize(s));
+    std::vector<char> sb(bytes + 1), rb((size_t)size * bytes + 1);
+    if (bytes) CFD_HIP(hipMemcpy(sb.data(), send, bytes, hipMemcpyDeviceToHost));
+    if (ag_(user_, sb.data(), rb.data(), bytes) != 0) throw std::runtime_error("host transport: allgather callback failed");
+    if (bytes) CFD_HIP(hipMemcpy(recv, rb.data(), (size_t)size * bytes, hipMemcpyHostToDevice));
+  }
+
+ private:
+  HostExchangeFn ex_;
+  HostAllgatherFn ag_;
+  void* user_;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_host_comm(int nranks, int rank, HostExchangeFn ex, HostAllgatherFn ag, void* user) {
+  return std::make_unique<HostComm>(nranks, rank, ex, ag, user);
+}
+
 // ----------------------------------------------------------- local group
 LocalGroup::LocalGroup(int n) : slots(n), n_(n) {}
 

@@ -54,6 +54,12 @@ constexpr int kUniqueIdBytes = 128;
 void rccl_unique_id(uint8_t out[kUniqueIdBytes]);
 std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUniqueIdBytes]);
 
+// ---- host-staged callbacks (test transport, cfd_solver_create_dist_host) ----
+using HostExchangeFn = int32_t (*)(void* user, int32_t n, const int32_t* peer, void* const* send,
+                                   const uint64_t* send_bytes, void* const* recv, const uint64_t* recv_bytes);
+using HostAllgatherFn = int32_t (*)(void* user, void* send, void* recv, uint64_t bytes);
+std::unique_ptr<Comm> make_host_comm(int nranks, int rank, HostExchangeFn ex, HostAllgatherFn ag, void* user);
+
 // ---- in-process group ----
 class LocalGroup {
  public:

@@ -226,6 +226,20 @@ cfd_status cfd_dist_unique_id(uint8_t out[128]);
 cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg,
                                   int32_t hip_device, int32_t nranks, int32_t rank,
                                   const uint8_t unique_id[128], cfd_solver** out);
+/* Host-staged transport (test / rehearsal mode, e.g. several processes on
+ * ONE GPU, where RCCL refuses a second rank per device): the same
+ * distributed solver, with every halo exchange and all-gather staged through
+ * host memory and handed to caller callbacks (bench.py binds them to
+ * torch.distributed's gloo backend).  exchange: transfers with the same peer
+ * match in list order, send k of one rank with receive k of the other;
+ * allgather: recv[r * bytes ...] = rank r's send.  Callbacks return 0 on
+ * success.  Not a performance path.                                          */
+typedef int32_t (*cfd_exchange_fn)(void* user, int32_t n, const int32_t* peer, void* const* send,
+                                   const uint64_t* send_bytes, void* const* recv, const uint64_t* recv_bytes);
+typedef int32_t (*cfd_allgather_fn)(void* user, void* send, void* recv, uint64_t bytes);
+cfd_status cfd_solver_create_dist_host(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
+                                       int32_t nranks, int32_t rank, cfd_exchange_fn exchange,
+                                       cfd_allgather_fn allgather, void* user, cfd_solver** out);
 /* In-process group (SURVEY §8(b) `cfd_solver_create_dist(..., nranks,
  * devices)`): nranks handles in this process, rank r on devices[r] (devices
  * may repeat: all ranks on one GPU is allowed).  Collective calls go through

@@ -1,0 +1,40 @@
+"""Worker of tests/test_gpu_multiproc.py: one rank (one process) of the
+distributed solver over the host-staged gloo transport, all ranks on GPU 0.
+Launched by torch.distributed.run; writes its owned fields to <out>/rank<r>.npz."""
+import os
+import sys
+
+import numpy as np
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "cfd-demo2_amd"))
+
+from cfd2_amd import GpuSolver  # noqa: E402
+from tests.meshes import backwards_step  # noqa: E402
+from tests.test_gpu_parity import _setup_amg_test  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    steps = int(sys.argv[2])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    mesh = backwards_step()
+    s = GpuSolver.create_dist_host(mesh, world, rank, device=0)
+    _setup_amg_test(s, mesh, 1)
+    for _ in range(steps):
+        s.step()
+    c0, c1 = s.owned
+    info = s.step_info()
+    np.savez(os.path.join(out, f"rank{rank}.npz"), c0=c0, c1=c1, u=s.get_u(), p=s.get_p(), d_p=s.get_d_p(),
+             outer_iterations=info.outer_iterations, linear=info.total_linear_iterations,
+             res_u=info.outer_residual_u, res_p=info.outer_residual_p)
+    s.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
