@@ -1136,19 +1136,20 @@ __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uin
 #endif
 constexpr int kU = CFD_AMG_U;
 
-// FULL levels (rows nearly as long as the ELL width, e.g. level 0 of a quad
-// mesh): slot loads unconditional, clamped to rmax, and the first group
-// peeled so its loads do not wait for the row lengths.  Other levels predicate
-// each slot load on the thread's longest row, which avoids reading the padding
-// of short rows.
-template <bool D16, bool FULL, bool ALWAYS = false>
+// MODE 1 (level 0 of a quad mesh, small latency-bound levels): slot loads
+// unconditional, clamped to rmax, the first group peeled so its loads do not
+// wait for the row lengths, gathers unconditional (vector gathers).  MODE 2:
+// the same loads, gathers predicated on the row lengths (coarse levels: their
+// columns are not consecutive).  MODE 0: every slot load predicated on the
+// thread's longest row (avoids reading the padding of short rows).
+template <bool D16, int MODE, bool ALWAYS = false>
 __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln,
                                              float4 v[kU], float xg[kU][4]) {
   int c[kU][4];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
-    if (FULL || r0 + u <= rmax) {
+    if (MODE != 0 || r0 + u <= rmax) {
       const size_t off = (size_t)min(r0 + u, rmax) * L.stride + i0;
       v[u] = *reinterpret_cast<const float4*>(L.val + off);
       load_cols4<D16>(L, off, i0, c[u]);
@@ -1158,7 +1159,7 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       for (int k = 0; k < 4; ++k) c[u][k] = (int)i0 + k;
     }
   }
-  if constexpr (ALWAYS && FULL && CFD_VGATHER) {
+  if constexpr (ALWAYS && MODE == 1 && CFD_VGATHER) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const f4u q = ld4u(x + c[u][0]);
@@ -1177,12 +1178,12 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && FULL>(r0 + u < u4(ln, k), x + c[u][k]);
+      for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && MODE == 1>(r0 + u < u4(ln, k), x + c[u][k]);
   }
 }
 
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
-template <bool D16, bool FULL>
+template <bool D16, int MODE>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
@@ -1194,14 +1195,14 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
   auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16, FULL, true>(L, x, i0, r0, rmax, ln, v, xg);
+    gather_group<D16, MODE, true>(L, x, i0, r0, rmax, ln, v, xg);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (r0 + u < u4(ln, k)) sg[k] += f4(v[u], k) * xg[u][k];
   };
-  if constexpr (FULL) {
+  if constexpr (MODE != 0) {
     // first slot group peeled: its loads (clamped to the ELL width) do not wait for the lengths
     step(0, (uint32_t)max(L.w, 1) - 1u);
     for (uint32_t r0 = kU; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
@@ -1242,7 +1243,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
 #endif
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
-template <bool D16, bool FULL>
+template <bool D16, int MODE>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
@@ -1257,7 +1258,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
   auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16, FULL, CFD_RESID_GATHER_ALWAYS>(L, x, i0, r0, rmax, ln, v, xg);
+    gather_group<D16, MODE, CFD_RESID_GATHER_ALWAYS>(L, x, i0, r0, rmax, ln, v, xg);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -1268,7 +1269,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
       }
   };
   uint32_t r0 = 0;
-  if constexpr (FULL) {
+  if constexpr (MODE != 0) {
     step(0, (uint32_t)max(L.w, 1) - 1u);  // peeled first group (see k_amg_smooth)
     r0 = kU;
   }
@@ -1297,8 +1298,22 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
                                                          const float* __restrict__ sm_de) {
   const uint32_t I = row_id();
   if (I < L.nc) {
+    // members fetched 4 at a time (indices clamped to the row's last member,
+    // unused values skipped): one round trip for the indices and one for the
+    // values per 4 members instead of one dependent pair per member
     float sum = 0.0f;
-    for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
+    const uint32_t k0 = L.r_row[I], k1 = L.r_row[I + 1];
+    for (uint32_t k = k0; k < k1; k += 4) {
+      uint32_t f[4];
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = L.r_col[min(k + q, k1 - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = r[f[q]];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k + q < k1) sum += 1.0f * v[q];
+    }
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
       sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
@@ -1837,9 +1852,10 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
                      hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
-// instance for a level: 16/32-bit columns x FULL (see gather_group)
-#define CFD_AMG_INSTANCE(kern, L) \
-  ((L).use16 ? ((L).full ? kern<true, true> : kern<true, false>) : ((L).full ? kern<false, true> : kern<false, false>))
+// instance for a level: 16/32-bit columns x load mode (see gather_group)
+#define CFD_AMG_INSTANCE(kern, L)                                                                            \
+  ((L).use16 ? ((L).full == 1 ? kern<true, 1> : (L).full == 2 ? kern<true, 2> : kern<true, 0>)              \
+             : ((L).full == 1 ? kern<false, 1> : (L).full == 2 ? kern<false, 2> : kern<false, 0>))
 
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
                        hipEvent_t ev0, hipEvent_t ev1) {
