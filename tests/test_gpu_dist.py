@@ -104,14 +104,17 @@ def test_rccl_transport_selftest():
     rccl_selftest(0)
 
 
-def test_group_c1_scale(replicate_rows):
-    """BASELINE configs[1] scale (~1M cells) on 4 in-process ranks, default
-    replication threshold: one real fixed-schedule step bit-exact vs oracle(4)."""
-    replicate_rows(262144)
+@pytest.mark.parametrize("nranks,rep", [(4, 262144), (8, 262144), (8, 4096)])
+def test_group_c1_scale(nranks, rep, replicate_rows):
+    """BASELINE configs[1] scale (~1M cells) on 4 and 8 in-process ranks (the
+    driver's 8-GPU rank count; rep 4096 keeps five levels distributed down to a
+    few hundred rows per rank): one real fixed-schedule step bit-exact vs
+    oracle(R)."""
+    replicate_rows(rep)
     mesh = bench_mesh(0.001723, 100)
     cfg = dict(fixed_outer=1, fixed_inner=6)
-    g = GpuGroup(mesh, 4, config=default_config(**cfg))
-    o = OracleSolver(mesh, config=default_config(**cfg), nranks=4)
+    g = GpuGroup(mesh, nranks, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
     for s in (g, o):
         s.set_dt(1e-3)
         s.set_viscosity(0.01)
@@ -123,8 +126,8 @@ def test_group_c1_scale(replicate_rows):
     for k in range(2):
         g.step()
         o.step()
-        _assert_same_fields(g, o, f"C1 R=4 step {k}")
-        _assert_same_info(g, o, f"C1 R=4 step {k}")
+        _assert_same_fields(g, o, f"C1 R={nranks} step {k}")
+        _assert_same_info(g, o, f"C1 R={nranks} step {k}")
     g.close()
 
 
