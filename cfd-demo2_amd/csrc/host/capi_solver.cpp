@@ -182,6 +182,7 @@ cfd_status cfd_profile_reset(cfd_solver* s) {
     s->s->prof_used = 0;
     s->s->prof_ms = 0.0;
     s->s->prof_launches = 0;
+    s->s->prof_grow(8192);  // 4096 timed launches without growing inside the timed steps
   });
 }
 cfd_status cfd_profile_smoother(const cfd_solver* cs, double* total_ms, uint64_t* launches,

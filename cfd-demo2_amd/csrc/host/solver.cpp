@@ -837,28 +837,35 @@ void Solver::build_tail_blob(int tf) {
   tail_blob_first = tf;
 }
 
-// HIP events around level-0 smoother launches (bench roofline); the pool is
-// drained into prof_ms when full.
 // Timing of level-0 smoother launches (bench roofline): a pair of pool events
-// per launch, recorded by the GPU at kernel start / end (hipExtLaunchKernel);
-// the pool is drained into prof_ms when full.
+// per launch, recorded by the GPU at kernel start / end (hipExtLaunchKernel).
+// The pool is created before the timed steps (cfd_profile_reset) and grows
+// without synchronising; only at kProfPoolMax events is it drained (a stream
+// synchronisation) into prof_ms.
 std::pair<hipEvent_t, hipEvent_t> Solver::prof_pair() {
   if (prof_used + 2 > prof_ev.size()) {
-    CFD_HIP(hipStreamSynchronize(stream));
-    for (size_t k = 0; k + 1 < prof_used; k += 2) {
-      float ms = 0.0f;
-      CFD_HIP(hipEventElapsedTime(&ms, prof_ev[k], prof_ev[k + 1]));
-      prof_ms += ms;
-    }
-    prof_used = 0;
-    while (prof_ev.size() < 512) {
-      hipEvent_t e;
-      CFD_HIP(hipEventCreate(&e));
-      prof_ev.push_back(e);
+    if (prof_ev.size() < kProfPoolMax) {
+      prof_grow(prof_ev.size() + 1024);  // no synchronisation inside the timed steps
+    } else {
+      CFD_HIP(hipStreamSynchronize(stream));
+      for (size_t k = 0; k + 1 < prof_used; k += 2) {
+        float ms = 0.0f;
+        CFD_HIP(hipEventElapsedTime(&ms, prof_ev[k], prof_ev[k + 1]));
+        prof_ms += ms;
+      }
+      prof_used = 0;
     }
   }
   prof_used += 2;
   return {prof_ev[prof_used - 2], prof_ev[prof_used - 1]};
+}
+
+void Solver::prof_grow(size_t n) {
+  while (prof_ev.size() < n) {
+    hipEvent_t e;
+    CFD_HIP(hipEventCreate(&e));
+    prof_ev.push_back(e);
+  }
 }
 
 void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {

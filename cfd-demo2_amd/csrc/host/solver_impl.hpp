@@ -293,6 +293,10 @@ struct Solver {
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);
   std::pair<hipEvent_t, hipEvent_t> prof_pair();
+ public:
+  static constexpr size_t kProfPoolMax = 1u << 15;
+  void prof_grow(size_t n);  // event pool of at least n events
+ private:
   float norm_blocking(const float* v, int mode, int slot);
   float residual_into_v0_blocking();
   void check_evolution();
