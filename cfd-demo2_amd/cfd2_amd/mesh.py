@@ -7,6 +7,7 @@ Arrays are exposed as zero-copy numpy views of the native mesh.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -175,3 +176,71 @@ def bench_channel(h: float, smooth_iters: int = 100) -> Mesh:
     if smooth_iters > 0:
         m.smooth(geo, 0.3, smooth_iters)
     return m
+
+
+# ---------------------------------------------------------------------------
+# Shared mesh file for one-process-per-GPU runs: rank 0 writes the SoA arrays
+# of the mesh view once (page-aligned raw arrays + a JSON header) and every
+# rank maps them read-only, so the ranks share ONE copy in the page cache
+# instead of each holding (and generating) the whole mesh.  Only the fields
+# of cfd_mesh_view are stored (what cfd_solver_create_dist reads).
+_VIEW_FIELDS = [  # (name, dtype, length: "F" faces, "N" cells, "N1" cells + 1, "S" cell-face entries)
+    ("face_owner", np.uint32, "F"), ("face_neighbor", np.uint32, "F"), ("face_boundary", np.uint32, "F"),
+    ("face_area", np.float64, "F"), ("face_nx", np.float64, "F"), ("face_ny", np.float64, "F"),
+    ("face_cx", np.float64, "F"), ("face_cy", np.float64, "F"),
+    ("cell_cx", np.float64, "N"), ("cell_cy", np.float64, "N"), ("cell_vol", np.float64, "N"),
+    ("cell_face_offsets", np.uint32, "N1"), ("cell_faces", np.uint32, "S"),
+]
+_PAGE = 4096
+
+
+def save_view_file(mesh: "Mesh", path: str) -> None:
+    import json
+    a = mesh.arrays()
+    n, f = mesh.num_cells(), mesh.num_faces()
+    s = int(a["cell_face_offsets"][-1])
+    lens = {"F": f, "N": n, "N1": n + 1, "S": s}
+    hdr, off = {"num_cells": n, "num_faces": f, "arrays": {}}, _PAGE
+    for name, dt, ln in _VIEW_FIELDS:
+        nbytes = lens[ln] * np.dtype(dt).itemsize
+        hdr["arrays"][name] = [off, lens[ln], np.dtype(dt).str]
+        off += (nbytes + _PAGE - 1) // _PAGE * _PAGE
+    raw = json.dumps(hdr).encode()
+    assert len(raw) < _PAGE
+    with open(path + ".tmp", "wb") as fh:
+        fh.write(raw)
+        for name, _, _ in _VIEW_FIELDS:
+            fh.seek(hdr["arrays"][name][0])
+            np.ascontiguousarray(a[name]).tofile(fh)
+        fh.truncate(off)
+    os.replace(path + ".tmp", path)  # readers never see a partial file
+
+
+class MappedMesh:
+    """A mesh view backed by a file of save_view_file (read-only memory map):
+    what GpuSolver.create_dist / create_dist_host need (view, sizes)."""
+
+    def __init__(self, path: str):
+        import json
+        with open(path, "rb") as fh:
+            hdr = json.loads(fh.read(_PAGE).split(b"\0", 1)[0].decode())
+        self._n, self._f = int(hdr["num_cells"]), int(hdr["num_faces"])
+        self._a = {name: np.memmap(path, dtype=np.dtype(dt), mode="r", offset=off, shape=(ln,))
+                   for name, (off, ln, dt) in hdr["arrays"].items()}
+
+    def num_cells(self) -> int:
+        return self._n
+
+    def num_faces(self) -> int:
+        return self._f
+
+    def arrays(self) -> dict:
+        return dict(self._a)
+
+    def view(self) -> _ffi.MeshView:
+        v = _ffi.MeshView()
+        v.num_cells, v.num_faces = self._n, self._f
+        for name, dt, _ in _VIEW_FIELDS:
+            ct = C.c_uint32 if dt == np.uint32 else C.c_double
+            setattr(v, name, self._a[name].ctypes.data_as(C.POINTER(ct)))
+        return v

@@ -108,3 +108,22 @@ def test_save_load_roundtrip():
         for k in a:
             assert np.array_equal(a[k], b[k]), k
         assert m2.calculate_max_skewness() == m.calculate_max_skewness()
+
+
+def test_shared_view_file_round_trip(tmp_path):
+    """bench.py --gpus N: rank 0 writes the mesh view once, every rank maps it
+    (cfd2_amd.mesh.save_view_file / MappedMesh); the mapped view must hold
+    exactly the generated arrays."""
+    import numpy as np
+    from cfd2_amd.mesh import MappedMesh, bench_channel, save_view_file
+    m = bench_channel(0.02, 20)
+    p = str(tmp_path / "mesh.bin")
+    save_view_file(m, p)
+    mm = MappedMesh(p)
+    assert (mm.num_cells(), mm.num_faces()) == (m.num_cells(), m.num_faces())
+    a, b = m.arrays(), mm.arrays()
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    v = mm.view()
+    assert v.num_cells == m.num_cells() and v.num_faces == m.num_faces()
+    assert v.cell_vol[0] == a["cell_vol"][0] and v.cell_faces[5] == a["cell_faces"][5]
