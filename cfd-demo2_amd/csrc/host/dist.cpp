@@ -1,6 +1,7 @@
 #include "dist.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace cfd2 {
@@ -70,9 +71,17 @@ HaloPlan build_halo_plan(const std::vector<uint64_t>& starts, int rank, const ui
     h.recv_cnt = rc;
     h.send_off = (uint32_t)P.send_idx.size();
     h.send_cnt = (uint32_t)send[q].size();
+    const auto& v = send[q];
+    bool run = true;
+    for (size_t t = 1; t < v.size() && run; ++t) run = v[t] == v[0] + (int32_t)t;
+    h.direct = v.empty() ? 0 : (run ? v[0] : -1);
     P.send_idx.insert(P.send_idx.end(), send[q].begin(), send[q].end());
     P.peers.push_back(h);
   }
+  P.all_direct = true;
+  for (const HaloPeer& h : P.peers) P.all_direct = P.all_direct && h.direct >= 0;
+  if (const char* e = std::getenv("CFD_HALO_PACK"))  // 1: always pack (A/B, tests)
+    if (e[0] == '1') P.all_direct = false;
   return P;
 }
 

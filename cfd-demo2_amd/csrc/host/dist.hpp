@@ -21,6 +21,7 @@ struct HaloPeer {
   uint32_t recv_cnt = 0;
   uint32_t send_off = 0;  // into HaloPlan::send_idx
   uint32_t send_cnt = 0;
+  int32_t direct = -1;    // the rows sent are the contiguous run [direct, direct + send_cnt) (else -1)
 };
 
 struct HaloPlan {
@@ -29,6 +30,9 @@ struct HaloPlan {
   int32_t* d_send_idx = nullptr;
   float* d_stage = nullptr;       // pack buffer (send_idx.size() x max comps)
   int max_comps = 0;
+  // every peer's send rows are one contiguous run (x-major slabs: the first /
+  // last columns of cells): fields are sent straight from their rows, no pack
+  bool all_direct = false;
   // rows reading ghosts: [0, lo_end) (lower ghosts) and [hi_begin, n) (upper);
   // the rows between are interior and overlap the exchange (multiples of 4)
   uint32_t lo_end = 0, hi_begin = 0;

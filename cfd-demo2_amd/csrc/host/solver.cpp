@@ -68,6 +68,8 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   CFD_HIP(hipSetDevice(device));
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
+    const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
+    if (oe) overlap_min_rows = (uint32_t)std::strtoul(oe, nullptr, 10);
     CFD_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     CFD_HIP(hipEventCreateWithFlags(&hev_pack, hipEventDisableTiming));
     CFD_HIP(hipEventCreateWithFlags(&hev_done, hipEventDisableTiming));
@@ -293,14 +295,15 @@ void Solver::halo_begin(HaloPlan& plan, std::initializer_list<HField> fields) {
   pa.idx = plan.d_send_idx;
   pa.n = ns;
   pa.stage = plan.d_stage;
-  launch_pack(pa, stream);
+  if (!plan.all_direct) launch_pack(pa, stream);
   std::vector<Msg> msgs;
   for (const HaloPeer& h : plan.peers) {
     for (int f = 0; f < pa.nf; ++f) {
       const PackField& F = pa.f[f];
       Msg mm;
       mm.peer = h.rank;
-      mm.sbuf = plan.d_stage + F.stage_off + (size_t)h.send_off * F.comps;
+      mm.sbuf = plan.all_direct ? F.src + (ptrdiff_t)h.direct * F.comps
+                                : plan.d_stage + F.stage_off + (size_t)h.send_off * F.comps;
       mm.sbytes = (size_t)h.send_cnt * F.comps * sizeof(float);
       mm.rbuf = const_cast<float*>(F.src) + (ptrdiff_t)h.recv_rel * F.comps;
       mm.rbytes = (size_t)h.recv_cnt * F.comps * sizeof(float);

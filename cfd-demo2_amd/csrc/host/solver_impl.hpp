@@ -319,10 +319,19 @@ struct Solver {
   void halo_begin(HaloPlan& plan, std::initializer_list<HField> fields);
   void halo_end();
   // launch(r0, r1) over rows [0, n): interior rows overlap the halo exchange,
-  // boundary rows run after it (one GPU: a single launch over all rows)
+  // boundary rows run after it (one GPU: a single launch over all rows).  Below
+  // overlap_min_rows the interior launch is too short to hide an exchange and
+  // the split only triples the launches of a latency-bound kernel: one launch
+  // after the exchange.
+  uint32_t overlap_min_rows = 1u << 20;
   template <class F>
   void overlapped(HaloPlan& plan, std::initializer_list<HField> fields, uint32_t n, F&& launch) {
     if (!dist()) {
+      launch(0u, n);
+      return;
+    }
+    if (n < overlap_min_rows) {
+      halo(plan, fields);
       launch(0u, n);
       return;
     }
