@@ -52,6 +52,23 @@ __device__ __forceinline__ uint32_t xcd_block() {
 }
 __device__ __forceinline__ uint32_t row_id() { return xcd_block() * kBlock + threadIdx.x; }
 
+// First row of this thread's 4 in a launch over [r0, r1) and [r2, r3) (the
+// second range lets a distributed rank process both boundary strips of a
+// halo'd kernel in one launch); false: no rows for this thread.
+__device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
+  const uint32_t t = row_id(), na = (r1 - r0 + 3) / 4;
+  if (t < na) {
+    i0 = r0 + 4 * t;
+    return i0 < r1;
+  }
+  i0 = r2 + 4 * (t - na);
+  return i0 < r3;
+}
+inline unsigned rows2_grid(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) {
+  const size_t t = (size_t)(r1 - r0 + 3) / 4 + (r3 > r2 ? (size_t)(r3 - r2 + 3) / 4 : 0);
+  return (unsigned)((t + 255) / 256);
+}
+
 // Halving tree over 256 per-thread values (canonical order): levels 128 and 64
 // through LDS, levels 32..1 by wavefront shuffles in wave 0.  Result valid in
 // thread 0.  `lds` must hold 256 floats; caller syncs before reusing it.
@@ -653,8 +670,8 @@ template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
                                                  float* __restrict__ y) {
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
-  const uint32_t i0 = A.r0 + 4 * row_id();
-  if (i0 >= A.r1) return;
+  uint32_t i0;
+  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
   float2 d2[4];
@@ -912,8 +929,8 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
                                                             float* temp_p, float* p_sol,
                                                             float* p_prev) {
   constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
-  const uint32_t i0 = A.r0 + 4 * row_id();
-  if (i0 >= A.r1) return;
+  uint32_t i0;
+  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const float sc = binv[jv];
   float wo[12];
   load12(w_in + 3 * (size_t)i0, wo);
@@ -1014,8 +1031,8 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
                                                             const float* __restrict__ dinv_uv,
                                                             float* __restrict__ z) {
   constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
-  const uint32_t i0 = A.r0 + 4 * row_id();
-  if (i0 >= A.r1) return;
+  uint32_t i0;
+  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1187,8 +1204,8 @@ template <bool D16, int MODE>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
-  const uint32_t i0 = L.r0 + 4 * row_id();
-  if (i0 >= L.r1) return;
+  uint32_t i0;
+  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -1247,8 +1264,8 @@ template <bool D16, int MODE>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
-  const uint32_t i0 = L.r0 + 4 * row_id();
-  if (i0 >= L.r1) return;
+  uint32_t i0;
+  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
@@ -1791,8 +1808,8 @@ void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, 
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
 }
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
-  if (A.r1 <= A.r0) return;
-  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
+  if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
+  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_spmv<true>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
   else
@@ -1820,8 +1837,8 @@ void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int 
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s) {
-  if (A.r1 <= A.r0) return;
-  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
+  if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
+  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_predict<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
                        temp_p, p_sol, p_prev);
@@ -1838,8 +1855,8 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
 }
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
-  if (A.r1 <= A.r0) return;
-  const unsigned nb = grid_for((A.r1 - A.r0 + 3) / 4);
+  if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
+  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_correct<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
   else
@@ -1859,8 +1876,8 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
 
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
                        hipEvent_t ev0, hipEvent_t ev1) {
-  if (L.r1 <= L.r0) return;
-  const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
+  if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
+  const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
   auto fn = CFD_AMG_INSTANCE(k_amg_smooth, L);
   if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
     hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
@@ -1871,8 +1888,8 @@ void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, 
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
 }
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
-  if (L.r1 <= L.r0) return;
-  const unsigned nb = grid_for((L.r1 - L.r0 + 3) / 4);
+  if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
+  const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
   auto fn = CFD_AMG_INSTANCE(k_amg_residual, L);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }

@@ -109,6 +109,7 @@ struct AssembleArgs {
 struct CoupledMatrix {
   uint32_t N;
   uint32_t r0, r1;        // rows this launch processes (multiples of 4 except r1 = N)
+  uint32_t r2, r3;        // optional second row range of the same launch (empty: r3 <= r2)
   uint32_t ld;            // slot stride (N rounded up to 64)
   int ws;
   int use16;
@@ -131,6 +132,7 @@ struct CoupledMatrix {
 struct AmgLevelDev {
   uint32_t n;
   uint32_t r0, r1;       // rows a smoother / residual launch processes (default 0, n)
+  uint32_t r2, r3;       // optional second row range of the same launch (empty: r3 <= r2)
   uint32_t stride;       // row stride of the ELL slots (n rounded up to 64)
   int w;                 // ELL width (max off-diagonals per row)
   int use16;             // 1: col16 holds deltas; 0: col32 holds absolute columns

@@ -188,6 +188,7 @@ CoupledMatrix Solver::cmat() const {
   A.N = N;
   A.r0 = 0;
   A.r1 = N;
+  A.r2 = A.r3 = 0;
   A.ld = topo.ld;
   A.ws = topo.ws;
   A.use16 = topo.use16 ? 1 : 0;
@@ -907,10 +908,12 @@ void Solver::v_cycle() {
       return;
     }
     const bool timed = prof && i == 0;  // kernel time only: each part timed separately
-    overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b) {
+    overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;
       d.r1 = b;
+      d.r2 = a2;
+      d.r3 = b2;
       if (timed) {
         const auto ev = prof_pair();
         launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second);
@@ -923,16 +926,18 @@ void Solver::v_cycle() {
   };
   auto res = [&](int i) {
     AmgGpuLevel& Lv = levels[i];
-    auto f = [&](uint32_t a, uint32_t b) {
+    auto f = [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;
       d.r1 = b;
+      d.r2 = a2;
+      d.r3 = b2;
       launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream);
     };
     if (Lv.dist)
       overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, f);
     else
-      f(0, Lv.dev.n);
+      f(0, Lv.dev.n, 0, 0);
   };
   bool presmoothed = false;  // level i's zero-x pre-smoother already ran inside the restriction
   for (int i = 0; i < down; ++i) {
@@ -982,10 +987,12 @@ void Solver::precondition(int j, float* z) {
   const bool jacobi = constants.precond_type != 1;
   float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
   // the prediction reads neighbours' r_u, r_v
-  overlapped(cell_plan, {{v, 3}}, N, [&](uint32_t a, uint32_t b) {
+  overlapped(cell_plan, {{v, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix Ar = A;
     Ar.r0 = a;
     Ar.r1 = b;
+    Ar.r2 = a2;
+    Ar.r3 = b2;
     launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
   });
   bool in_sol = true;
@@ -1005,10 +1012,12 @@ void Solver::precondition(int j, float* z) {
   }
   float* ps = in_sol ? p_sol : temp;
   // the velocity correction reads neighbours' p_sol
-  overlapped(cell_plan, {{ps, 1}}, N, [&](uint32_t a, uint32_t b) {
+  overlapped(cell_plan, {{ps, 1}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix Ar = A;
     Ar.r0 = a;
     Ar.r1 = b;
+    Ar.r2 = a2;
+    Ar.r3 = b2;
     launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream);
   });
 }
@@ -1027,10 +1036,12 @@ float Solver::norm_blocking(const float* v, int mode, int slot) {
 // g = [||r||, 0, ...] (coupled_solver_fgmres.rs:1880-1890, 2380-2392).
 float Solver::residual_into_v0_blocking() {
   CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
-  overlapped(cell_plan, {{x, 3}}, N, [&](uint32_t a, uint32_t b) {
+  overlapped(cell_plan, {{x, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix A = cmat();
     A.r0 = a;
     A.r1 = b;
+    A.r2 = a2;
+    A.r3 = b2;
     launch_spmv(A, x, w, stream);
   });
   launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
@@ -1073,10 +1084,12 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       ++total;
       float* zj = zvec + (size_t)j * stride;
       precondition(j, zj);
-      overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b) {
+      overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
         CoupledMatrix A = cmat();
         A.r0 = a;
         A.r1 = b;
+        A.r2 = a2;
+        A.r3 = b2;
         launch_spmv(A, zj, w, stream);
       });
       launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);

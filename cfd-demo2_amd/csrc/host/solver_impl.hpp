@@ -318,8 +318,9 @@ struct Solver {
   // exchange on the comm stream; halo_end makes the compute stream wait for it
   void halo_begin(HaloPlan& plan, std::initializer_list<HField> fields);
   void halo_end();
-  // launch(r0, r1) over rows [0, n): interior rows overlap the halo exchange,
-  // boundary rows run after it (one GPU: a single launch over all rows).  Below
+  // launch(r0, r1, r2, r3) over rows [0, n): interior rows overlap the halo
+  // exchange, both boundary strips follow it in one launch (one GPU: a single
+  // launch over all rows).  Below
   // overlap_min_rows the interior launch is too short to hide an exchange and
   // the split only triples the launches of a latency-bound kernel: one launch
   // after the exchange.
@@ -327,20 +328,20 @@ struct Solver {
   template <class F>
   void overlapped(HaloPlan& plan, std::initializer_list<HField> fields, uint32_t n, F&& launch) {
     if (!dist()) {
-      launch(0u, n);
+      launch(0u, n, 0u, 0u);
       return;
     }
     if (n < overlap_min_rows) {
       halo(plan, fields);
-      launch(0u, n);
+      launch(0u, n, 0u, 0u);
       return;
     }
     halo_begin(plan, fields);
-    if (plan.hi_begin > plan.lo_end) launch(plan.lo_end, plan.hi_begin);
+    if (plan.hi_begin > plan.lo_end) launch(plan.lo_end, plan.hi_begin, 0u, 0u);
     halo_end();
-    if (plan.lo_end > 0) launch(0u, plan.lo_end);
+    // both boundary strips in one launch
     const uint32_t hb = plan.hi_begin > plan.lo_end ? plan.hi_begin : plan.lo_end;
-    if (n > hb) launch(hb, n);
+    if (plan.lo_end > 0 || n > hb) launch(0u, plan.lo_end, hb, n > hb ? n : hb);
   }
   hipStream_t cstream = nullptr;  // RCCL / peer-copy stream of the halo exchanges
   hipEvent_t hev_pack = nullptr, hev_done = nullptr;
