@@ -1304,6 +1304,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
   *reinterpret_cast<float4*>(rr + i0) = o;
 }
 
+#ifndef CFD_RESTRICT_M4
+#define CFD_RESTRICT_M4 1
+#endif
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
 // also clears the coarse solution (amg.rs:721-725 `clear`, fused), including
 // its ghost entries [-glo, 0) and [stride_c, stride_c + ghi) on a distributed level
@@ -1315,21 +1318,36 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
                                                          const float* __restrict__ sm_de) {
   const uint32_t I = row_id();
   if (I < L.nc) {
-    // members fetched 4 at a time (indices clamped to the row's last member,
-    // unused values skipped): one round trip for the indices and one for the
-    // values per 4 members instead of one dependent pair per member
     float sum = 0.0f;
-    const uint32_t k0 = L.r_row[I], k1 = L.r_row[I + 1];
-    for (uint32_t k = k0; k < k1; k += 4) {
-      uint32_t f[4];
+    if (CFD_RESTRICT_M4 && L.r_m4) {
+      // the first 4 members in one 16-byte load, then their values
+      const int4 m = L.r_m4[I];
+      const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
+      const int f[4] = {m.x, m.y, m.z, over ? -2 - m.w : m.w};
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) f[q] = L.r_col[min(k + q, k1 - 1)];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = r[f[q]];
+      for (int q = 0; q < 4; ++q) v[q] = r[max(f[q], 0)];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (k + q < k1) sum += 1.0f * v[q];
+        if (f[q] >= 0) sum += 1.0f * v[q];
+      if (over)  // the members after the fourth, in ascending order
+        for (uint32_t k = L.r_row[I] + 4; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
+    } else {
+      // members fetched 4 at a time (indices clamped to the row's last member,
+      // unused values skipped): one round trip for the indices and one for the
+      // values per 4 members instead of one dependent pair per member
+      const uint32_t k0 = L.r_row[I], k1 = L.r_row[I + 1];
+      for (uint32_t k = k0; k < k1; k += 4) {
+        uint32_t f[4];
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) f[q] = L.r_col[min(k + q, k1 - 1)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = r[f[q]];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (k + q < k1) sum += 1.0f * v[q];
+      }
     }
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
@@ -1949,6 +1967,16 @@ void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStrea
 }
 void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s) {
   hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kBlock), 0, s, partial, np, out5);
+}
+
+void build_r_m4(const std::vector<uint32_t>& r_row, const std::vector<uint32_t>& r_col, std::vector<int32_t>& out) {
+  const size_t nc = r_row.empty() ? 0 : r_row.size() - 1;
+  out.assign(4 * nc, -1);
+  for (size_t I = 0; I < nc; ++I) {
+    const uint32_t k0 = r_row[I], m = r_row[I + 1] - k0;
+    for (uint32_t q = 0; q < m && q < 4; ++q) out[4 * I + q] = (int32_t)r_col[k0 + q];
+    if (m > 4) out[4 * I + 3] = -2 - (int32_t)r_col[k0 + 3];  // overflow flag; member 3 = -2 - w
+  }
 }
 
 }  // namespace cfd2

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../../include/cfd2_amd.h"
 
 namespace cfd2 {
@@ -149,6 +151,10 @@ struct AmgLevelDev {
   const uint32_t* agg;     // [stride] P: fine -> coarse (padding rows -> 0, never read)
   const uint32_t* r_row;   // [nc+1] R = P^T rows (fine indices ascending)
   const uint32_t* r_col;
+  // [nc] the first 4 members of each aggregate (k_amg_restrict: one 16-byte
+  // load instead of r_row -> r_col); -1 pads, r_m4[I].w < -1 flags an
+  // aggregate with more than 4 members (the rest read through r_row / r_col)
+  const int4* r_m4;
 };
 
 // Halo pack (distributed): up to 8 fields packed per launch.
@@ -164,6 +170,9 @@ struct PackArgs {
   uint32_t n;
   float* stage;
 };
+
+// r_m4 image of R (kernels.hip k_amg_restrict)
+void build_r_m4(const std::vector<uint32_t>& r_row, const std::vector<uint32_t>& r_col, std::vector<int32_t>& out);
 
 // Levels handled by the single-workgroup V-cycle tail kernel.
 struct AmgTailLevel {

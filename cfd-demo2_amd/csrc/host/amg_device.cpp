@@ -248,6 +248,11 @@ bool Solver::build_amg_device() {
     G.dev.agg = arena.upload(aggp, stream);
     G.dev.r_row = arena.upload(r_row, stream);
     G.dev.r_col = arena.upload(r_col, stream);
+    {
+      std::vector<int32_t> m4;
+      build_r_m4(r_row, r_col, m4);
+      G.dev.r_m4 = reinterpret_cast<const int4*>(arena.upload(m4, stream));
+    }
     G.dev.nc = nagg_own;
     // Galerkin columns: global aggregate ids of every (owned or ghost) fine column
     const uint32_t* gal_agg = G.dev.agg;

@@ -682,6 +682,11 @@ void Solver::build_amg_host() {
       G.dev.agg = arena.upload(agg, stream);
       G.dev.r_row = arena.upload(r_row, stream);
       G.dev.r_col = arena.upload(r_col, stream);
+      {
+        std::vector<int32_t> m4;
+        build_r_m4(r_row, r_col, m4);
+        G.dev.r_m4 = reinterpret_cast<const int4*>(arena.upload(m4, stream));
+      }
     }
   }
 }
