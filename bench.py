@@ -159,12 +159,21 @@ def main():
         except OSError:
             base = tempfile.gettempdir()
         shared = os.path.join(base, f"cfd2_bench_mesh_{os.environ.get('MASTER_PORT', '0')}_{args.config}_{world}.bin")
+        ok = [True]
         if rank == 0:
             m0 = make_mesh()
-            save_view_file(m0, shared)
+            try:
+                save_view_file(m0, shared)
+            except OSError as e:  # no room for the shared file: every rank generates its own mesh
+                log(f"[rank 0] shared mesh file {shared} failed ({e}); generating per rank")
+                ok[0] = False
             del m0
-        dist.barrier()
-        mesh = MappedMesh(shared)
+        dist.broadcast_object_list(ok, src=0)
+        if ok[0]:
+            mesh = MappedMesh(shared)
+        else:
+            shared = None
+            mesh = make_mesh()
     else:
         mesh = make_mesh()
     n_global = mesh.num_cells()
