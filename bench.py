@@ -167,6 +167,9 @@ def main():
             except OSError as e:  # no room for the shared file: every rank generates its own mesh
                 log(f"[rank 0] shared mesh file {shared} failed ({e}); generating per rank")
                 ok[0] = False
+                for junk in (shared, shared + ".tmp"):
+                    if os.path.exists(junk):
+                        os.unlink(junk)
             del m0
         dist.broadcast_object_list(ok, src=0)
         if ok[0]:
