@@ -560,9 +560,6 @@ __device__ __forceinline__ float gat(bool on, const float* p) {
 // slower in the same-box A/B (234 -> 250 us) while the scalar-vector kernels
 // gained (level-0 smoother 84 -> 78 us, Schur predict 198 -> 185, correct
 // 166 -> 159)
-#ifndef CFD_VGATHER_SPMV
-#define CFD_VGATHER_SPMV 0
-#endif
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ f4u ld4u(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 __device__ __forceinline__ bool consec4(const int c[4]) {
@@ -610,40 +607,16 @@ __device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* 
     load2x4(A.cval_g + off, g[u]);
     ccols4<D16>(A, off, i0, c[u]);
   }
-  if constexpr (CFD_VGATHER_SPMV) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {  // 12 consecutive floats = (u, v, p) of cells c0..c0+3
-      const float* b = x + 3 * (ptrdiff_t)c[u][0];
-      const f4u q0 = ld4u(b), q1 = ld4u(b + 4), q2 = ld4u(b + 8);
-      const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+  for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) xg[u][k][t] = f[3 * k + t];
+    for (int k = 0; k < 4; ++k) {
+      const bool on = r0 + u < u4(ln, k);
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+      xg[u][k][0] = gat<true>(on, x + j);
+      xg[u][k][1] = gat<true>(on, x + j + 1);
+      xg[u][k][2] = gat<true>(on, x + j + 2);
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (!consec4(c[u])) {
-#pragma unroll
-        for (int k = 1; k < 4; ++k) {
-          const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-          xg[u][k][0] = x[j];
-          xg[u][k][1] = x[j + 1];
-          xg[u][k][2] = x[j + 2];
-        }
-      }
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool on = r0 + u < u4(ln, k);
-        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-        xg[u][k][0] = gat<true>(on, x + j);
-        xg[u][k][1] = gat<true>(on, x + j + 1);
-        xg[u][k][2] = gat<true>(on, x + j + 2);
-      }
-  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -1155,10 +1128,11 @@ constexpr int kU = CFD_AMG_U;
 
 // MODE 1 (level 0 of a quad mesh, small latency-bound levels): slot loads
 // unconditional, clamped to rmax, the first group peeled so its loads do not
-// wait for the row lengths, gathers unconditional (vector gathers).  MODE 2:
-// the same loads, gathers predicated on the row lengths (coarse levels: their
-// columns are not consecutive).  MODE 0: every slot load predicated on the
-// thread's longest row (avoids reading the padding of short rows).
+// wait for the row lengths, gathers unconditional (vector gathers).  MODE 0
+// (the big coarse levels, whose row lengths vary): every slot load predicated
+// on the thread's longest row (avoids reading the padding of short rows);
+// peeled loads with predicated gathers were slower there (A/B level 1: 62
+// vs 57 us).
 template <bool D16, int MODE, bool ALWAYS = false>
 __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln,
@@ -1888,9 +1862,8 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
   if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
 // instance for a level: 16/32-bit columns x load mode (see gather_group)
-#define CFD_AMG_INSTANCE(kern, L)                                                                            \
-  ((L).use16 ? ((L).full == 1 ? kern<true, 1> : (L).full == 2 ? kern<true, 2> : kern<true, 0>)              \
-             : ((L).full == 1 ? kern<false, 1> : (L).full == 2 ? kern<false, 2> : kern<false, 0>))
+#define CFD_AMG_INSTANCE(kern, L) \
+  ((L).use16 ? ((L).full ? kern<true, 1> : kern<true, 0>) : ((L).full ? kern<false, 1> : kern<false, 0>))
 
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
                        hipEvent_t ev0, hipEvent_t ev1) {

@@ -138,7 +138,7 @@ struct AmgLevelDev {
   uint32_t stride;       // row stride of the ELL slots (n rounded up to 64)
   int w;                 // ELL width (max off-diagonals per row)
   int use16;             // 1: col16 holds deltas; 0: col32 holds absolute columns
-  int full;              // slot-load mode of the row kernels (kernels.hip gather_group): 0, 1, 2
+  int full;              // slot-load mode of the row kernels (kernels.hip gather_group): 0 or 1
   const float* val;      // [r*stride + i]
   const int16_t* col16;  // [r*stride + i]  col - i
   const int32_t* col32;  // [r*stride + i] signed local column

@@ -529,9 +529,7 @@ std::vector<uint64_t> Solver::allgather_u64(uint64_t mine) {
 
 void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
   const char* fe = std::getenv("CFD_AMG_FULL");
-  const char* me = std::getenv("CFD_AMG_MID_MODE");  // mode of the big coarse levels
-  const int mid = me ? std::atoi(me) : 0;
-  G.dev.full = fe ? std::atoi(fe) : ((li == 0 || G.dev.n <= (1u << 19)) ? 1 : mid);
+  G.dev.full = fe ? (fe[0] == '1') : (li == 0 || G.dev.n <= (1u << 19));
 }
 
 // Host AMG setup (amg_setup.cpp): the assembled scalar matrix is downloaded,
