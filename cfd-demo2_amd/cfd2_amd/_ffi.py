@@ -99,6 +99,27 @@ class StepInfo(C.Structure):
     ]
 
 
+class StateFileHeader(C.Structure):  # cfd_state_file_header (512 bytes)
+    _fields_ = [
+        ("magic", C.c_char * 8),
+        ("version", C.c_uint32),
+        ("header_bytes", C.c_uint32),
+        ("num_cells", C.c_uint64),
+        ("num_faces", C.c_uint64),
+        ("amg_nnz", C.c_uint64),
+        ("step_index", C.c_int32),
+        ("have_prev", C.c_int32),
+        ("inner_has_last", C.c_int32),
+        ("inner_last", C.c_float),
+        ("n_variance", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("variance", (C.c_double * 2) * 10),
+        ("constants", Constants),
+        ("info", StepInfo),
+        ("reserved", C.c_uint8 * 176),
+    ]
+
+
 def default_config(**overrides) -> Config:
     cfg = Config(
         n_outer_correctors=20,
@@ -127,7 +148,8 @@ EXPORTED = [
     "cfd_set_alpha_u", "cfd_set_density", "cfd_set_scheme", "cfd_set_time_scheme",
     "cfd_set_inlet_velocity", "cfd_set_ramp_time", "cfd_set_precond_type", "cfd_update_constants",
     "cfd_initialize_history", "cfd_step", "cfd_get_u", "cfd_get_p", "cfd_get_d_p",
-    "cfd_get_step_info", "cfd_num_cells", "cfd_num_faces", "cfd_profile_enable", "cfd_profile_reset",
+    "cfd_get_step_info", "cfd_num_cells", "cfd_num_faces", "cfd_state_save", "cfd_state_load",
+    "cfd_group_state_save", "cfd_profile_enable", "cfd_profile_reset",
     "cfd_profile_smoother", "cfd_amg_levels", "cfd_step_algorithmic_bytes", "cfd_debug_buffer",
     "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_amg_info",
     "cfd_dist_unique_id", "cfd_solver_create_dist", "cfd_solver_create_dist_host", "cfd_group_create",

@@ -6,6 +6,7 @@ There is no CPU fallback: constructing a solver without a GPU raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -76,6 +77,9 @@ def _bind():
     L.cfd_dist_plan.argtypes = [C.POINTER(_ffi.MeshView), C.c_int32, C.c_int32, u32p, u32p, u32p, u32p,
                                 u32p, u32p, C.POINTER(C.c_int32), u32p, u32p, u32p]
     L.cfd_debug_rccl_selftest.argtypes = [C.c_int32]
+    L.cfd_state_save.argtypes = [_vp, C.c_char_p]
+    L.cfd_state_load.argtypes = [_vp, C.c_char_p]
+    L.cfd_group_state_save.argtypes = [C.POINTER(_vp), C.c_int32, C.c_char_p]
     _bound = True
     return L
 
@@ -297,6 +301,15 @@ class GpuSolver:
         self._call("cfd_debug_buffer", int(bid), a.ctypes.data_as(C.POINTER(C.c_float)), n)
         return a
 
+    # checkpoint / resume (cfd_state_file_header; read the file with cfd2_amd.state)
+    def save_state(self, path):
+        """Write the whole solver state to ``path`` (collective on a distributed rank)."""
+        self._call("cfd_state_save", os.fsencode(path))
+
+    def load_state(self, path):
+        """Replace the state with a saved one (before this solver's first AMG solve)."""
+        self._call("cfd_state_load", os.fsencode(path))
+
     def debug_prepare_assemble(self, assemble=True):
         self._call("cfd_debug_prepare_assemble", 1 if assemble else 0)
 
@@ -364,6 +377,14 @@ class GpuGroup:
             c0, c1 = r.owned
             out[c0:c1] = getattr(r, getter)()
         return out
+
+    def save_state(self, path):
+        _ffi.check(_bind().cfd_group_state_save(self._harr, self.nranks, os.fsencode(path)),
+                   "cfd_group_state_save")
+
+    def load_state(self, path):
+        for r in self.ranks:
+            r.load_state(path)
 
     def get_u(self): return self._gather("get_u", 2)
     def get_p(self): return self._gather("get_p", 1)

@@ -167,6 +167,16 @@ cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out) {
   *out = s->s->info;
   return CFD_OK;
 }
+cfd_status cfd_state_save(cfd_solver* s, const char* path) {
+  CHECK_S(s);
+  if (!path) return set_error(CFD_ERR_INVALID, "null path");
+  return guard([&] { s->s->save_state(path); });
+}
+cfd_status cfd_state_load(cfd_solver* s, const char* path) {
+  CHECK_S(s);
+  if (!path) return set_error(CFD_ERR_INVALID, "null path");
+  return guard([&] { s->s->load_state(path); });
+}
 uint32_t cfd_num_cells(const cfd_solver* s) { return (s && s->s) ? s->s->N : 0; }
 uint32_t cfd_num_faces(const cfd_solver* s) { return (s && s->s) ? s->s->F : 0; }
 
@@ -305,7 +315,12 @@ cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, in
   return CFD_OK;
 }
 
-cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
+}  // extern "C"
+
+namespace {
+// a collective call on every rank of an in-process group, one host thread each
+template <class F>
+cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
   if (!h || n < 1) return set_error(CFD_ERR_INVALID, "bad argument");
   for (int r = 0; r < n; ++r) CHECK_S(h[r]);
   std::vector<cfd_status> st(n, CFD_OK);
@@ -313,13 +328,25 @@ cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
   std::vector<std::thread> th;
   for (int r = 0; r < n; ++r)
     th.emplace_back([&, r] {
-      st[r] = guard([&] { h[r]->s->step(); });
+      st[r] = guard([&] { f(*h[r]->s); });
       if (st[r] != CFD_OK) msg[r] = cfd_last_error();
     });
   for (auto& t : th) t.join();
   for (int r = 0; r < n; ++r)
     if (st[r] != CFD_OK) return set_error(st[r], "rank " + std::to_string(r) + ": " + msg[r]);
   return CFD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
+  return group_run(h, n, [](cfd2::Solver& s) { s.step(); });
+}
+
+cfd_status cfd_group_state_save(cfd_solver* const* h, int32_t n, const char* path) {
+  if (!path) return set_error(CFD_ERR_INVALID, "null path");
+  return group_run(h, n, [path](cfd2::Solver& s) { s.save_state(path); });
 }
 
 // RCCL plumbing self-test on ONE GPU (RCCL refuses two ranks per device, so

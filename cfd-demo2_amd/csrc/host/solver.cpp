@@ -30,17 +30,6 @@ T* Solver::valloc(int comps) {
   return base + (size_t)shift * comps;
 }
 
-// image of a global per-cell array in this rank's local layout (owned + ghosts)
-void Solver::local_image(const double* g, int comps, std::vector<float>& out) const {
-  out.assign(vlen * comps, 0.0f);
-  auto put = [&](size_t local, uint64_t gid) {
-    for (int c = 0; c < comps; ++c) out[local * comps + c] = (float)g[gid * comps + c];
-  };
-  for (uint32_t li = 0; li < N; ++li) put(shift + li, (uint64_t)topo.c0 + li);
-  for (uint32_t k = 0; k < topo.glo; ++k) put(shift - topo.glo + k, topo.ghost[k]);
-  for (uint32_t k = 0; k < topo.ghi; ++k) put(shift + topo.npad + k, topo.ghost[topo.glo + k]);
-}
-
 void Solver::make_plan_buffers(HaloPlan& p, int max_comps) {
   p.d_send_idx = arena.upload(p.send_idx, stream);
   p.max_comps = max_comps;
@@ -533,9 +522,8 @@ void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
 }
 
 // Host AMG setup (amg_setup.cpp): the assembled scalar matrix is downloaded,
-// the whole hierarchy is built on the host and every level image uploaded.
-// Distributed solvers always take this path (partition-aware hierarchy,
-// replicated coarse levels).
+// the whole hierarchy is built on the host and every level image uploaded
+// (fallback of build_amg_device, or CFD_AMG_SETUP=host).
 void Solver::build_amg_host() {
   const size_t ld = topo.ld;
   std::vector<float> ell((size_t)topo.ws * ld);
@@ -697,12 +685,25 @@ void Solver::ensure_amg() {
   const bool device_setup = !(se && std::string(se) == "host");
   const char* how = "device";
   amg_setup_path = 2;
-  if (!(device_setup && build_amg_device())) {
-    how = "host";
-    amg_setup_path = 1;
-    levels.clear();
-    build_amg_host();
+  const size_t slots_s = (size_t)topo.ws * topo.ld;
+  if (!amg_src) amg_src = arena.alloc<float>(slots_s);
+  if (!amg_src_loaded)  // keep the source matrix for cfd_state_save
+    CFD_HIP(hipMemcpyAsync(amg_src, sval, slots_s * sizeof(float), hipMemcpyDeviceToDevice, stream));
+  // both setup paths read `sval`: point it at the source for the build
+  float* const live = sval;
+  sval = amg_src;
+  try {
+    if (!(device_setup && build_amg_device())) {
+      how = "host";
+      amg_setup_path = 1;
+      levels.clear();
+      build_amg_host();
+    }
+  } catch (...) {
+    sval = live;
+    throw;
   }
+  sval = live;
   const int L = (int)levels.size();
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");

@@ -247,6 +247,10 @@ struct Solver {
   uint32_t tail_blob_words = 0, tail_vec_floats = 0;
   void build_tail_blob(int tf);
   std::vector<AmgGpuLevel> levels;
+  // the scalar matrix (ELL image, like sval) the hierarchy was built from:
+  // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)
+  float* amg_src = nullptr;
+  bool amg_src_loaded = false;
   // host-side state
   cfd_constants constants{};
   cfd_step_info info{};
@@ -276,6 +280,9 @@ struct Solver {
   void debug_buffer(int id, float* out);
   double algorithmic_step_bytes() const;
   double smoother_bytes() const;
+  // checkpoint / resume (checkpoint.cpp, cfd_state_file_header)
+  void save_state(const char* path);  // collective on a distributed solver
+  void load_state(const char* path);
   uint64_t amg_level_digest(int li);  // FNV-1a over every byte of level li's device image
 
  private:
@@ -307,7 +314,18 @@ struct Solver {
   T* valloc(int comps);
   template <class T>
   T* vbase(T* p, int comps) const { return p - (size_t)shift * comps; }
-  void local_image(const double* global, int comps, std::vector<float>& out) const;
+  // image of a global per-cell array (f64 input or f32 checkpoint) in this
+  // rank's local layout (owned + ghosts)
+  template <class G>
+  void local_image(const G* g, int comps, std::vector<float>& out) const {
+    out.assign(vlen * comps, 0.0f);
+    auto put = [&](size_t local, uint64_t gid) {
+      for (int c = 0; c < comps; ++c) out[local * comps + c] = (float)g[gid * comps + c];
+    };
+    for (uint32_t li = 0; li < N; ++li) put(shift + li, (uint64_t)topo.c0 + li);
+    for (uint32_t k = 0; k < topo.glo; ++k) put(shift - topo.glo + k, topo.ghost[k]);
+    for (uint32_t k = 0; k < topo.ghi; ++k) put(shift + topo.npad + k, topo.ghost[topo.glo + k]);
+  }
   // distributed plumbing
   bool dist() const { return R > 1; }
   struct HField {

@@ -178,6 +178,50 @@ uint32_t cfd_num_cells(const cfd_solver* s);
 uint32_t cfd_num_faces(const cfd_solver* s);
 
 /* ------------------------------------------------------------------------ */
+/* Checkpoint / resume (the reference keeps its state only in GPU
+ * buffers, get_u/get_p being its only export).  The file holds everything a
+ * step reads from earlier steps, in f32 exactly as the device holds it, so a
+ * solver that loads it steps bit-identically to the one that saved it:
+ *   header (cfd_state_file_header, 512 bytes), then GLOBAL per-cell arrays
+ *   (cell order of the mesh, independent of the rank count):
+ *   ring slot 0, 1, 2: u f32[2N] (interleaved), p f32[N], d_p f32[N],
+ *                      grad_p f32[2N]                (FluidState x3, structs.rs)
+ *   prev (check_evolution snapshot): the same four arrays
+ *   x f32[3N]  (FGMRES solution = initial guess of the next solve)
+ *   if amg_nnz > 0: amg_rowptr u64[N+1], amg_val f32[amg_nnz] -- the scalar
+ *   pressure matrix the AMG hierarchy was built from (CSR, columns ascending;
+ *   the pattern is the mesh's), so the loader rebuilds the same hierarchy.  */
+typedef struct cfd_state_file_header {
+  char magic[8];        /* "CFD2STAT" */
+  uint32_t version;     /* 1 */
+  uint32_t header_bytes; /* 512 */
+  uint64_t num_cells;
+  uint64_t num_faces;
+  uint64_t amg_nnz;     /* 0: no AMG hierarchy built when saved */
+  int32_t step_index;   /* ring rotation (coupled_solver.rs:43-71) */
+  int32_t have_prev;
+  int32_t inner_has_last; /* FGMRES lagged residual read (async_buffer.rs) */
+  float inner_last;
+  uint32_t n_variance;  /* entries of variance[] in use (<= 10), oldest first */
+  uint32_t reserved0;
+  double variance[10][2]; /* check_evolution's (var_u, var_v) history */
+  cfd_constants constants;
+  cfd_step_info info;
+  uint8_t reserved[176];
+} cfd_state_file_header;
+
+/* Writes the state to `path`.  Distributed solver: COLLECTIVE, every rank
+ * writes its owned cells into the same file (one node: one filesystem).    */
+cfd_status cfd_state_save(cfd_solver* s, const char* path);
+/* Replaces the state with the file's (not collective: a distributed rank
+ * reads its owned cells and ghosts).  The file may come from any rank
+ * count.  The solver must not have built its AMG hierarchy yet (load into a
+ * fresh solver); the saved scalar matrix, if any, becomes the AMG source.  */
+cfd_status cfd_state_load(cfd_solver* s, const char* path);
+/* In-process group: cfd_state_save on every rank (one host thread each).   */
+cfd_status cfd_group_state_save(cfd_solver* const* handles, int32_t nranks, const char* path);
+
+/* ------------------------------------------------------------------------ */
 /* Instrumentation (replaces profiling.rs): HIP-event timing of the level-0
  * AMG smoother sweep, on the solver's own stream.                            */
 cfd_status cfd_profile_enable(cfd_solver* s, int32_t enable);

@@ -26,6 +26,8 @@ def main():
     _setup_amg_test(s, mesh, 1)
     for _ in range(steps):
         s.step()
+    if len(sys.argv) > 3:  # collective checkpoint: every process writes its rows
+        s.save_state(sys.argv[3])
     c0, c1 = s.owned
     info = s.step_info()
     np.savez(os.path.join(out, f"rank{rank}.npz"), c0=c0, c1=c1, u=s.get_u(), p=s.get_p(), d_p=s.get_d_p(),

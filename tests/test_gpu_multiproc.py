@@ -13,6 +13,7 @@ import sys
 import numpy as np
 import pytest
 
+from cfd2_amd.state import read_state
 from tests.meshes import backwards_step
 from tests.oracle_py import OracleSolver
 from tests.test_gpu_parity import _setup_amg_test
@@ -34,7 +35,7 @@ def test_multiprocess_host_transport_parity(nranks, tmp_path):
     env = dict(os.environ, CFD_AMG_REPLICATE_ROWS="50", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "tests", "mp_worker.py"), str(tmp_path), str(steps)]
+           os.path.join(ROOT, "tests", "mp_worker.py"), str(tmp_path), str(steps), str(tmp_path / "state.bin")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     mesh = backwards_step()
@@ -54,3 +55,8 @@ def test_multiprocess_host_transport_parity(nranks, tmp_path):
     assert np.array_equal(u, o.get_u())
     assert np.array_equal(p, o.get_p())
     assert np.array_equal(dp, o.get_d_p())
+    # the checkpoint the processes wrote together holds the same global fields
+    st = read_state(tmp_path / "state.bin")
+    assert np.array_equal(st.current["u"].astype(np.float64), u)
+    assert np.array_equal(st.current["p"].astype(np.float64), p)
+    assert st.amg_val is not None
