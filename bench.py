@@ -113,6 +113,9 @@ def main():
     ap.add_argument("--inproc-ranks", type=int, default=0,
                     help="test mode: run the distributed solver as R in-process ranks on GPU 0 "
                          "(not a bench line; exercises the multi-GPU code path at scale on one GPU)")
+    ap.add_argument("--amg-rebuild", type=int, default=0,
+                    help="rebuild the AMG hierarchy every K steps (opt-in deviation from the reference's "
+                         "frozen hierarchy; not the headline configuration)")
     ap.add_argument("--mesh-cache", default=None,
                     help="binary mesh file: loaded if present, else generated and saved (A/B runs)")
     args = ap.parse_args()
@@ -182,7 +185,7 @@ def main():
     n_global = mesh.num_cells()
     log(f"[rank {rank}] mesh {n_global} cells / {mesh.num_faces()} faces in {time.perf_counter() - t0:.1f}s")
 
-    cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner)
+    cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner, amg_rebuild_interval=args.amg_rebuild)
     t0 = time.perf_counter()
     # test / rehearsal mode: CFD_DIST_TRANSPORT=host stages every exchange through
     # the gloo process group (several ranks may then share one GPU: CFD_BENCH_DEVICE)
@@ -272,7 +275,9 @@ def main():
         "data": "synthetic: deterministic cut-cell channel+obstacle mesh (reference generator restated)",
         "config": {
             "workload": (f"BASELINE {cfg_label}: channel+obstacle {n_global} cells on {world} GPU(s) (~{n_cells} per GPU), "
-                         f"fixed schedule {args.outer} Picard x {args.inner} FGMRES/AMG per step"),
+                         f"fixed schedule {args.outer} Picard x {args.inner} FGMRES/AMG per step"
+                         + (f", AMG hierarchy rebuilt every {args.amg_rebuild} step(s) (opt-in deviation)"
+                            if args.amg_rebuild else "")),
             "cells_total": n_global,
             "cells_per_gpu": n_cells,
             "h": h_run,

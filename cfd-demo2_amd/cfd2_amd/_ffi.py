@@ -73,6 +73,7 @@ class Config(C.Structure):
         ("fgmres_atol", C.c_float),
         ("log_level", C.c_int32),
         ("use_graphs", C.c_int32),
+        ("amg_rebuild_interval", C.c_int32),
     ]
 
 
@@ -116,7 +117,8 @@ class StateFileHeader(C.Structure):  # cfd_state_file_header (512 bytes)
         ("variance", (C.c_double * 2) * 10),
         ("constants", Constants),
         ("info", StepInfo),
-        ("reserved", C.c_uint8 * 176),
+        ("amg_age", C.c_uint32),
+        ("reserved", C.c_uint8 * 172),
     ]
 
 
@@ -132,6 +134,7 @@ def default_config(**overrides) -> Config:
         fgmres_atol=1e-7,
         log_level=0,
         use_graphs=0,
+        amg_rebuild_interval=0,
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)

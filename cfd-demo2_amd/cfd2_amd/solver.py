@@ -307,7 +307,7 @@ class GpuSolver:
         self._call("cfd_state_save", os.fsencode(path))
 
     def load_state(self, path):
-        """Replace the state with a saved one (before this solver's first AMG solve)."""
+        """Replace the state with a saved one (drops this solver's AMG hierarchy)."""
         self._call("cfd_state_load", os.fsencode(path))
 
     def debug_prepare_assemble(self, assemble=True):

@@ -56,6 +56,7 @@ class SolverState:
     inner_has_last: bool = False
     inner_last: float = 0.0
     variance: list = field(default_factory=list)   # [(var_u, var_v)], oldest first, <= 10
+    amg_age: int = 0                                # steps since the hierarchy was built
     amg_rowptr: np.ndarray | None = None            # uint64 (N+1,) or None
     amg_val: np.ndarray | None = None               # float32 (nnz,)
 
@@ -95,7 +96,7 @@ def read_state(path) -> SolverState:
         slots=[block(f"slot{k}") for k in range(3)], prev=block("prev"),
         x=arr(off["x"], np.float32, 3 * n, (n, 3)),
         have_prev=bool(h.have_prev), inner_has_last=bool(h.inner_has_last), inner_last=float(h.inner_last),
-        variance=[(h.variance[k][0], h.variance[k][1]) for k in range(h.n_variance)],
+        variance=[(h.variance[k][0], h.variance[k][1]) for k in range(h.n_variance)], amg_age=int(h.amg_age),
         amg_rowptr=arr(off["amg_rowptr"], np.uint64, n + 1) if nnz else None,
         amg_val=arr(off["amg_val"], np.float32, nnz) if nnz else None)
 
@@ -121,6 +122,7 @@ def write_state(path, st: SolverState) -> None:
         h.variance[k][0], h.variance[k][1] = float(a), float(b)
     h.constants = st.constants
     h.info = st.info
+    h.amg_age = int(st.amg_age)
     tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "wb") as f:
         f.write(bytes(h))

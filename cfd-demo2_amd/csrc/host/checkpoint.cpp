@@ -34,6 +34,7 @@ static_assert(sizeof(cfd_state_file_header) == 512, "cfd_state_file_header layou
 static_assert(offsetof(cfd_state_file_header, variance) == 64, "cfd_state_file_header layout");
 static_assert(offsetof(cfd_state_file_header, constants) == 224, "cfd_state_file_header layout");
 static_assert(offsetof(cfd_state_file_header, info) == 280, "cfd_state_file_header layout");
+static_assert(offsetof(cfd_state_file_header, amg_age) == 336, "cfd_state_file_header layout");
 
 namespace {
 
@@ -112,6 +113,7 @@ void Solver::save_state(const char* path) {
         }
         h.constants = constants;
         h.info = info;
+        h.amg_age = amg_age;
         pwrite_all(fd, &h, sizeof(h), 0);
       }
       // owned rows of every per-cell array at their global offsets
@@ -165,8 +167,6 @@ void Solver::save_state(const char* path) {
 
 void Solver::load_state(const char* path) {
   CFD_HIP(hipSetDevice(device));
-  if (amg_built)
-    throw std::invalid_argument("state load: this solver already built its AMG hierarchy (load into a fresh solver)");
   const int fd = ::open(path, O_RDONLY);
   if (fd < 0) throw std::invalid_argument(std::string("state load: cannot open ") + path + ": " + std::strerror(errno));
   struct stat st;
@@ -241,7 +241,9 @@ void Solver::load_state(const char* path) {
     CFD_HIP(hipMemcpyAsync(amg_src, ell.data(), ell.size() * sizeof(float), hipMemcpyHostToDevice, stream));
     sync();
   }
+  if (amg_built) drop_amg();  // the saved run's hierarchy replaces this solver's
   amg_src_loaded = h.amg_nnz != 0;
+  amg_age = h.amg_age;
   step_index = (h.step_index + 2) % 3;  // rotate() advances it back to the saved slot triple
   rotate();
   have_prev = h.have_prev != 0;

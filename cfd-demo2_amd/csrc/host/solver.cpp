@@ -70,6 +70,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
     red_comb = arena.alloc<float>(m1 + 1);
     mx_gather = arena.alloc<uint32_t>(2 * (size_t)R);
     ev_gather = arena.alloc<double>(5 * (size_t)R);
+    d_u64 = arena.alloc<uint64_t>((size_t)R + 1);  // not lazily: the AMG build runs on amg_arena
     // check_evolution's stride bug reads records (i >> 2) of the global state
     ev_a = (uint64_t)topo.c0 >> 2;
     ev_b = (((uint64_t)topo.c1 - 1) >> 2) + 1;
@@ -168,6 +169,7 @@ Solver::~Solver() {
   if (hev_done) (void)hipEventDestroy(hev_done);
   comm.reset();
   arena.release();
+  amg_arena.release();
   if (cstream) (void)hipStreamDestroy(cstream);
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -677,6 +679,23 @@ void Solver::build_amg_host() {
   }
 }
 
+// Drop the hierarchy (its device memory included); the next AMG solve builds
+// a new one from the matrix of that moment (or from a loaded source).
+void Solver::drop_amg() {
+  CFD_HIP(hipSetDevice(device));
+  sync();
+  levels.clear();
+  d_tail = nullptr;
+  tail_blob_first = -1;
+  d_tail_blob = nullptr;
+  d_tail_desc = nullptr;
+  tail_blob_words = tail_vec_floats = 0;
+  amg_arena.release();
+  amg_built = false;
+  amg_setup_path = 0;
+  amg_age = 0;
+}
+
 void Solver::ensure_amg() {
   if (amg_built) return;
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
@@ -687,23 +706,31 @@ void Solver::ensure_amg() {
   amg_setup_path = 2;
   const size_t slots_s = (size_t)topo.ws * topo.ld;
   if (!amg_src) amg_src = arena.alloc<float>(slots_s);
-  if (!amg_src_loaded)  // keep the source matrix for cfd_state_save
+  const bool from_checkpoint = amg_src_loaded;  // then amg_age is the saved run's
+  if (!from_checkpoint)  // keep the source matrix for cfd_state_save
     CFD_HIP(hipMemcpyAsync(amg_src, sval, slots_s * sizeof(float), hipMemcpyDeviceToDevice, stream));
-  // both setup paths read `sval`: point it at the source for the build
+  amg_src_loaded = false;
+  // both setup paths read `sval`: point it at the source for the build; the
+  // hierarchy's allocations go to amg_arena (arena swapped for the build)
   float* const live = sval;
   sval = amg_src;
-  try {
-    if (!(device_setup && build_amg_device())) {
-      how = "host";
-      amg_setup_path = 1;
-      levels.clear();
-      build_amg_host();
+  amg_arena.release();
+  arena.swap(amg_arena);
+  struct Restore {
+    Solver* s;
+    float* live;
+    ~Restore() {
+      s->sval = live;
+      s->arena.swap(s->amg_arena);
     }
-  } catch (...) {
-    sval = live;
-    throw;
+  } restore{this, live};
+  if (!(device_setup && build_amg_device())) {
+    how = "host";
+    amg_setup_path = 1;
+    levels.clear();
+    arena.release();  // the device attempt's partial hierarchy
+    build_amg_host();
   }
-  sval = live;
   const int L = (int)levels.size();
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
@@ -728,6 +755,7 @@ void Solver::ensure_amg() {
   if (tail_lds && !(tb_env && tb_env[0] == '0')) build_tail_blob(std::max({tail_first, 1, dist() ? amg_g : 0}));
   sync();
   amg_built = true;
+  if (!from_checkpoint) amg_age = 0;
   if (timing)
     std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s\n", how, L,
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
@@ -1269,6 +1297,8 @@ void Solver::check_evolution() {
 
 void Solver::step() {  // coupled_solver.rs:33-499
   CFD_HIP(hipSetDevice(device));
+  // opt-in deviation from the frozen hierarchy
+  if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) drop_amg();
   rotate();
   constants.component = 0;
   if (dist()) halo_state(true);  // the rotated slot's ghosts (last written 3 steps ago)
@@ -1342,6 +1372,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
     prev_p = dp;
   }
   constants.time += constants.dt;
+  if (amg_built) ++amg_age;
   check_evolution();
 }
 

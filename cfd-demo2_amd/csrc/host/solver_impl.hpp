@@ -47,6 +47,10 @@ class DeviceArena {
     if (!v.empty()) CFD_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
     return p;
   }
+  void swap(DeviceArena& o) {
+    ptrs_.swap(o.ptrs_);
+    std::swap(bytes_, o.bytes_);
+  }
   void release() {
     for (void* p : ptrs_) (void)hipFree(p);
     ptrs_.clear();
@@ -251,6 +255,11 @@ struct Solver {
   // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)
   float* amg_src = nullptr;
   bool amg_src_loaded = false;
+  // every device allocation of the hierarchy (levels, plans, tail images):
+  // released as a whole when it is rebuilt (cfg.amg_rebuild_interval, load_state)
+  DeviceArena amg_arena;
+  uint32_t amg_age = 0;  // steps completed since the hierarchy was built
+  void drop_amg();
   // host-side state
   cfd_constants constants{};
   cfd_step_info info{};

@@ -117,6 +117,9 @@ typedef struct cfd_config {
   float fgmres_atol;          /* 1e-7                                                   */
   int32_t log_level;          /* 0 silent, 1 reference println! lines to stderr        */
   int32_t use_graphs;         /* capture the fixed-schedule inner solve in a hipGraph   */
+  int32_t amg_rebuild_interval; /* 0: AMG hierarchy frozen after the first AMG solve
+                                   (reference, amg.rs); k > 0: rebuilt from the current
+                                   matrix every k steps (opt-in deviation) */
 } cfd_config;
 
 void cfd_config_default(cfd_config* cfg);
@@ -207,7 +210,8 @@ typedef struct cfd_state_file_header {
   double variance[10][2]; /* check_evolution's (var_u, var_v) history */
   cfd_constants constants;
   cfd_step_info info;
-  uint8_t reserved[176];
+  uint32_t amg_age;     /* steps since the hierarchy was built (amg_rebuild_interval) */
+  uint8_t reserved[172];
 } cfd_state_file_header;
 
 /* Writes the state to `path`.  Distributed solver: COLLECTIVE, every rank
@@ -215,8 +219,8 @@ typedef struct cfd_state_file_header {
 cfd_status cfd_state_save(cfd_solver* s, const char* path);
 /* Replaces the state with the file's (not collective: a distributed rank
  * reads its owned cells and ghosts).  The file may come from any rank
- * count.  The solver must not have built its AMG hierarchy yet (load into a
- * fresh solver); the saved scalar matrix, if any, becomes the AMG source.  */
+ * count.  The solver's own AMG hierarchy, if built, is dropped; the saved
+ * scalar matrix, if any, is what the next AMG solve rebuilds it from.      */
 cfd_status cfd_state_load(cfd_solver* s, const char* path);
 /* In-process group: cfd_state_save on every rank (one host thread each).   */
 cfd_status cfd_group_state_save(cfd_solver* const* handles, int32_t nranks, const char* path);

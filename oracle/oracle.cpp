@@ -369,6 +369,7 @@ struct oracle_solver {
   bool inner_has_last = false;
   float inner_last = 0.0f;
   std::unique_ptr<Amg> amg;
+  uint32_t amg_age = 0;  // steps since the hierarchy was built (cfg.amg_rebuild_interval)
   // outer-loop / step info
   cfd_step_info info{};
   std::vector<float> prev_u_cpu;
@@ -1095,6 +1096,7 @@ cfd_linear_stats solve(oracle_solver* s) {
   if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
     s->amg.reset(new Amg);
     s->amg->build(s->scalar, 20, s->starts);
+    s->amg_age = 0;
   }
   const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts));
   // The two early exits are kept even under the fixed schedule: the first
@@ -1351,6 +1353,9 @@ void rotate(oracle_solver* s) {  // coupled_solver.rs:43-71
 }
 
 int step(oracle_solver* s) {  // coupled_solver.rs:33-499
+  // opt-in deviation: drop the frozen hierarchy; the next AMG solve rebuilds it
+  if (s->cfg.amg_rebuild_interval > 0 && s->amg && s->amg_age >= (uint32_t)s->cfg.amg_rebuild_interval)
+    s->amg.reset();
   rotate(s);
   s->constants.component = 0;
   prepare(s);
@@ -1412,6 +1417,7 @@ int step(oracle_solver* s) {  // coupled_solver.rs:33-499
     }
   }
   s->constants.time += s->constants.dt;
+  if (s->amg) ++s->amg_age;
   check_evolution(s);
   return 0;
 }

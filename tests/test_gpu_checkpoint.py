@@ -39,12 +39,13 @@ def _same(a, b, ctx):
         assert np.array_equal(x, y), f"{ctx}: item {k} differs"
 
 
-@pytest.mark.parametrize("precond,time_scheme,scheme,lag", [(1, 1, 0, 1), (1, 0, 1, 0), (0, 1, 2, 1)])
-def test_resume_is_bitexact(precond, time_scheme, scheme, lag, tmp_path):
+@pytest.mark.parametrize("precond,time_scheme,scheme,lag,rebuild",
+                         [(1, 1, 0, 1, 0), (1, 0, 1, 0, 0), (0, 1, 2, 1, 0), (1, 0, 0, 1, 2)])
+def test_resume_is_bitexact(precond, time_scheme, scheme, lag, rebuild, tmp_path):
     mesh = backwards_step()
-    cfg = default_config(convergence_lag=lag)
+    cfg = default_config(convergence_lag=lag, amg_rebuild_interval=rebuild)
     a = GpuSolver(mesh, config=cfg)
-    o = OracleSolver(mesh, config=default_config(convergence_lag=lag))
+    o = OracleSolver(mesh, config=default_config(convergence_lag=lag, amg_rebuild_interval=rebuild))
     for s in (a, o):
         _setup(s, mesh, precond, time_scheme, scheme)
     k0, k1 = 3, 3
@@ -133,8 +134,6 @@ def test_load_errors(tmp_path):
     g.step()
     path = str(tmp_path / "s.bin")
     g.save_state(path)
-    with pytest.raises(RuntimeError, match="already built its AMG"):
-        g.load_state(path)  # AMG hierarchy exists
     other = GpuSolver(channel_obstacle(h=0.03))
     with pytest.raises(RuntimeError, match="different mesh"):
         other.load_state(path)
@@ -149,3 +148,30 @@ def test_load_errors(tmp_path):
     fresh.load_state(path)  # a failed load leaves the solver usable
     fresh.step()
     assert np.all(np.isfinite(fresh.get_u()))
+
+
+def test_load_into_a_running_solver(tmp_path):
+    """Loading drops the solver's own hierarchy (built from a different matrix)
+    and resumes bit-exactly: the same solver rewinds and replays."""
+    mesh = backwards_step()
+    g = GpuSolver(mesh)
+    _setup(g, mesh, 1, 1, 0)
+    g.step()
+    path = str(tmp_path / "s.bin")
+    g.save_state(path)
+    ref = []
+    for _ in range(3):
+        g.step()
+        ref.append(_snap(g))
+    digests = g.amg_setup_info()[1]
+    h = GpuSolver(mesh)
+    _setup(h, mesh, 1, 0, 2)  # different scheme: its first hierarchy differs
+    for _ in range(2):
+        h.step()
+    assert h.amg_setup_info()[1] != digests
+    for s in (g, h):
+        s.load_state(path)
+        for k in range(3):
+            s.step()
+            _same(_snap(s), ref[k], f"replay step {k}")
+        assert s.amg_setup_info()[1] == digests

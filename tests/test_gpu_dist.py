@@ -172,3 +172,21 @@ def test_group_amg_device_setup_matches_host(nranks, rep, which, replicate_rows,
     _assert_same_fields(dev, host, f"{which} R={nranks} device vs host setup")
     dev.close()
     host.close()
+
+
+def test_group_amg_rebuild_interval(replicate_rows):
+    """Rebuilding the distributed hierarchy (all its device memory released
+    and re-made, halo plans included) stays bit-exact with oracle(R)."""
+    replicate_rows(50)
+    mesh = backwards_step()
+    cfg = dict(amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8)
+    g = GpuGroup(mesh, 2, config=default_config(**cfg))
+    o = OracleSolver(mesh, nranks=2, config=default_config(**cfg))
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    for k in range(5):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"R=2 rebuild step {k}")
+        _assert_same_info(g, o, f"R=2 rebuild step {k}")
+    g.close()

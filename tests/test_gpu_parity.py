@@ -413,3 +413,22 @@ def test_amg_device_setup_matches_host(which, monkeypatch):
     assert dd == dh, [i for i, (a, b) in enumerate(zip(dd, dh)) if a != b]
     _assert_same_fields(dev, host, f"{which} device vs host AMG setup")
     _assert_same_info(dev, host, which)
+
+
+@pytest.mark.parametrize("interval", [1, 2])
+def test_amg_rebuild_interval_parity(interval):
+    """Opt-in hierarchy rebuild every `interval` steps:
+    GPU == oracle bit-exact, and the device hierarchy really changes."""
+    mesh = backwards_step()
+    g, o = _pair(mesh, amg_rebuild_interval=interval, fixed_outer=3, fixed_inner=10)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    digests = []
+    for k in range(6):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"rebuild/{interval} step {k}")
+        _assert_same_info(g, o, f"rebuild/{interval} step {k}")
+        digests.append(g.amg_setup_info()[1])
+    assert digests[0] == digests[1] == digests[2]  # stale-ring steps: same source matrix
+    assert digests[5] != digests[0]
