@@ -59,10 +59,11 @@ struct SetupLevel {
   const uint32_t* col = nullptr;
   std::vector<uint32_t> own_row, own_col;  // storage of a downloaded coarse pattern
   SetupMatrix dev{};
-  DevTmp<uint32_t> d_rowptr;
-  DevTmp<int32_t> d_col;           // global columns
-  DevTmp<int32_t> d_relcol;        // distributed level: signed local columns
-  DevTmp<float> d_val;
+  // device CSR of a coarse level: kept (amg_arena) for the numeric re-setup
+  uint32_t* d_rowptr = nullptr;
+  int32_t* d_col = nullptr;     // global columns
+  int32_t* d_relcol = nullptr;  // distributed level: signed local columns
+  float* d_val = nullptr;
 };
 
 }  // namespace
@@ -82,6 +83,7 @@ bool Solver::build_amg_device() {
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
   levels.clear();
+  amg_refresh.clear();
   const char* rep_env = std::getenv("CFD_AMG_REPLICATE_ROWS");
   const uint64_t rep = rep_env ? std::strtoull(rep_env, nullptr, 10) : 262144u;
   amg_g = -1;
@@ -90,8 +92,8 @@ bool Solver::build_amg_device() {
     CFD_HIP(hipMemsetAsync(p, 0, (cnt + 64) * sizeof(float), stream));
     return p;
   };
-  DevTmp<uint32_t> d_flag(1);
-  CFD_HIP(hipMemsetAsync(d_flag.p, 0, sizeof(uint32_t), stream));
+  amg_setup_flag = arena.alloc<uint32_t>(1);
+  CFD_HIP(hipMemsetAsync(amg_setup_flag, 0, sizeof(uint32_t), stream));
   auto gather_counts = [&](uint64_t mine) { return allgather_u64(mine); };
 
   SetupLevel cur;
@@ -141,9 +143,9 @@ bool Solver::build_amg_device() {
       G.plan = build_halo_plan(cur.part, rk, cur.row, n, cur.col, ghost, G.glo, G.npad);
       make_plan_buffers(G.plan, 1);
       if (li > 0) {  // level 0's device columns (d_scol) are local already
-        cur.d_relcol = DevTmp<int32_t>(nnz);
-        CFD_HIP(hipMemcpyAsync(cur.d_relcol.p, rcol.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice, stream));
-        cur.dev.col = cur.d_relcol.p;
+        cur.d_relcol = arena.alloc<int32_t>(nnz);
+        CFD_HIP(hipMemcpyAsync(cur.d_relcol, rcol.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+        cur.dev.col = cur.d_relcol;
       }
     }
     int wmax = 0;
@@ -191,6 +193,8 @@ bool Solver::build_amg_device() {
     G.dev.drank = drank;
     G.dev.dv = dv;
     G.dev.de = de;
+    amg_refresh.emplace_back();
+    amg_refresh.back().fine = cur.dev;
     uint32_t sh = 0;  // ghost space below the owned rows of a distributed level's vectors
     if (cur.dist) {
       sh = (G.glo + 63) & ~63u;
@@ -256,14 +260,13 @@ bool Solver::build_amg_device() {
     G.dev.nc = nagg_own;
     // Galerkin columns: global aggregate ids of every (owned or ghost) fine column
     const uint32_t* gal_agg = G.dev.agg;
-    DevTmp<uint32_t> gagg;
     if (cur.dist) {
-      gagg = DevTmp<uint32_t>((size_t)sh + G.npad + G.ghi + 64);
+      uint32_t* gagg = arena.alloc<uint32_t>((size_t)sh + G.npad + G.ghi + 64);
       std::vector<uint32_t> ga(n);
       for (uint32_t i = 0; i < n; ++i) ga[i] = agg[i] + (uint32_t)cpart[rk];
-      CFD_HIP(hipMemcpyAsync(gagg.p + sh, ga.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-      halo(G.plan, {{reinterpret_cast<float*>(gagg.p + sh), 1}});  // bit copies
-      gal_agg = gagg.p + sh;
+      CFD_HIP(hipMemcpyAsync(gagg + sh, ga.data(), (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+      halo(G.plan, {{reinterpret_cast<float*>(gagg + sh), 1}});  // bit copies
+      gal_agg = gagg + sh;
     }
     // ---- Galerkin product on the device (this rank's aggregates)
     SetupLevel next;
@@ -271,13 +274,13 @@ bool Solver::build_amg_device() {
     next.part = cpart;
     DevTmp<uint32_t> d_cnt(nagg_own);
     launch_galerkin(cur.dev, gal_agg, G.dev.r_row, G.dev.r_col, nagg_own, d_cnt.p, nullptr, nullptr, nullptr,
-                    d_flag.p, stream);
+                    amg_setup_flag, stream);
     CFD_HIP(hipGetLastError());
     next.own_row.assign((size_t)nagg_own + 1, 0);
     uint32_t flag = 0;
     CFD_HIP(hipMemcpyAsync(next.own_row.data() + 1, d_cnt.p, (size_t)nagg_own * sizeof(uint32_t),
                            hipMemcpyDeviceToHost, stream));
-    CFD_HIP(hipMemcpyAsync(&flag, d_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(&flag, amg_setup_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     sync();
     // every rank must take the same path: the overflow flag is combined over ranks
     bool overflow = flag != 0;
@@ -288,18 +291,29 @@ bool Solver::build_amg_device() {
     if (overflow) {
       if (timing) std::fprintf(stderr, "[amg setup] device path: capacity overflow at level %d\n", li);
       levels.clear();
+      amg_refresh.clear();
       return false;
     }
     for (uint32_t I = 0; I < nagg_own; ++I) next.own_row[I + 1] += next.own_row[I];
     size_t nnz_c = next.own_row[nagg_own];
-    next.d_rowptr = DevTmp<uint32_t>((size_t)nagg_own + 1);
-    next.d_col = DevTmp<int32_t>(nnz_c);
-    next.d_val = DevTmp<float>(nnz_c);
-    CFD_HIP(hipMemcpyAsync(next.d_rowptr.p, next.own_row.data(), ((size_t)nagg_own + 1) * sizeof(uint32_t),
+    next.d_rowptr = arena.alloc<uint32_t>((size_t)nagg_own + 1);
+    next.d_col = arena.alloc<int32_t>(nnz_c);
+    next.d_val = arena.alloc<float>(nnz_c);
+    CFD_HIP(hipMemcpyAsync(next.d_rowptr, next.own_row.data(), ((size_t)nagg_own + 1) * sizeof(uint32_t),
                            hipMemcpyHostToDevice, stream));
-    launch_galerkin(cur.dev, gal_agg, G.dev.r_row, G.dev.r_col, nagg_own, nullptr, next.d_rowptr.p,
-                    reinterpret_cast<uint32_t*>(next.d_col.p), next.d_val.p, d_flag.p, stream);
+    launch_galerkin(cur.dev, gal_agg, G.dev.r_row, G.dev.r_col, nagg_own, nullptr, next.d_rowptr,
+                    reinterpret_cast<uint32_t*>(next.d_col), next.d_val, amg_setup_flag, stream);
     CFD_HIP(hipGetLastError());
+    {
+      AmgRefreshLevel& F = amg_refresh.back();
+      F.has_coarse = true;
+      F.gal_agg = gal_agg;
+      F.nagg_own = nagg_own;
+      F.rowptr_c = next.d_rowptr;
+      F.col_c = reinterpret_cast<uint32_t*>(next.d_col);
+      F.val_c = next.d_val;
+      F.nnz_own = nnz_c;
+    }
     next.dist = next_dist;
     if (cur.dist && !next_dist) {
       // first replicated level: all-gather row lengths, columns and values
@@ -315,38 +329,42 @@ bool Solver::build_amg_device() {
       std::vector<uint32_t> lens(ng, 0);
       for (uint32_t I = 0; I < nagg_own; ++I) lens[cpart[rk] + I] = next.own_row[I + 1] - next.own_row[I];
       DevTmp<uint32_t> d_lens(ng);
-      DevTmp<int32_t> d_colall(nnz_all);
-      DevTmp<float> d_valall(nnz_all);
+      int32_t* d_colall = arena.alloc<int32_t>(nnz_all);
+      float* d_valall = arena.alloc<float>(nnz_all);
       CFD_HIP(hipMemcpyAsync(d_lens.p, lens.data(), ng * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-      CFD_HIP(hipMemcpyAsync(d_colall.p + eoff[rk], next.d_col.p, nnz_c * sizeof(int32_t), hipMemcpyDeviceToDevice,
+      CFD_HIP(hipMemcpyAsync(d_colall + eoff[rk], next.d_col, nnz_c * sizeof(int32_t), hipMemcpyDeviceToDevice,
                              stream));
-      CFD_HIP(hipMemcpyAsync(d_valall.p + eoff[rk], next.d_val.p, nnz_c * sizeof(float), hipMemcpyDeviceToDevice,
+      CFD_HIP(hipMemcpyAsync(d_valall + eoff[rk], next.d_val, nnz_c * sizeof(float), hipMemcpyDeviceToDevice,
                              stream));
       comm->allgatherv_inplace(d_lens.p, roff, stream);
-      comm->allgatherv_inplace(d_colall.p, coff, stream);
-      comm->allgatherv_inplace(d_valall.p, coff, stream);
+      comm->allgatherv_inplace(d_colall, coff, stream);
+      comm->allgatherv_inplace(d_valall, coff, stream);
+      AmgRefreshLevel& F = amg_refresh.back();
+      F.val_all = d_valall;
+      F.coff = coff;
+      F.e_own = eoff[rk];
       CFD_HIP(hipMemcpyAsync(lens.data(), d_lens.p, ng * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
       sync();
       next.own_row.assign(ng + 1, 0);
       for (uint64_t I = 0; I < ng; ++I) next.own_row[I + 1] = next.own_row[I] + lens[I];
       next.n = (uint32_t)ng;
       nnz_c = nnz_all;
-      next.d_rowptr = DevTmp<uint32_t>(ng + 1);
-      CFD_HIP(hipMemcpyAsync(next.d_rowptr.p, next.own_row.data(), (ng + 1) * sizeof(uint32_t),
+      next.d_rowptr = arena.alloc<uint32_t>(ng + 1);
+      CFD_HIP(hipMemcpyAsync(next.d_rowptr, next.own_row.data(), (ng + 1) * sizeof(uint32_t),
                              hipMemcpyHostToDevice, stream));
-      next.d_col = std::move(d_colall);
-      next.d_val = std::move(d_valall);
+      next.d_col = d_colall;
+      next.d_val = d_valall;
     }
     next.own_col.resize(nnz_c);
-    CFD_HIP(hipMemcpyAsync(next.own_col.data(), next.d_col.p, nnz_c * sizeof(uint32_t), hipMemcpyDeviceToHost,
+    CFD_HIP(hipMemcpyAsync(next.own_col.data(), next.d_col, nnz_c * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            stream));
     sync();  // the fine level's buffers may be released after this
     next.row = next.own_row.data();
     next.col = next.own_col.data();
     next.dev.ell = 0;
-    next.dev.rowptr = next.d_rowptr.p;
-    next.dev.col = next.d_col.p;
-    next.dev.val = next.d_val.p;
+    next.dev.rowptr = next.d_rowptr;
+    next.dev.col = next.d_col;
+    next.dev.val = next.d_val;
     if (timing)
       std::fprintf(stderr, "[amg setup] device level %d%s: n=%u nagg=%llu nnz_c=%zu  aggregate+R %.3fs  total %.3fs\n",
                    li, cur.dist ? " (dist)" : "", n, (unsigned long long)nagg_glob, nnz_c, t_agg, secs(t0));
@@ -355,6 +373,36 @@ bool Solver::build_amg_device() {
   if (amg_g < 0) amg_g = dist() ? (int)levels.size() : 0;
   sync();
   return true;
+}
+
+// Numeric re-setup from the current matrix (cfg.amg_rebuild_interval): the
+// structure built by build_amg_device is value-independent (aggregation and
+// R on the pattern, Galerkin patterns structural -- explicit zeros are kept,
+// as amg.rs keeps them), so packing every level and re-running the Galerkin
+// fill over it in level order gives the bytes a full rebuild gives
+// (tests/test_gpu_parity.py::test_amg_refresh_matches_full_rebuild).
+void Solver::refresh_amg() {
+  const size_t slots_s = (size_t)topo.ws * topo.ld;
+  CFD_HIP(hipMemcpyAsync(amg_src, sval, slots_s * sizeof(float), hipMemcpyDeviceToDevice, stream));
+  for (size_t li = 0; li < amg_refresh.size(); ++li) {
+    const AmgRefreshLevel& F = amg_refresh[li];
+    const AmgLevelDev& d = levels[li].dev;
+    launch_amg_pack(F.fine, d.n, d.stride, d.w, d.use16, const_cast<float*>(d.val), const_cast<int16_t*>(d.col16),
+                    const_cast<int32_t*>(d.col32), const_cast<uint8_t*>(d.len), const_cast<uint8_t*>(d.drank),
+                    const_cast<float*>(d.dv), const_cast<float*>(d.de), stream);
+    if (!F.has_coarse) continue;
+    launch_galerkin(F.fine, F.gal_agg, d.r_row, d.r_col, F.nagg_own, nullptr, F.rowptr_c, F.col_c, F.val_c,
+                    amg_setup_flag, stream);
+    if (F.val_all) {  // first replicated level: every rank's coarse values (collective)
+      if (F.nnz_own)
+        CFD_HIP(hipMemcpyAsync(F.val_all + F.e_own, F.val_c, F.nnz_own * sizeof(float), hipMemcpyDeviceToDevice,
+                               stream));
+      comm->allgatherv_inplace(F.val_all, F.coff, stream);
+    }
+  }
+  CFD_HIP(hipGetLastError());
+  if (tail_blob_first >= 0) build_tail_blob(tail_blob_first, true);
+  sync();
 }
 
 }  // namespace cfd2

@@ -77,7 +77,9 @@ void Solver::save_state(const char* path) {
   CFD_HIP(hipSetDevice(device));
   sync();
   // collective: every rank learns the AMG source size and its value offset
-  const uint64_t my_nnz = (amg_built || amg_src_loaded) ? (uint64_t)topo.scol.size() : 0;
+  // a pending refresh stands for a dropped hierarchy (the next AMG solve re-makes it)
+  const bool have_amg = (amg_built && !amg_refresh_pending) || amg_src_loaded;
+  const uint64_t my_nnz = have_amg ? (uint64_t)topo.scol.size() : 0;
   const std::vector<uint64_t> nz = allgather_u64(my_nnz);
   uint64_t nnz = 0, e0 = 0;
   for (int q = 0; q < R; ++q) {
@@ -113,7 +115,7 @@ void Solver::save_state(const char* path) {
         }
         h.constants = constants;
         h.info = info;
-        h.amg_age = amg_age;
+        h.amg_age = amg_refresh_pending ? 0 : amg_age;
         pwrite_all(fd, &h, sizeof(h), 0);
       }
       // owned rows of every per-cell array at their global offsets

@@ -690,6 +690,9 @@ void Solver::drop_amg() {
   d_tail_blob = nullptr;
   d_tail_desc = nullptr;
   tail_blob_words = tail_vec_floats = 0;
+  amg_refresh.clear();
+  amg_setup_flag = nullptr;
+  amg_refresh_pending = false;
   amg_arena.release();
   amg_built = false;
   amg_setup_path = 0;
@@ -697,7 +700,14 @@ void Solver::drop_amg() {
 }
 
 void Solver::ensure_amg() {
-  if (amg_built) return;
+  if (amg_built) {
+    if (amg_refresh_pending) {
+      refresh_amg();
+      amg_refresh_pending = false;
+      amg_age = 0;
+    }
+    return;
+  }
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
   const auto t_start = std::chrono::steady_clock::now();
   const char* se = std::getenv("CFD_AMG_SETUP");
@@ -764,7 +774,8 @@ void Solver::ensure_amg() {
 // LDS image of the tail levels [tf, L) for k_amg_tail_blob: every array the
 // tail V-cycle reads, compacted (off-diagonal CSR, u16 indices) from the
 // level images, when vectors + blob fit in one CU's LDS.
-void Solver::build_tail_blob(int tf) {
+void Solver::build_tail_blob(int tf, bool reuse) {
+  const uint32_t old_words = tail_blob_words;
   tail_blob_first = -1;
   const int L = (int)levels.size();
   if (tf >= L) return;
@@ -866,8 +877,16 @@ void Solver::build_tail_blob(int tf) {
   }
   align4();
   if (4 * ((size_t)vec + blob.size()) > kTailLdsMax) return;
-  d_tail_blob = arena.upload(blob, stream);
-  d_tail_desc = arena.upload(desc, stream);
+  if (reuse && d_tail_blob && blob.size() == old_words) {  // same structure: new values in place
+    CFD_HIP(hipMemcpyAsync(d_tail_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice, stream));
+    CFD_HIP(hipMemcpyAsync(d_tail_desc, desc.data(), desc.size() * sizeof(TailBlobLevel), hipMemcpyHostToDevice,
+                           stream));
+    sync();  // the host staging vectors die here
+  } else {
+    if (reuse) throw std::logic_error("AMG refresh: tail blob layout changed");
+    d_tail_blob = arena.upload(blob, stream);
+    d_tail_desc = arena.upload(desc, stream);
+  }
   tail_blob_words = (uint32_t)blob.size();
   tail_vec_floats = vec;
   tail_blob_first = tf;
@@ -1298,7 +1317,15 @@ void Solver::check_evolution() {
 void Solver::step() {  // coupled_solver.rs:33-499
   CFD_HIP(hipSetDevice(device));
   // opt-in deviation from the frozen hierarchy
-  if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) drop_amg();
+  if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) {
+    // numeric re-setup over the kept structure when the device setup built it
+    // (CFD_AMG_REFRESH=0: full rebuild; both give the same hierarchy)
+    const char* re = std::getenv("CFD_AMG_REFRESH");
+    if (amg_setup_path == 2 && !amg_refresh.empty() && !(re && re[0] == '0'))
+      amg_refresh_pending = true;
+    else
+      drop_amg();
+  }
   rotate();
   constants.component = 0;
   if (dist()) halo_state(true);  // the rotated slot's ghosts (last written 3 steps ago)

@@ -11,6 +11,7 @@
 #include <memory>
 
 #include "../../../include/cfd2_amd.h"
+#include "../hip/amg_setup.hpp"
 #include "../hip/kernels.hpp"
 #include "comm.hpp"
 #include "dist.hpp"
@@ -249,7 +250,7 @@ struct Solver {
   uint32_t* d_tail_blob = nullptr;
   TailBlobLevel* d_tail_desc = nullptr;
   uint32_t tail_blob_words = 0, tail_vec_floats = 0;
-  void build_tail_blob(int tf);
+  void build_tail_blob(int tf, bool reuse = false);  // reuse: rewrite the existing blob in place
   std::vector<AmgGpuLevel> levels;
   // the scalar matrix (ELL image, like sval) the hierarchy was built from:
   // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)
@@ -260,6 +261,27 @@ struct Solver {
   DeviceArena amg_arena;
   uint32_t amg_age = 0;  // steps completed since the hierarchy was built
   void drop_amg();
+  // numeric re-setup (device setup only): aggregation, P/R, every coarse
+  // pattern, level layout and halo plan depend only on the sparsity pattern,
+  // so a rebuild from new values re-runs just the Galerkin fill and the level
+  // packing over the kept structure -- the same bytes as a full rebuild.
+  struct AmgRefreshLevel {
+    SetupMatrix fine{};                  // the level as the setup kernels read it
+    bool has_coarse = false;
+    const uint32_t* gal_agg = nullptr;   // aggregate id per (owned or ghost) fine column
+    uint32_t nagg_own = 0;
+    const uint32_t* rowptr_c = nullptr;  // this rank's coarse rows (fill output)
+    uint32_t* col_c = nullptr;
+    float* val_c = nullptr;
+    size_t nnz_own = 0;
+    float* val_all = nullptr;            // first replicated level: all-gathered values
+    std::vector<size_t> coff;            // byte offsets of each rank's values in val_all
+    size_t e_own = 0;                    // this rank's first value in val_all
+  };
+  std::vector<AmgRefreshLevel> amg_refresh;
+  uint32_t* amg_setup_flag = nullptr;  // k_galerkin overflow flag (amg_arena)
+  bool amg_refresh_pending = false;    // refresh at the next AMG solve
+  void refresh_amg();
   // host-side state
   cfd_constants constants{};
   cfd_step_info info{};

@@ -174,9 +174,13 @@ def test_group_amg_device_setup_matches_host(nranks, rep, which, replicate_rows,
     host.close()
 
 
-def test_group_amg_rebuild_interval(replicate_rows):
-    """Rebuilding the distributed hierarchy (all its device memory released
-    and re-made, halo plans included) stays bit-exact with oracle(R)."""
+@pytest.mark.parametrize("refresh", ["1", "0"])
+def test_group_amg_rebuild_interval(refresh, replicate_rows, monkeypatch):
+    """Re-setting up the distributed hierarchy -- numeric refresh (Galerkin
+    fill, packing and the replicated level's value all-gather over the kept
+    structure) or full rebuild (device memory released and re-made, halo
+    plans included) -- stays bit-exact with oracle(R)."""
+    monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
     replicate_rows(50)
     mesh = backwards_step()
     cfg = dict(amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8)

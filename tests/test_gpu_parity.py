@@ -432,3 +432,22 @@ def test_amg_rebuild_interval_parity(interval):
         digests.append(g.amg_setup_info()[1])
     assert digests[0] == digests[1] == digests[2]  # stale-ring steps: same source matrix
     assert digests[5] != digests[0]
+
+
+def test_amg_refresh_matches_full_rebuild(monkeypatch):
+    """The numeric re-setup (Galerkin fill + packing over the kept structure)
+    produces the same hierarchy bytes and fields as dropping and rebuilding."""
+    mesh = channel_obstacle(h=0.03)
+    runs = {}
+    for refresh in ("1", "0"):
+        monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
+        g = GpuSolver(mesh, config=default_config(amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8))
+        _setup_amg_test(g, mesh, 1)
+        out = []
+        for _ in range(6):
+            g.step()
+            out.append((g.get_u(), g.get_p(), g.amg_setup_info()[1]))
+        runs[refresh] = out
+    for k, (a, b) in enumerate(zip(runs["1"], runs["0"])):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), f"step {k} fields"
+        assert a[2] == b[2], f"step {k} AMG level digests"
