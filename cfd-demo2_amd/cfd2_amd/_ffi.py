@@ -72,7 +72,6 @@ class Config(C.Structure):
         ("fgmres_rtol", C.c_float),
         ("fgmres_atol", C.c_float),
         ("log_level", C.c_int32),
-        ("use_graphs", C.c_int32),
         ("amg_rebuild_interval", C.c_int32),
     ]
 
@@ -133,7 +132,6 @@ def default_config(**overrides) -> Config:
         fgmres_rtol=1e-5,
         fgmres_atol=1e-7,
         log_level=0,
-        use_graphs=0,
         amg_rebuild_interval=0,
     )
     for k, v in overrides.items():

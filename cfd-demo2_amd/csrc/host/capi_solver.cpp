@@ -65,7 +65,6 @@ void cfd_config_default(cfd_config* c) {
   c->fgmres_rtol = 1e-5f;
   c->fgmres_atol = 1e-7f;
   c->log_level = 0;
-  c->use_graphs = 0;
   c->amg_rebuild_interval = 0;
 }
 

@@ -10,7 +10,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
+#include <string>
 #include <cstring>
 #include <limits>
 
@@ -19,6 +21,21 @@
 namespace cfd2 {
 
 namespace {
+// Rust's `{:.2e}` (the reference's log format): 1.23e-5, 3.40e38, NaN, inf
+std::string e2(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "inf" : "-inf";
+  char buf[48];
+  std::snprintf(buf, sizeof(buf), "%.2e", v);
+  const std::string s(buf);
+  const size_t e = s.find('e');
+  size_t i = e + 1;
+  const bool neg = s[i] == '-';
+  if (s[i] == '-' || s[i] == '+') ++i;
+  while (i + 1 < s.size() && s[i] == '0') ++i;
+  return s.substr(0, e) + "e" + (neg ? "-" : "") + s.substr(i);
+}
+const char* tf(bool b) { return b ? "true" : "false"; }
 constexpr int kScalBase = 0;   // dsc[0..15]: rhs_norm, resid, inv_resid, wnorm, inv_w, resid_est
 constexpr int kHOff = 16;
 }  // namespace
@@ -191,6 +208,14 @@ CoupledMatrix Solver::cmat() const {
   A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
   return A;
+}
+
+void Solver::log(const char* fmt, ...) const {
+  if (cfg.log_level < 1 || rk != 0) return;
+  va_list ap;
+  va_start(ap, fmt);
+  std::vfprintf(stderr, fmt, ap);
+  va_end(ap);
 }
 
 // ---------------------------------------------------------------- state API
@@ -1117,10 +1142,12 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   float residual_norm = residual_into_v0_blocking();
   const float target = std::fmax(tol * rhs_norm, abstol);
   if (residual_norm < target) {
+    log("FGMRES: Initial guess already converged (||r|| = %s < %s)\n", e2(residual_norm).c_str(), e2(target).c_str());
     st.residual = residual_norm;
     st.converged = 1;
     return st;
   }
+  log("FGMRES: Initial residual = %s\n", e2(residual_norm).c_str());
   uint32_t total = 0;
   float final_resid = residual_norm;
   bool converged = false;
@@ -1172,6 +1199,8 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         check = inner.last;
         inner.pending = j;
       }
+      if (have && (total % 10 == 0 || check < tol * rhs_norm))
+        log("FGMRES iter %u: residual = %s (target %s)\n", total, e2(check).c_str(), e2(tol * rhs_norm).c_str());
       if (have && check < tol * rhs_norm) {
         converged = true;
         break;
@@ -1187,6 +1216,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         inner.pending = -1;
       }
       final_resid = inner.last;
+      log("FGMRES restart %d: estimated residual = %s\n", outer + 1, e2(final_resid).c_str());
       break;
     }
     residual_norm = residual_into_v0_blocking();
@@ -1197,15 +1227,18 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     }
     if (residual_norm < tol * rhs_norm) {
       converged = true;
+      log("FGMRES restart %d: true residual = %s (converged)\n", outer + 1, e2(residual_norm).c_str());
       break;
     }
     if (residual_norm <= 0.0f) {
+      log("FGMRES: residual vanished at restart %d\n", outer + 1);
       converged = true;
       break;
     }
     const float improvement = (prev_resid - residual_norm) / prev_resid;
     if (improvement < 1e-3f) {
       if (++stagnation >= 3) {
+        log("FGMRES: Stagnation detected at restart %d (residual %s)\n", outer + 1, e2(residual_norm).c_str());
         converged = true;
         break;
       }
@@ -1213,7 +1246,11 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       stagnation = 0;
     }
     prev_resid = residual_norm;
+    log("FGMRES restart %d: residual = %s (target %s)\n", outer + 1, e2(residual_norm).c_str(),
+        e2(tol * rhs_norm).c_str());
   }
+  log("FGMRES finished: %u iterations, residual = %s, converged = %s\n", total, e2(final_resid).c_str(),
+      tf(converged));
   st.iterations = total;
   st.residual = final_resid;
   st.converged = converged;
@@ -1311,7 +1348,15 @@ void Solver::check_evolution() {
     info.degenerate_count = 0;
     info.steady_state_count = 0;
   }
-  if (info.degenerate_count > 10 || info.steady_state_count > 10) info.should_stop = 1;
+  if (info.degenerate_count > 10) {
+    log("Solution is degenerate: Velocity field is uniform and not evolving. Variance U: %s, V: %s\n",
+        e2(var_u).c_str(), e2(var_v).c_str());
+    info.should_stop = 1;
+  }
+  if (info.steady_state_count > 10) {
+    log("Steady state reached. Evolution diff: %s\n", e2(evo).c_str());
+    info.should_stop = 1;
+  }
 }
 
 void Solver::step() {  // coupled_solver.rs:33-499
@@ -1339,9 +1384,12 @@ void Solver::step() {  // coupled_solver.rs:33-499
   int pend = -1;
   info.total_linear_iterations = 0;
   for (int iter = 0; iter < max_iters; ++iter) {
+    log("Coupled Iteration: %d\n", iter + 1);
     if (iter > 0 || constants.scheme != 0) prepare();
     assemble();
     const cfd_linear_stats ls = solve();
+    log("Coupled linear solve: %u iterations, residual %s, converged=%s\n", ls.iterations, e2(ls.residual).c_str(),
+        tf(ls.converged));
     info.stats_p = ls;
     info.total_linear_iterations += ls.iterations;
     if (std::isnan(ls.residual)) throw std::domain_error("Coupled Linear Solver Diverged: NaN detected in linear residual");
@@ -1387,13 +1435,20 @@ void Solver::step() {  // coupled_solver.rs:33-499
     info.outer_residual_u = cu;
     info.outer_residual_p = cp;
     info.outer_iterations = iter + 1;
+    log("Coupled Residuals - U: %s, P: %s\n", e2(du).c_str(), e2(dp).c_str());
     if (!fixed) {
-      if (du < tol_u && dp < tol_p) break;
+      if (du < tol_u && dp < tol_p) {
+        log("Coupled Solver Converged in %d iterations\n", iter + 1);
+        break;
+      }
       const double rel_u = (std::isfinite(prev_u) && std::fabs(prev_u) > 1e-14) ? std::fabs((du - prev_u) / prev_u)
                                                                                 : std::numeric_limits<double>::infinity();
       const double rel_p = (std::isfinite(prev_p) && std::fabs(prev_p) > 1e-14) ? std::fabs((dp - prev_p) / prev_p)
                                                                                 : std::numeric_limits<double>::infinity();
-      if (rel_u < 1e-2 && rel_p < 1e-2 && iter > 2) break;
+      if (rel_u < 1e-2 && rel_p < 1e-2 && iter > 2) {
+        log("Coupled solver stagnated at iter %d: U=%s, P=%s\n", iter + 1, e2(du).c_str(), e2(dp).c_str());
+        break;
+      }
     }
     prev_u = du;
     prev_p = dp;

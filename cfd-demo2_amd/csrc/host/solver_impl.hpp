@@ -339,6 +339,8 @@ struct Solver {
   float residual_into_v0_blocking();
   void check_evolution();
   void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
+  // cfg.log_level >= 1: the reference's println! progress lines, on stderr, rank 0
+  void log(const char* fmt, ...) const __attribute__((format(printf, 2, 3)));
   CoupledMatrix cmat() const;
   // per-cell vectors: allocation with ghost space, owned-base pointers
   template <class T>

@@ -115,8 +115,9 @@ typedef struct cfd_config {
   int32_t max_outer_restarts; /* 20  (coupled_solver_fgmres.rs:1738)                   */
   float fgmres_rtol;          /* 1e-5                                                   */
   float fgmres_atol;          /* 1e-7                                                   */
-  int32_t log_level;          /* 0 silent, 1 reference println! lines to stderr        */
-  int32_t use_graphs;         /* capture the fixed-schedule inner solve in a hipGraph   */
+  int32_t log_level;          /* 0 silent; 1 the reference's println! progress lines
+                                 (coupled_solver.rs, coupled_solver_fgmres.rs) on stderr,
+                                 rank 0 only                                             */
   int32_t amg_rebuild_interval; /* 0: AMG hierarchy frozen after the first AMG solve
                                    (reference, amg.rs); k > 0: rebuilt from the current
                                    matrix every k steps (opt-in deviation) */

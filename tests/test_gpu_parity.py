@@ -451,3 +451,30 @@ def test_amg_refresh_matches_full_rebuild(monkeypatch):
     for k, (a, b) in enumerate(zip(runs["1"], runs["0"])):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), f"step {k} fields"
         assert a[2] == b[2], f"step {k} AMG level digests"
+
+
+def test_log_level_reference_lines(capfd):
+    """cfg.log_level = 1 prints the reference's progress lines (coupled_solver.rs:126,333,434;
+    coupled_solver_fgmres.rs:1897,2264,2430) on stderr, with Rust's {:.2e} formatting."""
+    import re
+    mesh = backwards_step()
+    g = GpuSolver(mesh, config=default_config(log_level=1))
+    _setup_amg_test(g, mesh, 1)
+    capfd.readouterr()
+    g.step()
+    err = capfd.readouterr().err
+    info = g.step_info()
+    assert "Coupled Iteration: 1\n" in err
+    assert f"Coupled Iteration: {info.outer_iterations}\n" in err
+    assert "FGMRES: Initial residual = " in err or "FGMRES: Initial guess already converged" in err
+    solves = re.findall(r"Coupled linear solve: (\d+) iterations, residual (\S+), converged=(true|false)", err)
+    assert len(solves) == info.outer_iterations
+    last = solves[-1]
+    assert int(last[0]) == info.stats_p.iterations
+    assert re.fullmatch(r"-?\d\.\d\de-?\d+", last[1]), last[1]  # 1.23e-5, never 1.23e-05
+    assert float(last[1]) == pytest.approx(info.stats_p.residual, rel=6e-3)
+    quiet = GpuSolver(mesh)
+    _setup_amg_test(quiet, mesh, 1)
+    capfd.readouterr()
+    quiet.step()
+    assert capfd.readouterr().err == ""
