@@ -219,8 +219,10 @@ def main():
     log(f"[rank {rank}] solver created in {time.perf_counter() - t0:.1f}s (owns {n_cells} cells)")
 
     def barrier_sync():
-        # solver.step() returns after its blocking check_evolution read, so the
-        # library's stream is idle here; the barrier lines the ranks up
+        # device fence (the torch.cuda.synchronize() of the contract: the
+        # solver's own HIP device sync; torch never touches the GPU here), then
+        # the barrier lines the ranks up
+        solver.synchronize()
         if dist is not None:
             dist.barrier()
 

@@ -43,7 +43,7 @@ def _bind():
         getattr(L, n).argtypes = [_vp, C.c_float]
     for n in ("cfd_set_scheme", "cfd_set_time_scheme", "cfd_set_precond_type"):
         getattr(L, n).argtypes = [_vp, C.c_uint32]
-    for n in ("cfd_update_constants", "cfd_initialize_history", "cfd_step"):
+    for n in ("cfd_update_constants", "cfd_initialize_history", "cfd_step", "cfd_synchronize"):
         getattr(L, n).argtypes = [_vp]
     L.cfd_get_step_info.argtypes = [_vp, C.POINTER(_ffi.StepInfo)]
     L.cfd_num_cells.argtypes = [_vp]
@@ -231,6 +231,7 @@ class GpuSolver:
 
     def initialize_history(self): self._call("cfd_initialize_history")
     def step(self): self._call("cfd_step")
+    def synchronize(self): self._call("cfd_synchronize")
 
     # set_u / set_p take GLOBAL arrays (a distributed rank keeps its cells + ghosts)
     def _global_len(self):
@@ -352,7 +353,7 @@ class GpuGroup:
     def __getattr__(self, name):
         # setters / state writers apply to every rank
         if name.startswith("set_") or name in ("update_constants", "initialize_history",
-                                               "profile_enable", "profile_reset"):
+                                               "profile_enable", "profile_reset", "synchronize"):
             def f(*a, **k):
                 for r in self.ranks:
                     getattr(r, name)(*a, **k)

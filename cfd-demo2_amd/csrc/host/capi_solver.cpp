@@ -146,6 +146,13 @@ cfd_status cfd_step(cfd_solver* s) {
   CHECK_S(s);
   return guard([&] { s->s->step(); });
 }
+cfd_status cfd_synchronize(cfd_solver* s) {
+  CHECK_S(s);
+  return guard([&] {
+    CFD_HIP(hipSetDevice(s->s->device));
+    CFD_HIP(hipDeviceSynchronize());
+  });
+}
 cfd_status cfd_get_u(cfd_solver* s, double* uv) {
   CHECK_S(s);
   if (!uv) return set_error(CFD_ERR_INVALID, "null out");

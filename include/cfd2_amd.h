@@ -173,6 +173,9 @@ cfd_status cfd_update_constants(cfd_solver* s);
 cfd_status cfd_initialize_history(cfd_solver* s);
 /* solver.rs:242 -> coupled_solver.rs:33-499                                  */
 cfd_status cfd_step(cfd_solver* s);
+/* Waits until the handle's GPU is idle (hipDeviceSynchronize on its device):
+ * the timing fence bench.py puts on both sides of the timed steps.          */
+cfd_status cfd_synchronize(cfd_solver* s);
 /* solver.rs:97-128 (blocking)                                               */
 cfd_status cfd_get_u(cfd_solver* s, double* uv /* [2N] */);
 cfd_status cfd_get_p(cfd_solver* s, double* p /* [N] */);
