@@ -126,7 +126,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # gloo announces its connections on fd 1; keep stdout for the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     import numpy as np  # noqa: F401
     from cfd2_amd import GpuSolver, default_config, dist_unique_id
