@@ -194,3 +194,31 @@ def test_group_amg_rebuild_interval(refresh, replicate_rows, monkeypatch):
         _assert_same_fields(g, o, f"R=2 rebuild step {k}")
         _assert_same_info(g, o, f"R=2 rebuild step {k}")
     g.close()
+
+
+@pytest.mark.parametrize("nranks,which", [(2, "amg_test"), (3, "channel"), (4, "c1")])
+def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
+    """The interior/boundary split that hides every halo exchange behind the
+    interior rows (Solver::overlapped; production: >= 1M rows per rank, so no
+    other test reaches it) forced on for every level with >= 64 rows:
+    bit-exact vs oracle(R)."""
+    monkeypatch.setenv("CFD_OVERLAP_MIN_ROWS", "64")
+    replicate_rows(50 if which != "c1" else 4096)
+    if which == "c1":
+        mesh = bench_mesh(0.001723, 100)
+        cfg = dict(fixed_outer=1, fixed_inner=6)
+    else:
+        mesh = backwards_step() if which == "amg_test" else channel_obstacle(h=0.03)
+        cfg = dict(fixed_outer=3, fixed_inner=10)
+    g = GpuGroup(mesh, nranks, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+        s.set_scheme(1)  # SOU: neighbour gradients through the halo
+        s.update_constants()
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"overlapped R={nranks} {which} step {k}")
+        _assert_same_info(g, o, f"overlapped R={nranks} {which} step {k}")
+    g.close()

@@ -29,10 +29,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_multiprocess_host_transport_parity(nranks, tmp_path):
+@pytest.mark.parametrize("nranks,overlap", [(2, False), (3, False), (2, True)])
+def test_multiprocess_host_transport_parity(nranks, overlap, tmp_path):
     steps = 3
     env = dict(os.environ, CFD_AMG_REPLICATE_ROWS="50", MASTER_ADDR="127.0.0.1")
+    if overlap:  # the interior/boundary split of every halo'd launch (production: >= 1M rows per rank)
+        env["CFD_OVERLAP_MIN_ROWS"] = "64"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(ROOT, "tests", "mp_worker.py"), str(tmp_path), str(steps), str(tmp_path / "state.bin")]
