@@ -222,3 +222,25 @@ def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
         _assert_same_fields(g, o, f"overlapped R={nranks} {which} step {k}")
         _assert_same_info(g, o, f"overlapped R={nranks} {which} step {k}")
     g.close()
+
+
+@pytest.mark.parametrize("env", [{"CFD_HALO_PACK": "1"}, {"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_group_variants_parity(env, replicate_rows, monkeypatch):
+    """Distributed runs through the packed halo path and the alternative AMG
+    kernel paths: bit-exact vs oracle(R)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    replicate_rows(50)
+    mesh = backwards_step()
+    cfg = dict(fixed_outer=3, fixed_inner=10)
+    g = GpuGroup(mesh, 3, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=3)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"{env} step {k}")
+        _assert_same_info(g, o, f"{env} step {k}")
+    g.close()

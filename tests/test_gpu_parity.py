@@ -478,3 +478,36 @@ def test_log_level_reference_lines(capfd):
     capfd.readouterr()
     quiet.step()
     assert capfd.readouterr().err == ""
+
+
+VARIANTS = [
+    {"CFD_AMG_FULL": "0"},            # predicated slot loads (production: coarse levels > 2^19 rows)
+    {"CFD_AMG_FULL": "1"},            # unconditional slot loads on every level
+    {"CFD_AMG_TAIL_BLOB": "0"},       # LDS tail with vectors only
+    {"CFD_AMG_TAIL_LDS": "0"},        # global-memory single-workgroup tail
+    {"CFD_AMG_TAIL_ROWS": "0"},       # no tail kernel: every level launched
+    {"CFD_AMG_FUSE_PRESMOOTH": "0"},  # coarse pre-smoother as its own sweep
+]
+
+
+@pytest.mark.parametrize("env", VARIANTS, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+@pytest.mark.parametrize("mesh_name", ["amg_test", "graded"])
+def test_amg_kernel_variants_parity(env, mesh_name, monkeypatch):
+    """Every V-cycle code path the level sizes select in production (some only
+    at 10 M cells) forced on a small mesh: GPU == oracle bit-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if mesh_name == "amg_test":
+        mesh = backwards_step()
+    else:
+        from cfd2_amd.mesh import ChannelWithObstacle, generate_cut_cell_mesh
+        geo = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.5), obstacle_radius=0.15)
+        mesh = generate_cut_cell_mesh(geo, 0.02, 0.08, 1.2, (3.0, 1.0))
+    g, o = _pair(mesh, fixed_outer=3, fixed_inner=10)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"{env} {mesh_name} step {k}")
+        _assert_same_info(g, o, f"{env} {mesh_name} step {k}")
