@@ -511,3 +511,51 @@ def test_amg_kernel_variants_parity(env, mesh_name, monkeypatch):
         o.step()
         _assert_same_fields(g, o, f"{env} {mesh_name} step {k}")
         _assert_same_info(g, o, f"{env} {mesh_name} step {k}")
+
+
+def test_midrun_api_changes_parity():
+    """The reference API used mid-run the way the GUI does (src/ui/app.rs):
+    dt / viscosity / scheme / time-scheme / preconditioner switches, a direct
+    `constants` write, set_u and set_p clobbers and initialize_history between
+    steps -- GPU == oracle bit-exact after every step."""
+    mesh = channel_obstacle(h=0.04)
+    g, o = _pair(mesh)
+    a = mesh.arrays()
+    n = mesh.num_cells()
+    u0 = np.zeros((n, 2))
+    u0[a["cell_cx"] < 0.05, 0] = 1.0
+
+    def actions(s, k):
+        if k == 0:
+            s.set_dt(0.005)
+            s.set_viscosity(0.01)
+            s.set_density(1.0)
+            s.set_u(u0)
+            s.initialize_history()
+            s.set_precond_type(1)
+        elif k == 2:
+            s.set_scheme(1)
+            s.set_dt(0.004)  # dt_old keeps the previous dt (solver.rs:36-44)
+        elif k == 3:
+            s.set_time_scheme(1)
+            s.set_precond_type(0)  # Jacobi; the frozen AMG hierarchy stays built
+        elif k == 4:
+            s.set_precond_type(1)
+            c = s.constants
+            c.alpha_u = 0.8
+            c.inlet_velocity = 1.5
+            s.constants = c
+        elif k == 5:
+            s.set_p(0.1 * a["cell_cx"])  # clobbers u, d_p, grad_p too (solver.rs:23-34)
+        elif k == 6:
+            s.set_u(np.column_stack([0.5 + 0.0 * a["cell_cx"], 0.0 * a["cell_cx"]]))
+            s.set_scheme(2)
+        s.update_constants()
+
+    for k in range(8):
+        for s in (g, o):
+            actions(s, k)
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"mid-run step {k}")
+        _assert_same_info(g, o, f"mid-run step {k}")
