@@ -130,6 +130,15 @@ class Mesh:
         n = nv.value
         return _np(vx, n, np.float64), _np(vy, n, np.float64), _np(vf, n, np.uint8).astype(bool)
 
+    def topology(self) -> dict:
+        """face_v1, face_v2, cell_vertex_offsets, cell_vertices (CCW polygons)."""
+        p = [C.POINTER(C.c_uint32)() for _ in range(4)]
+        _ffi.check(_ffi.lib().cfd_mesh_get_topology(self._h, *[C.byref(q) for q in p]), "cfd_mesh_get_topology")
+        nf, n = self.num_faces(), self.num_cells()
+        offs = _np(p[2], n + 1, np.uint32)
+        return dict(face_v1=_np(p[0], nf, np.uint32), face_v2=_np(p[1], nf, np.uint32), cell_vertex_offsets=offs,
+                    cell_vertices=_np(p[3], int(offs[-1]) if n else 0, np.uint32))
+
     def smooth(self, geo, target_skew: float, max_iterations: int) -> int:
         it = C.c_int32()
         g = geo._geo()
@@ -159,6 +168,18 @@ def generate_cut_cell_mesh(geo, min_cell_size: float, max_cell_size: float, grow
                                                      growth_rate, float(domain_size[0]),
                                                      float(domain_size[1]), C.byref(h)),
                "cfd_mesh_generate_cut_cell")
+    return Mesh(h.value)
+
+
+def generate_voronoi_mesh(geo, min_cell_size: float, max_cell_size: float, growth_rate: float,
+                          domain_size, seed: int = 12345) -> Mesh:
+    """voronoi.rs:23 (seeded restatement: same seed, same mesh)."""
+    h = C.c_void_p()
+    g = geo._geo()
+    _ffi.check(_ffi.lib().cfd_mesh_generate_voronoi(C.byref(g), min_cell_size, max_cell_size, growth_rate,
+                                                    float(domain_size[0]), float(domain_size[1]),
+                                                    int(seed), C.byref(h)),
+               "cfd_mesh_generate_voronoi")
     return Mesh(h.value)
 
 

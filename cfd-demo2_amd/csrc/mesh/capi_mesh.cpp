@@ -1,6 +1,7 @@
 // C ABI for the host mesh: generation, smoothing, view, binary dump/load.
 #include <cstdio>
 #include <cstring>
+#include <stdexcept>
 #include <exception>
 #include <string>
 
@@ -57,6 +58,31 @@ cfd_status cfd_mesh_generate_cut_cell(const cfd_geometry* geo, double min_cell_s
   }
 }
 
+cfd_status cfd_mesh_generate_voronoi(const cfd_geometry* geo, double min_cell_size, double max_cell_size,
+                                     double growth_rate, double domain_x, double domain_y, uint64_t seed,
+                                     cfd_mesh** out) {
+  if (!out) return set_error(CFD_ERR_INVALID, "out is null");
+  cfd2::Geometry g;
+  if (!to_geo(geo, &g)) return set_error(CFD_ERR_INVALID, "bad geometry");
+  if (!(min_cell_size > 0) || !(max_cell_size >= min_cell_size) || !(domain_x > 0) || !(domain_y > 0))
+    return set_error(CFD_ERR_INVALID, "cell sizes and domain must be positive, max >= min");
+  try {
+    auto* m = new cfd_mesh;
+    try {
+      m->m = cfd2::generate_voronoi_mesh(g, min_cell_size, max_cell_size, growth_rate, domain_x, domain_y, seed);
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = m;
+    return CFD_OK;
+  } catch (const std::invalid_argument& e) {
+    return set_error(CFD_ERR_INVALID, e.what());
+  } catch (const std::exception& e) {
+    return set_error(CFD_ERR_INTERNAL, e.what());
+  }
+}
+
 cfd_status cfd_mesh_smooth(cfd_mesh* m, const cfd_geometry* geo, double target_skew,
                            int32_t max_iterations, int32_t* iters) {
   cfd2::Geometry g;
@@ -100,6 +126,16 @@ cfd_status cfd_mesh_get_vertices(const cfd_mesh* m, uint32_t* nv, const double**
   if (vx) *vx = m->m.vx.data();
   if (vy) *vy = m->m.vy.data();
   if (vf) *vf = m->m.v_fixed.data();
+  return CFD_OK;
+}
+
+cfd_status cfd_mesh_get_topology(const cfd_mesh* m, const uint32_t** face_v1, const uint32_t** face_v2,
+                                 const uint32_t** cell_vertex_offsets, const uint32_t** cell_vertices) {
+  if (!m) return set_error(CFD_ERR_INVALID, "null");
+  if (face_v1) *face_v1 = m->m.face_v1.data();
+  if (face_v2) *face_v2 = m->m.face_v2.data();
+  if (cell_vertex_offsets) *cell_vertex_offsets = m->m.cell_vertex_offsets.data();
+  if (cell_vertices) *cell_vertices = m->m.cell_vertices.data();
   return CFD_OK;
 }
 

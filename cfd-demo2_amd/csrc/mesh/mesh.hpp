@@ -55,5 +55,8 @@ static constexpr uint32_t kNoNeighbor = 0xFFFFFFFFu;
 
 Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double max_cell_size,
                             double growth_rate, double domain_x, double domain_y);
+// seeded restatement of generate_voronoi_mesh (voronoi.rs:23; voronoi.cpp)
+Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
+                           double domain_x, double domain_y, uint64_t seed);
 
 }  // namespace cfd2

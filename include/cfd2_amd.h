@@ -71,6 +71,14 @@ typedef struct cfd_mesh cfd_mesh; /* owned host mesh */
 cfd_status cfd_mesh_generate_cut_cell(const cfd_geometry* geo, double min_cell_size,
                                       double max_cell_size, double growth_rate,
                                       double domain_x, double domain_y, cfd_mesh** out);
+/* generate_voronoi_mesh (src/solver/mesh/voronoi.rs:23, delaunay.rs): a
+ * behavioural restatement with a SEEDED generator (the reference's
+ * thread_rng is unseeded): Poisson-disk generators graded like the cut-cell
+ * sizing, Bowyer-Watson Delaunay, 20 generator-smoothing sweeps, polygonal
+ * dual cells.  Same seed and arguments: the same mesh.  Geometry kinds 0-3. */
+cfd_status cfd_mesh_generate_voronoi(const cfd_geometry* geo, double min_cell_size,
+                                     double max_cell_size, double growth_rate, double domain_x,
+                                     double domain_y, uint64_t seed, cfd_mesh** out);
 /* Mesh::smooth (structs.rs:159-292); returns iterations done in *iters.     */
 cfd_status cfd_mesh_smooth(cfd_mesh* m, const cfd_geometry* geo, double target_skew,
                            int32_t max_iterations, int32_t* iters);
@@ -81,6 +89,10 @@ cfd_status cfd_mesh_get_view(const cfd_mesh* m, cfd_mesh_view* out);
 /* Vertex arrays (vx, vy, v_fixed) for mesh-validity tests.                  */
 cfd_status cfd_mesh_get_vertices(const cfd_mesh* m, uint32_t* num_vertices, const double** vx,
                                  const double** vy, const uint8_t** v_fixed);
+/* Vertex topology (structs.rs face_v1/face_v2, cell_vertex_offsets[N+1],
+ * cell_vertices: CCW polygon of each cell) for mesh-validity tests.        */
+cfd_status cfd_mesh_get_topology(const cfd_mesh* m, const uint32_t** face_v1, const uint32_t** face_v2,
+                                 const uint32_t** cell_vertex_offsets, const uint32_t** cell_vertices);
 /* Binary SoA dump / load.                              */
 cfd_status cfd_mesh_save(const cfd_mesh* m, const char* path);
 cfd_status cfd_mesh_load(const char* path, cfd_mesh** out);
