@@ -142,7 +142,7 @@ def default_config(**overrides) -> Config:
 # Every symbol include/cfd2_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
     "cfd_last_error",
-    "cfd_mesh_generate_cut_cell", "cfd_mesh_generate_voronoi", "cfd_mesh_get_topology", "cfd_mesh_smooth", "cfd_mesh_max_skewness", "cfd_mesh_get_view",
+    "cfd_mesh_generate_cut_cell", "cfd_mesh_generate_voronoi", "cfd_mesh_generate_delaunay", "cfd_mesh_get_topology", "cfd_mesh_smooth", "cfd_mesh_max_skewness", "cfd_mesh_get_view",
     "cfd_mesh_get_vertices", "cfd_mesh_save", "cfd_mesh_load", "cfd_mesh_destroy",
     "cfd_config_default", "cfd_solver_create", "cfd_solver_destroy", "cfd_set_u", "cfd_set_p",
     "cfd_get_constants", "cfd_set_constants", "cfd_set_dt", "cfd_set_viscosity", "cfd_set_alpha_p",
@@ -176,8 +176,9 @@ def lib() -> C.CDLL:
                                              C.c_double, C.c_double, C.POINTER(vp)]
     u32pp = C.POINTER(C.POINTER(C.c_uint32))
     L.cfd_mesh_get_topology.argtypes = [vp, u32pp, u32pp, u32pp, u32pp]
-    L.cfd_mesh_generate_voronoi.argtypes = [C.POINTER(Geometry), C.c_double, C.c_double, C.c_double,
-                                            C.c_double, C.c_double, C.c_uint64, C.POINTER(vp)]
+    for fn in (L.cfd_mesh_generate_voronoi, L.cfd_mesh_generate_delaunay):
+        fn.argtypes = [C.POINTER(Geometry), C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                       C.c_uint64, C.POINTER(vp)]
     L.cfd_mesh_smooth.argtypes = [vp, C.POINTER(Geometry), C.c_double, C.c_int32, C.POINTER(C.c_int32)]
     L.cfd_mesh_max_skewness.argtypes = [vp]
     L.cfd_mesh_max_skewness.restype = C.c_double

@@ -183,6 +183,18 @@ def generate_voronoi_mesh(geo, min_cell_size: float, max_cell_size: float, growt
     return Mesh(h.value)
 
 
+def generate_delaunay_mesh(geo, min_cell_size: float, max_cell_size: float, growth_rate: float,
+                           domain_size, seed: int = 12345) -> Mesh:
+    """delaunay.rs:732 (seeded restatement; triangle cells)."""
+    h = C.c_void_p()
+    g = geo._geo()
+    _ffi.check(_ffi.lib().cfd_mesh_generate_delaunay(C.byref(g), min_cell_size, max_cell_size, growth_rate,
+                                                     float(domain_size[0]), float(domain_size[1]),
+                                                     int(seed), C.byref(h)),
+               "cfd_mesh_generate_delaunay")
+    return Mesh(h.value)
+
+
 def channel_obstacle_h(target_cells: float) -> float:
     """Cell size h for a ~target_cells channel+obstacle mesh (N ≈ 2.9686/h²)."""
     return float(np.sqrt(2.9686 / target_cells))

@@ -83,6 +83,31 @@ cfd_status cfd_mesh_generate_voronoi(const cfd_geometry* geo, double min_cell_si
   }
 }
 
+cfd_status cfd_mesh_generate_delaunay(const cfd_geometry* geo, double min_cell_size, double max_cell_size,
+                                     double growth_rate, double domain_x, double domain_y, uint64_t seed,
+                                     cfd_mesh** out) {
+  if (!out) return set_error(CFD_ERR_INVALID, "out is null");
+  cfd2::Geometry g;
+  if (!to_geo(geo, &g)) return set_error(CFD_ERR_INVALID, "bad geometry");
+  if (!(min_cell_size > 0) || !(max_cell_size >= min_cell_size) || !(domain_x > 0) || !(domain_y > 0))
+    return set_error(CFD_ERR_INVALID, "cell sizes and domain must be positive, max >= min");
+  try {
+    auto* m = new cfd_mesh;
+    try {
+      m->m = cfd2::generate_delaunay_mesh(g, min_cell_size, max_cell_size, growth_rate, domain_x, domain_y, seed);
+    } catch (...) {
+      delete m;
+      throw;
+    }
+    *out = m;
+    return CFD_OK;
+  } catch (const std::invalid_argument& e) {
+    return set_error(CFD_ERR_INVALID, e.what());
+  } catch (const std::exception& e) {
+    return set_error(CFD_ERR_INTERNAL, e.what());
+  }
+}
+
 cfd_status cfd_mesh_smooth(cfd_mesh* m, const cfd_geometry* geo, double target_skew,
                            int32_t max_iterations, int32_t* iters) {
   cfd2::Geometry g;

@@ -58,5 +58,8 @@ Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double ma
 // seeded restatement of generate_voronoi_mesh (voronoi.rs:23; voronoi.cpp)
 Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
                            double domain_x, double domain_y, uint64_t seed);
+// seeded restatement of generate_delaunay_mesh (delaunay.rs:732; triangle cells)
+Mesh generate_delaunay_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
+                            double domain_x, double domain_y, uint64_t seed);
 
 }  // namespace cfd2

@@ -395,16 +395,16 @@ P dual_point(P a, P b, P c) {
   return g;
 }
 
-}  // namespace
 
-Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
-                           double domain_x, double domain_y, uint64_t seed) {
+// delaunay.rs triangulate (:125-193): generators, triangulation, smoothing
+void triangulate(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate, double domain_x,
+                 double domain_y, uint64_t seed, std::vector<P>& pts, std::vector<uint8_t>& fixed,
+                 std::vector<Tri>& T) {
   if (!(min_cell_size > 0.0) || !(max_cell_size >= min_cell_size) || !(domain_x > 0.0) || !(domain_y > 0.0))
     throw std::invalid_argument("voronoi mesher: bad sizes");
   const Sizing size{geo, min_cell_size, max_cell_size, growth_rate};
-  // 1. generators
-  std::vector<P> pts;
-  std::vector<uint8_t> fixed;
+  pts.clear();
+  fixed.clear();
   {
     std::map<std::pair<int64_t, int64_t>, size_t> seen;  // quantised de-duplication (delaunay.rs:137-149)
     for (const P& p : boundary_points(geo, min_cell_size)) {
@@ -435,12 +435,21 @@ Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max
     pts.swap(sp);
     fixed.swap(sf);
   }
-  // 2-3. triangulate, smooth the generators, re-triangulate
-  std::vector<Tri> T = keep_fluid(delaunay(pts, domain_x, domain_y), pts, fixed, geo);
+  T = keep_fluid(delaunay(pts, domain_x, domain_y), pts, fixed, geo);
   for (int it = 0; it < 20; ++it) {
     smooth_generators(pts, T, fixed, size);
     T = keep_fluid(delaunay(pts, domain_x, domain_y), pts, fixed, geo);
   }
+}
+
+}  // namespace
+
+Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
+                           double domain_x, double domain_y, uint64_t seed) {
+  std::vector<P> pts;
+  std::vector<uint8_t> fixed;
+  std::vector<Tri> T;
+  triangulate(geo, min_cell_size, max_cell_size, growth_rate, domain_x, domain_y, seed, pts, fixed, T);
   const size_t n = pts.size(), nt = T.size();
   // every generator must be used and every hull vertex must have exactly one fan
   std::vector<int64_t> first_tri(n, -1);
@@ -589,6 +598,70 @@ Mesh generate_voronoi_mesh(const Geometry& geo, double min_cell_size, double max
     m.cell_vol.push_back(0.0);
   }
   m.recalculate_geometry();
+  return m;
+}
+
+// generate_delaunay_mesh (delaunay.rs:732-846): the triangles themselves as
+// cells (centroid, area), one face per edge; a hull edge is a boundary face
+// typed by position (the reference leaves an unshared edge with a free end as
+// a face with neither neighbour nor boundary type; here every hull edge is a
+// boundary).  Normals point out of the owner, the first cell to use the edge.
+Mesh generate_delaunay_mesh(const Geometry& geo, double min_cell_size, double max_cell_size, double growth_rate,
+                            double domain_x, double domain_y, uint64_t seed) {
+  std::vector<P> pts;
+  std::vector<uint8_t> fixed;
+  std::vector<Tri> T;
+  triangulate(geo, min_cell_size, max_cell_size, growth_rate, domain_x, domain_y, seed, pts, fixed, T);
+  Mesh m;
+  for (size_t i = 0; i < pts.size(); ++i) {
+    m.vx.push_back(pts[i].x);
+    m.vy.push_back(pts[i].y);
+    m.v_fixed.push_back(fixed[i]);
+  }
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> edge_face;
+  m.cell_face_offsets.push_back(0);
+  m.cell_vertex_offsets.push_back(0);
+  for (size_t t = 0; t < T.size(); ++t) {
+    const uint32_t c = (uint32_t)t;
+    const P a = pts[T[t].v[0]], b = pts[T[t].v[1]], d = pts[T[t].v[2]];
+    m.cell_cx.push_back((a.x + b.x + d.x) / 3.0);
+    m.cell_cy.push_back((a.y + b.y + d.y) / 3.0);
+    m.cell_vol.push_back(0.5 * std::fabs((b.x - a.x) * (d.y - a.y) - (d.x - a.x) * (b.y - a.y)));
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t u = T[t].v[k], v = T[t].v[(k + 1) % 3];
+      const auto key = std::make_pair(std::min(u, v), std::max(u, v));
+      auto it = edge_face.find(key);
+      if (it != edge_face.end()) {
+        m.face_neighbor[it->second] = c;
+        m.face_boundary[it->second] = kNone;
+        m.cell_faces.push_back(it->second);
+        continue;
+      }
+      const uint32_t f = (uint32_t)m.face_cx.size();
+      const P pa = pts[key.first], pb = pts[key.second];
+      const double fx = (pa.x + pb.x) / 2.0, fy = (pa.y + pb.y) / 2.0, len = std::hypot(pb.x - pa.x, pb.y - pa.y);
+      double nx = (pb.y - pa.y) / len, ny = (pa.x - pb.x) / len;
+      if ((fx - m.cell_cx[c]) * nx + (fy - m.cell_cy[c]) * ny < 0.0) {
+        nx = -nx;
+        ny = -ny;
+      }
+      m.face_v1.push_back(key.first);
+      m.face_v2.push_back(key.second);
+      m.face_owner.push_back(c);
+      m.face_neighbor.push_back(kNoNeighbor);
+      m.face_boundary.push_back(fx < 1e-6 ? kInlet : std::fabs(fx - domain_x) < 1e-6 ? kOutlet : kWall);
+      m.face_nx.push_back(nx);
+      m.face_ny.push_back(ny);
+      m.face_area.push_back(len);
+      m.face_cx.push_back(fx);
+      m.face_cy.push_back(fy);
+      edge_face.emplace(key, f);
+      m.cell_faces.push_back(f);
+    }
+    m.cell_face_offsets.push_back((uint32_t)m.cell_faces.size());
+    for (int k = 0; k < 3; ++k) m.cell_vertices.push_back(T[t].v[k]);  // CCW
+    m.cell_vertex_offsets.push_back((uint32_t)m.cell_vertices.size());
+  }
   return m;
 }
 

@@ -79,6 +79,11 @@ cfd_status cfd_mesh_generate_cut_cell(const cfd_geometry* geo, double min_cell_s
 cfd_status cfd_mesh_generate_voronoi(const cfd_geometry* geo, double min_cell_size,
                                      double max_cell_size, double growth_rate, double domain_x,
                                      double domain_y, uint64_t seed, cfd_mesh** out);
+/* generate_delaunay_mesh (delaunay.rs:732): the same seeded triangulation
+ * with the triangles as cells.                                             */
+cfd_status cfd_mesh_generate_delaunay(const cfd_geometry* geo, double min_cell_size,
+                                      double max_cell_size, double growth_rate, double domain_x,
+                                      double domain_y, uint64_t seed, cfd_mesh** out);
 /* Mesh::smooth (structs.rs:159-292); returns iterations done in *iters.     */
 cfd_status cfd_mesh_smooth(cfd_mesh* m, const cfd_geometry* geo, double target_skew,
                            int32_t max_iterations, int32_t* iters);

@@ -9,7 +9,7 @@ import pytest
 
 from cfd2_amd import default_config
 from cfd2_amd.mesh import (BackwardsStep, ChannelWithObstacle, CircleObstacle, RectangularChannel,
-                           generate_voronoi_mesh)
+                           generate_delaunay_mesh, generate_voronoi_mesh)
 from tests.oracle_py import OracleSolver
 
 NONE = 0xFFFFFFFF
@@ -191,3 +191,40 @@ def test_native_voronoi_group_parity(nranks, monkeypatch):
         o.step()
         _assert_same_fields(g, o, f"native voronoi R={nranks} step {k}")
     g.close()
+
+
+@pytest.mark.parametrize("name", ["step", "channel"])
+def test_delaunay_mesh_validity(name):
+    """generate_delaunay_mesh (delaunay.rs:732): triangle cells, closed, fluid area."""
+    geo, mn, mx, gr, dom = CASES[name]
+    m = generate_delaunay_mesh(geo, mn, mx, gr, dom, seed=5)
+    a = m.arrays()
+    n = m.num_cells()
+    assert np.all(np.diff(a["cell_face_offsets"].astype(np.int64)) == 3)
+    assert a["cell_vol"].min() > 0.0
+    area = {"step": 1.75, "channel": 3.0 - np.pi * 0.04}[name]
+    assert abs(a["cell_vol"].sum() - area) < 0.02
+    own = a["face_owner"].astype(np.int64)
+    nb = a["face_neighbor"].astype(np.int64)
+    internal = nb != NONE
+    an = np.stack([a["face_area"] * a["face_nx"], a["face_area"] * a["face_ny"]], 1)
+    s = np.zeros((n, 2))
+    np.add.at(s, own, an)
+    np.add.at(s, nb[internal], -an[internal])
+    assert np.abs(s).max() < 1e-12
+    assert {1, 2, 3} <= set(np.unique(a["face_boundary"]).tolist())
+
+
+@pytest.mark.gpu
+def test_delaunay_mesh_gpu_parity():
+    from cfd2_amd import GpuSolver
+    from tests.test_gpu_parity import _assert_same_fields, _assert_same_info
+    m = generate_delaunay_mesh(CHANNEL, 0.03, 0.1, 1.2, (3.0, 1.0), seed=5)
+    g, o = GpuSolver(m), OracleSolver(m)
+    for s in (g, o):
+        _setup(s, 1, 1)
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"delaunay step {k}")
+        _assert_same_info(g, o, f"delaunay step {k}")
