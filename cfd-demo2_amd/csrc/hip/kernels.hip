@@ -18,10 +18,6 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ float wdistance(float ax, float ay, float bx, float by) {
-  const float dx = ax - bx, dy = ay - by;
-  return sqrtf(dx * dx + dy * dy);
-}
 __device__ __forceinline__ float wsmoothstep(float lo, float hi, float x) {
   const float t = fminf(fmaxf((x - lo) / (hi - lo), 0.0f), 1.0f);
   return t * t * (3.0f - 2.0f * t);

@@ -36,7 +36,7 @@ std::string e2(double v) {
   return s.substr(0, e) + "e" + (neg ? "-" : "") + s.substr(i);
 }
 const char* tf(bool b) { return b ? "true" : "false"; }
-constexpr int kScalBase = 0;   // dsc[0..15]: rhs_norm, resid, inv_resid, wnorm, inv_w, resid_est
+// device scalars dsc[0..15]: rhs_norm, resid, inv_resid, wnorm, inv_w, resid_est
 constexpr int kHOff = 16;
 }  // namespace
 
