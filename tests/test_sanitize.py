@@ -1,4 +1,4 @@
-"""Host sanitizers: the oracle and the product's host mesh code
+"""Host sanitizers: the oracle, the product's host mesh code
 (cut-cell, Voronoi, Delaunay generators) built with AddressSanitizer + UBSan
 (+ leak detection) straight from the sources and run on small meshes, one and
 three ranks (oracle/sanitize_main.cpp).  CPU only."""
@@ -25,3 +25,24 @@ def test_oracle_and_mesh_code_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert r.stdout.count(": ok") == 6, r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or not os.path.isdir("/opt/rocm/include"),
+                    reason="g++ / ROCm headers not available")
+def test_host_setup_code_under_asan_ubsan(tmp_path):
+    """The product's GPU-free host setup code: slab topology and halo plans for
+    1-4 ranks, the host AMG hierarchy (tests/native/sanitize_host.cpp)."""
+    exe = str(tmp_path / "sanitize_host")
+    srcs = [os.path.join(ROOT, p) for p in ("tests/native/sanitize_host.cpp", "cfd-demo2_amd/csrc/host/topology.cpp",
+                                            "cfd-demo2_amd/csrc/host/amg_setup.cpp", "cfd-demo2_amd/csrc/host/dist.cpp",
+                                            "cfd-demo2_amd/csrc/mesh/cut_cell.cpp",
+                                            "cfd-demo2_amd/csrc/mesh/voronoi.cpp")]
+    cmd = ["g++", "-O1", "-g", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fsanitize=address,undefined",
+           "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined", "-D__HIP_PLATFORM_AMD__",
+           "-I/opt/rocm/include", *srcs, "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count(": ok") == 12, r.stdout
