@@ -74,6 +74,7 @@ void pwrite_all(int fd, const void* p, size_t bytes, uint64_t off) {
 }  // namespace
 
 void Solver::save_state(const char* path) {
+  const Range range("state save");
   CFD_HIP(hipSetDevice(device));
   sync();
   // collective: every rank learns the AMG source size and its value offset
@@ -168,6 +169,7 @@ void Solver::save_state(const char* path) {
 }
 
 void Solver::load_state(const char* path) {
+  const Range range("state load");
   CFD_HIP(hipSetDevice(device));
   const int fd = ::open(path, O_RDONLY);
   if (fd < 0) throw std::invalid_argument(std::string("state load: cannot open ") + path + ": " + std::strerror(errno));

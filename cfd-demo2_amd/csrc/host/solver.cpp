@@ -727,12 +727,14 @@ void Solver::drop_amg() {
 void Solver::ensure_amg() {
   if (amg_built) {
     if (amg_refresh_pending) {
+      const Range range("amg refresh");
       refresh_amg();
       amg_refresh_pending = false;
       amg_age = 0;
     }
     return;
   }
+  const Range range("amg setup");
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
   const auto t_start = std::chrono::steady_clock::now();
   const char* se = std::getenv("CFD_AMG_SETUP");
@@ -1125,6 +1127,7 @@ float Solver::residual_into_v0_blocking() {
 }
 
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
+  const Range range("fgmres solve");
   cfd_linear_stats st{};
   const size_t n = 3 * (size_t)N;
   const float tol = cfg.fgmres_rtol, abstol = cfg.fgmres_atol;
@@ -1158,6 +1161,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   for (int outer = 0; outer < outer_max; ++outer) {
     int basis_size = 0;
     for (int j = 0; j < inner_max; ++j) {
+      const Range it_range("fgmres iteration");
       basis_size = j + 1;
       ++total;
       float* zj = zvec + (size_t)j * stride;
@@ -1360,6 +1364,7 @@ void Solver::check_evolution() {
 }
 
 void Solver::step() {  // coupled_solver.rs:33-499
+  const Range range("cfd step");
   CFD_HIP(hipSetDevice(device));
   // opt-in deviation from the frozen hierarchy
   if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) {
@@ -1384,6 +1389,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
   int pend = -1;
   info.total_linear_iterations = 0;
   for (int iter = 0; iter < max_iters; ++iter) {
+    const Range outer_range("picard iteration");
     log("Coupled Iteration: %d\n", iter + 1);
     if (iter > 0 || constants.scheme != 0) prepare();
     assemble();

@@ -1,6 +1,7 @@
 // Host-side driver state of the HIP solver (one instance per GPU handle).
 #pragma once
 #include <hip/hip_runtime_api.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -62,6 +63,15 @@ class DeviceArena {
  private:
   std::vector<void*> ptrs_;
   size_t bytes_ = 0;
+};
+
+// roctx range (rocprofv3 --marker-trace shows steps, Picard iterations,
+// FGMRES solves and iterations, AMG setup / refresh, checkpoint I/O)
+struct Range {
+  explicit Range(const char* what) { roctxRangePushA(what); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
 };
 
 struct HostCsr {
