@@ -306,7 +306,8 @@ def main():
             "traffic": load_traffic(args.round, args.config, world if args.inproc_ranks <= 1 else args.inproc_ranks),
             "bytes_per_launch": sm_bytes,
             "avg_launch_us": sm_avg_s * 1e6,
-            "launches": sm_n,
+            "launches": sm_n,  # timed sweeps: every sample_stride-th level-0 sweep of the timed steps
+            "sample_stride": max(1, int(os.environ.get("CFD_PROF_STRIDE", "1"))),
         },
         "step_algorithmic_gbs": step_bytes / (ms_per_step / 1e3) / 1e9,
         "linear_iterations_last_step": int(info.total_linear_iterations),

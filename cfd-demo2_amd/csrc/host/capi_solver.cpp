@@ -1,6 +1,8 @@
 // C ABI of the solver (include/cfd2_amd.h).  Each entry replaces one method of
 // the reference's `impl GpuSolver` (src/solver/gpu/solver.rs, init/mod.rs);
 // exceptions become status codes (the reference panics).
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -199,6 +201,9 @@ cfd_status cfd_profile_reset(cfd_solver* s) {
     s->s->prof_used = 0;
     s->s->prof_ms = 0.0;
     s->s->prof_launches = 0;
+    s->s->prof_seq = 0;
+    const char* ps = std::getenv("CFD_PROF_STRIDE");
+    s->s->prof_stride = ps ? std::max(1u, (uint32_t)std::strtoul(ps, nullptr, 10)) : 1u;
     s->s->prof_grow(8192);  // 4096 timed launches without growing inside the timed steps
   });
 }

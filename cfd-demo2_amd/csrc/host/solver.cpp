@@ -954,7 +954,7 @@ void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {
   AmgGpuLevel& L = levels[li];
   if (x_zero) {
     launch_amg_smooth_zero(L.dev, b, L.xt, stream);
-  } else if (prof && li == 0) {
+  } else if (li == 0 && prof_take()) {
     const auto ev = prof_pair();
     launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second);
     prof_launches++;
@@ -985,7 +985,7 @@ void Solver::v_cycle() {
       amg_smooth(i, Lv.x, Lv.b, x_zero);
       return;
     }
-    const bool timed = prof && i == 0;  // kernel time only: each part timed separately
+    const bool timed = i == 0 && prof_take();  // kernel time only: each part timed separately
     overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;

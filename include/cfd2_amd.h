@@ -251,8 +251,9 @@ cfd_status cfd_group_state_save(cfd_solver* const* handles, int32_t nranks, cons
  * AMG smoother sweep, on the solver's own stream.                            */
 cfd_status cfd_profile_enable(cfd_solver* s, int32_t enable);
 cfd_status cfd_profile_reset(cfd_solver* s);
-/* total_ms / launches for the level-0 smoother; bytes = algorithmic bytes per
- * sweep (4(n+1) + 8 nnz + 12 n).                              */
+/* total_ms / launches over the TIMED level-0 smoother sweeps (every
+ * CFD_PROF_STRIDE-th sweep, default 1, from cfd_profile_reset on); bytes =
+ * algorithmic bytes per sweep (4(n+1) + 8 nnz + 12 n).       */
 cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t* launches,
                                 double* bytes_per_launch);
 /* AMG hierarchy summary: number of levels and rows/nnz per level.            */
