@@ -559,3 +559,26 @@ def test_midrun_api_changes_parity():
         o.step()
         _assert_same_fields(g, o, f"mid-run step {k}")
         _assert_same_info(g, o, f"mid-run step {k}")
+
+
+@pytest.mark.parametrize("inlet", [0.0, 1.0])
+def test_fixed_schedule_early_exits(inlet):
+    """Fixed schedule with the solve's early exits (coupled_solver_fgmres.rs
+    rhs / initial-residual checks, kept under the fixed schedule): with a zero
+    state and no inflow every solve exits early (rhs = 0); with inflow the
+    t = 0 step exits early and the rest run.  GPU == oracle bit-exact, step
+    statistics included."""
+    mesh = channel_obstacle(h=0.04)
+    g, o = _pair(mesh, fixed_outer=2, fixed_inner=8)
+    for s in (g, o):
+        s.set_dt(1e-3)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_inlet_velocity(inlet)
+        s.set_precond_type(1)
+        s.initialize_history()
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"inlet={inlet} step {k}")
+        _assert_same_info(g, o, f"inlet={inlet} step {k}")
