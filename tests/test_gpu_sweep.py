@@ -2,6 +2,7 @@
 rectangular channel, graded meshes with hanging faces), random physics and
 solver settings, 1-3 ranks -- the HIP path must equal the oracle bit for bit
 on every case.  Each case is a few thousand cells and two or three steps."""
+import os
 import random
 
 import numpy as np
@@ -69,7 +70,7 @@ def _setup(s, mesh, phys, useed):
     s.update_constants()
 
 
-@pytest.mark.parametrize("seed", range(32))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
     kind, mesh, cfg, phys, nranks, useed = _case(seed)
     monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "200")  # distributed coarse levels on these small meshes
