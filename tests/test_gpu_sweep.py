@@ -1,5 +1,6 @@
 """Seeded parity sweep: random geometries (backwards step, channel + obstacle,
-rectangular channel, graded meshes with hanging faces), random physics and
+rectangular channel, graded meshes with hanging faces; cut-cell, seeded
+Voronoi and Delaunay meshes), random physics and
 solver settings, 1-3 ranks -- the HIP path must equal the oracle bit for bit
 on every case.  Each case is a few thousand cells and two or three steps."""
 import os
@@ -9,7 +10,8 @@ import numpy as np
 import pytest
 
 from cfd2_amd import GpuGroup, GpuSolver, default_config
-from cfd2_amd.mesh import BackwardsStep, ChannelWithObstacle, RectangularChannel, generate_cut_cell_mesh
+from cfd2_amd.mesh import (BackwardsStep, ChannelWithObstacle, RectangularChannel, generate_cut_cell_mesh,
+                           generate_delaunay_mesh, generate_voronoi_mesh)
 from tests.oracle_py import OracleSolver
 from tests.test_gpu_parity import _assert_same_fields, _assert_same_info
 
@@ -18,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 def _case(seed):
     rng = random.Random(seed)
-    kind = rng.choice(["step", "obstacle", "rect", "graded"])
+    kind = rng.choice(["step", "obstacle", "rect", "graded", "voronoi", "delaunay"])
     h = rng.uniform(0.045, 0.07)
     mn = mx = h
     if kind == "step":
@@ -30,6 +32,11 @@ def _case(seed):
         length = rng.uniform(1.0, 3.0)
         geo = RectangularChannel(length=length, height=1.0)
         dom = (length, 1.0)
+    elif kind in ("voronoi", "delaunay") and rng.random() < 0.5:
+        length = rng.uniform(1.5, 3.0)
+        geo = BackwardsStep(length=length, height_inlet=rng.uniform(0.3, 0.7), height_outlet=1.0,
+                            step_x=rng.uniform(0.3, 1.0))
+        dom = (length, 1.0)
     else:
         geo = ChannelWithObstacle(length=3.0, height=1.0,
                                   obstacle_center=(rng.uniform(0.6, 1.6), rng.uniform(0.35, 0.65)),
@@ -37,7 +44,11 @@ def _case(seed):
         dom = (3.0, 1.0)
         if kind == "graded":  # quadtree refinement towards the obstacle: hanging faces, 5+-face cells
             mn, mx = h * 0.5, h * 2.0
-    mesh = generate_cut_cell_mesh(geo, mn, mx, 1.2, dom)
+    if kind in ("voronoi", "delaunay"):  # seeded polygonal / triangle meshes (voronoi.cpp)
+        gen = generate_voronoi_mesh if kind == "voronoi" else generate_delaunay_mesh
+        mesh = gen(geo, h * 0.8, h * 2.0, 1.2, dom, seed=rng.randrange(1 << 20))
+    else:
+        mesh = generate_cut_cell_mesh(geo, mn, mx, 1.2, dom)
     mesh.smooth(geo, 0.3, rng.choice([0, 20]))
     cfg = dict(convergence_lag=rng.choice([0, 1]))
     if rng.random() < 0.6:
