@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def _case(seed):
     rng = random.Random(seed)
     kind = rng.choice(["step", "obstacle", "rect", "graded", "voronoi", "delaunay"])
-    h = rng.uniform(0.045, 0.07)
+    h = rng.uniform(0.045, 0.07) * float(os.environ.get("CFD_SWEEP_H_SCALE", "1"))  # < 1: bigger meshes
     mn = mx = h
     if kind == "step":
         length = rng.uniform(2.0, 3.5)
@@ -58,7 +58,7 @@ def _case(seed):
     phys = dict(dt=rng.choice([1e-3, 5e-3, 1e-2]), nu=rng.choice([1e-3, 1e-2]), scheme=rng.choice([0, 1, 2]),
                 time_scheme=rng.choice([0, 1]), precond=rng.choice([0, 1, 1]), alpha_u=rng.choice([0.7, 0.9]),
                 alpha_p=rng.choice([0.3, 0.9]))
-    nranks = rng.choice([1, 1, 2, 3])
+    nranks = rng.choice([1, 1, 2, 3] + ([4, 6, 8] if os.environ.get("CFD_SWEEP_MANY_RANKS") else []))
     return kind, mesh, cfg, phys, nranks, rng.randrange(1 << 30)
 
 
