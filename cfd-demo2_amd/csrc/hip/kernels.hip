@@ -40,19 +40,43 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // deals blocks round-robin over the 8 XCDs; remapping gives XCD k a contiguous
 // range of rows, so the i +- n_y neighbour gathers of a structured-ish cut-cell
 // mesh hit that XCD's L2.  Bijective for any grid size; a speed choice only.
+// REV: each XCD walks its range from the top down.  Blocks are dispatched in
+// blockIdx order, so a kernel launched right after a forward kernel over the
+// same data starts on the rows whose lines that kernel touched last, which may
+// still sit in the memory-side Infinity Cache (MALL, 256 MB, shared by all
+// XCDs).  Order only: every row's arithmetic is unchanged.
+template <bool REV = false>
 __device__ __forceinline__ uint32_t xcd_block() {
   const uint32_t b = blockIdx.x, nb = gridDim.x;
   const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
   const uint32_t base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  if constexpr (REV) return base + ((xcd < r) ? q : q - 1u) - (b >> 3);
   return base + (b >> 3);
 }
-__device__ __forceinline__ uint32_t row_id() { return xcd_block() * kBlock + threadIdx.x; }
+template <bool REV = false>
+__device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock + threadIdx.x; }
+
+// Kernels that run top-down (xcd_block<true>) to reuse the Infinity Cache lines
+// of the kernel before them (build-time tunables, tools/ab_variants.py).  Same-box
+// A/B at C2 (profiles/r01/ab_reverse_order.txt): k_amg_residual, which follows
+// the bottom-up pre-smoother over the same level matrix, 83.1 -> 67.4 us at
+// level 0; k_spmv, which follows k_precond_correct over the same cval_g / column
+// slots, 233.5 -> 223.1 us; 278.9 -> 273.5 ms/step.  The CGS update after the
+// dots gains nothing (its nontemporal basis reads do not stay in the MALL, and
+// temporal ones cost 20 %), so the CGS kernels keep one direction.
+#ifndef CFD_REV_SPMV
+#define CFD_REV_SPMV 1
+#endif
+#ifndef CFD_REV_RESIDUAL
+#define CFD_REV_RESIDUAL 1
+#endif
 
 // First row of this thread's 4 in a launch over [r0, r1) and [r2, r3) (the
 // second range lets a distributed rank process both boundary strips of a
 // halo'd kernel in one launch); false: no rows for this thread.
+template <bool REV = false>
 __device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
-  const uint32_t t = row_id(), na = (r1 - r0 + 3) / 4;
+  const uint32_t t = row_id<REV>(), na = (r1 - r0 + 3) / 4;
   if (t < na) {
     i0 = r0 + 4 * t;
     return i0 < r1;
@@ -640,7 +664,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
                                                  float* __restrict__ y) {
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   uint32_t i0;
-  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  if (!row_range<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
   float2 d2[4];
@@ -1235,7 +1259,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
   uint32_t i0;
-  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  if (!row_range<CFD_REV_RESIDUAL>(L.r0, L.r1, L.r2, L.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
