@@ -7,4 +7,4 @@ from . import mesh  # noqa: F401
 from .mesh import (BackwardsStep, ChannelWithObstacle, CircleObstacle, Mesh,  # noqa: F401
                    RectangularChannel, generate_cut_cell_mesh)
 from .solver import GpuGroup, GpuSolver, dist_plan, dist_unique_id  # noqa: F401,E402
-from ._ffi import Config, Constants, default_config  # noqa: F401,E402
+from ._ffi import Config, Constants, build_id, default_config  # noqa: F401,E402

@@ -141,7 +141,7 @@ def default_config(**overrides) -> Config:
 
 # Every symbol include/cfd2_amd.h declares (checked by tests/test_capi.py).
 EXPORTED = [
-    "cfd_last_error",
+    "cfd_last_error", "cfd_build_id",
     "cfd_mesh_generate_cut_cell", "cfd_mesh_generate_voronoi", "cfd_mesh_generate_delaunay", "cfd_mesh_get_topology", "cfd_mesh_smooth", "cfd_mesh_max_skewness", "cfd_mesh_get_view",
     "cfd_mesh_get_vertices", "cfd_mesh_save", "cfd_mesh_load", "cfd_mesh_destroy",
     "cfd_config_default", "cfd_solver_create", "cfd_solver_destroy", "cfd_set_u", "cfd_set_p",
@@ -172,6 +172,7 @@ def lib() -> C.CDLL:
     L = C.CDLL(LIB_PATH)
     vp = C.c_void_p
     L.cfd_last_error.restype = C.c_char_p
+    L.cfd_build_id.restype = C.c_char_p
     L.cfd_mesh_generate_cut_cell.argtypes = [C.POINTER(Geometry), C.c_double, C.c_double, C.c_double,
                                              C.c_double, C.c_double, C.POINTER(vp)]
     u32pp = C.POINTER(C.POINTER(C.c_uint32))
@@ -191,6 +192,11 @@ def lib() -> C.CDLL:
     L.cfd_mesh_destroy.restype = None
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """cfd_build_id(): the source hash the loaded library was built from."""
+    return lib().cfd_build_id().decode()
 
 
 def check(status: int, what: str = "") -> None:

@@ -10,6 +10,11 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
 #include "kernels.hpp"
 
 namespace cfd2 {
@@ -1384,7 +1389,7 @@ __device__ __forceinline__ int col_at(const AmgLevelDev& L, size_t off, uint32_t
 __device__ __forceinline__ float smooth_row(const AmgLevelDev& L, const float* x, const float* b,
                                             uint32_t i) {
   float sigma = 0.0f;
-  const uint32_t len = L.len[i];
+  const uint32_t len = L.len16 ? (uint32_t)L.len16[i] : (uint32_t)L.len[i];
   for (uint32_t r = 0; r < len; ++r) {
     const size_t off = (size_t)r * L.stride + i;
     sigma += L.val[off] * x[col_at(L, off, i)];
@@ -1393,7 +1398,8 @@ __device__ __forceinline__ float smooth_row(const AmgLevelDev& L, const float* x
 }
 __device__ __forceinline__ float residual_row(const AmgLevelDev& L, const float* x, const float* b,
                                               uint32_t i) {
-  const uint32_t len = L.len[i], dr = L.drank[i];
+  const uint32_t len = L.len16 ? (uint32_t)L.len16[i] : (uint32_t)L.len[i];
+  const uint32_t dr = L.drank16 ? (uint32_t)L.drank16[i] : (uint32_t)L.drank[i];
   float ax = 0.0f;
   for (uint32_t r = 0; r <= len; ++r) {
     if (r == dr) ax += L.dv[i] * x[i];
@@ -1919,25 +1925,44 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
     hipLaunchKernelGGL(k_amg_tail, dim3(1), dim3(1024), 0, s, tail, first, nlev);
     return;
   }
-  static bool attr = false;
-  if (!attr) {  // allow up to the whole 160 KiB LDS of a CU for this kernel
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_lds),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax);
-    attr = true;
-  }
   hipLaunchKernelGGL(k_amg_tail_lds, dim3(1), dim3(1024), lds_bytes, s, tail, first, nlev);
 }
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax);
-    attr = true;
-  }
   const size_t lds = 4 * ((size_t)vec_floats + blob_words);
   hipLaunchKernelGGL(k_amg_tail_blob, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats, first,
                      nlev);
+}
+// Per-device kernel attributes: the LDS-resident tail kernels take more than
+// the default 64 KiB of dynamic LDS.  The attribute belongs to the device that
+// is current when it is set, so each device gets it once (std::call_once per
+// device id; the in-process group runs one host thread per rank and device).
+// Returns the dynamic-LDS budget of those kernels on this device: the smaller
+// of kTailLdsMax and the device's opt-in per-block limit.
+size_t init_kernel_attributes(int device) {
+  constexpr int kMaxDevices = 64;
+  static std::once_flag once[kMaxDevices];
+  static hipError_t status[kMaxDevices];
+  static size_t budget[kMaxDevices];
+  if (device < 0 || device >= kMaxDevices) throw std::invalid_argument("HIP device id out of range");
+  std::call_once(once[device], [device] {
+    int optin = 0;
+    hipError_t e = hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, device);
+    size_t lim = kTailLdsMax;
+    if (e == hipSuccess && optin > 0) lim = std::min(lim, (size_t)optin);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_lds),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
+    status[device] = e;
+    budget[device] = lim;
+  });
+  if (status[device] != hipSuccess)
+    throw std::runtime_error(std::string("setting the tail kernels' dynamic-LDS limit: ") +
+                             hipGetErrorString(status[device]));
+  return budget[device];
 }
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
                               uint64_t gbase, uint64_t rec0, double* partial, hipStream_t s) {

@@ -146,6 +146,12 @@ struct AmgLevelDev {
   const uint8_t* drank;  // [stride] position of the diagonal among the row's entries
   const float* dv;       // [stride] raw diagonal value (0 if absent)
   const float* de;       // [stride] smoother diagonal (dv, or 1.0 if |dv| < 1e-14)
+  // wide level (a row with more off-diagonals than kAmgWideLimit): 16-bit row
+  // lengths / diagonal ranks here (len / drank then hold min(., 255) and are
+  // not read).  Only the one-workgroup tail kernels run wide levels
+  // (Solver::ensure_amg moves the tail up to the first wide level).
+  const uint16_t* len16;
+  const uint16_t* drank16;
   // coarsening operators (only when nc > 0)
   uint32_t nc;
   const uint32_t* agg;     // [stride] P: fine -> coarse (padding rows -> 0, never read)
@@ -254,6 +260,10 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
+// Sets the tail kernels' dynamic-LDS attribute on `device` (once per device,
+// thread-safe; throws on failure) and returns their LDS budget there:
+// min(kTailLdsMax, the device's opt-in per-block LDS).  Call with `device` current.
+size_t init_kernel_attributes(int device);
 // check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
 // partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
 // The variance part reads record ((gbase + c) >> 2) - rec0 of `var` (stride bug, §0.1-12).

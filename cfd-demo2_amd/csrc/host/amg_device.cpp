@@ -167,7 +167,21 @@ bool Solver::build_amg_device() {
       }
       wmax = std::max(wmax, off);
     }
-    if (wmax > 255) throw std::domain_error("AMG level row wider than 255 entries");
+    // a row wider than the u8 layout: the host path builds that level with
+    // 16-bit lengths (every rank must take the same path: combined over ranks)
+    {
+      bool wide = wmax > amg_wide_limit;
+      if (dist()) {
+        const std::vector<uint64_t> fl = gather_counts(wide ? 1u : 0u);
+        for (uint64_t f : fl) wide = wide || f != 0;
+      }
+      if (wide) {
+        if (timing) std::fprintf(stderr, "[amg setup] device path: wide rows at level %d, host path\n", li);
+        levels.clear();
+        amg_refresh.clear();
+        return false;
+      }
+    }
     const uint32_t st = (n + 63) & ~63u;
     const size_t slots = (size_t)std::max(wmax, 1) * st;
     G.nnz = cur.row[n] - cur.row[0];

@@ -341,11 +341,18 @@ cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
   for (int r = 0; r < n; ++r)
     th.emplace_back([&, r] {
       st[r] = guard([&] { f(*h[r]->s); });
-      if (st[r] != CFD_OK) msg[r] = cfd_last_error();
+      if (st[r] != CFD_OK) {
+        msg[r] = cfd_last_error();
+        // wake the ranks waiting for this one in a collective (they fail too)
+        if (h[r]->s->comm) h[r]->s->comm->abort();
+      }
     });
   for (auto& t : th) t.join();
+  // report the first rank that failed on its own (the others fail with "aborted")
+  int first = -1;
   for (int r = 0; r < n; ++r)
-    if (st[r] != CFD_OK) return set_error(st[r], "rank " + std::to_string(r) + ": " + msg[r]);
+    if (st[r] != CFD_OK && (first < 0 || msg[first].find("group aborted") != std::string::npos)) first = r;
+  if (first >= 0) return set_error(st[first], "rank " + std::to_string(first) + ": " + msg[first]);
   return CFD_OK;
 }
 }  // namespace

@@ -141,14 +141,22 @@ LocalGroup::~LocalGroup() {
 
 void LocalGroup::barrier() {
   std::unique_lock<std::mutex> lk(mu_);
+  if (aborted_) throw std::runtime_error("in-process group aborted: another rank failed");
   const uint64_t g = gen_;
   if (++arrived_ == n_) {
     arrived_ = 0;
     ++gen_;
     cv_.notify_all();
   } else {
-    cv_.wait(lk, [&] { return gen_ != g; });
+    cv_.wait(lk, [&] { return gen_ != g || aborted_; });
+    if (gen_ == g) throw std::runtime_error("in-process group aborted: another rank failed");
   }
+}
+
+void LocalGroup::abort() {
+  std::lock_guard<std::mutex> lk(mu_);
+  aborted_ = true;
+  cv_.notify_all();
 }
 
 namespace {
@@ -210,6 +218,8 @@ class LocalComm final : public Comm {
         waited[m.peer] = 1;
       }
   }
+
+  void abort() override { g_->abort(); }
 
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     auto& me = g_->slots[rank];

@@ -47,6 +47,10 @@ class Comm {
   // Variable-size in-place all-gather: every rank's piece [off[r], off[r+1]) of
   // buf (bytes) is distributed to all ranks.
   void allgatherv_inplace(void* buf, const std::vector<size_t>& off, hipStream_t s);
+  // A rank failed: wake every rank blocked in this transport (in-process
+  // group) so they fail too instead of waiting forever.  RCCL / host
+  // transports: no-op (the launcher tears the processes down).
+  virtual void abort() {}
 };
 
 // ---- RCCL ----
@@ -66,7 +70,9 @@ class LocalGroup {
   explicit LocalGroup(int n);
   ~LocalGroup();
   int size() const { return n_; }
+  // throws std::runtime_error once the group is aborted (sticky)
   void barrier();
+  void abort();
   struct Slot {
     std::vector<Msg> posted;
     const void* gather_src = nullptr;
@@ -81,6 +87,7 @@ class LocalGroup {
   std::condition_variable cv_;
   int arrived_ = 0;
   uint64_t gen_ = 0;
+  bool aborted_ = false;
 };
 
 std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank, int device);

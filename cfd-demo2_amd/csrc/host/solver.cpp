@@ -72,6 +72,13 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   shift = (topo.glo + 63) & ~63u;
   vlen = (size_t)shift + topo.npad + topo.ghi;
   CFD_HIP(hipSetDevice(device));
+  lds_budget = init_kernel_attributes(device);
+  if (const char* wl = std::getenv("CFD_AMG_WIDE_LIMIT"))
+    amg_wide_limit = std::max(1, std::min(255, (int)std::strtol(wl, nullptr, 10)));
+  {
+    const char* cs = std::getenv("CFD_CHECK_SYNC");
+    check_sync = cs && cs[0] == '1';
+  }
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -374,6 +381,7 @@ void Solver::prepare() {
   a.grad_u = grad_u;
   a.grad_v = grad_v;
   launch_prepare(a, stream);
+  check_launch("prepare");
   // commit d_p / grad_p (snapshot semantics): swap the scratch into the slot
   std::swap(S().dp, dp_scratch);
   std::swap(S().gp, gp_scratch);
@@ -403,6 +411,7 @@ void Solver::assemble() {
   a.dinv_uv = dinv_uv;
   a.dinv_p = dinv_p;
   launch_assemble(a, stream);
+  check_launch("assemble");
   if (dist()) halo(cell_plan, {{dinv_uv, 1}});  // the Schur prediction reads neighbours' D_u^-1
 }
 
@@ -445,11 +454,12 @@ namespace {
 // off-diagonal columns mapped to local indices by `rel`; see AmgLevelDev.
 template <class Rel>
 void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel& G, DeviceArena& arena,
-                 hipStream_t stream) {
+                 hipStream_t stream, int wide_limit) {
   const uint32_t st = (n + 63) & ~63u;  // padded row count (16-byte row groups)
   int wmax = 0;
   bool small_delta = true;
   std::vector<uint8_t> len(st, 0), drank(st, 0);
+  std::vector<uint16_t> len16(st, 0), drank16(st, 0);
   std::vector<float> dv(st, 0.0f), de(st, 1.0f);
   uint64_t nnz = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -473,9 +483,11 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
     nnz += A.row[gi + 1] - A.row[gi];
     if (!has) dr = off;  // no diagonal entry: raw diag contributes nothing (dv = 0)
     if (std::fabs(diag) < 1e-14f) diag = 1.0f;  // amg.wgsl:46
-    if (off > 255) throw std::domain_error("AMG level row wider than 255 entries");
-    len[i] = (uint8_t)off;
-    drank[i] = (uint8_t)dr;
+    if (off > 65535) throw std::invalid_argument("AMG level row wider than 65535 entries (unsupported)");
+    len[i] = (uint8_t)std::min(off, 255u);
+    drank[i] = (uint8_t)std::min(dr, 255u);
+    len16[i] = (uint16_t)off;
+    drank16[i] = (uint16_t)dr;
     dv[i] = raw;
     de[i] = diag;
     wmax = std::max(wmax, (int)off);
@@ -518,6 +530,9 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
   G.dev.drank = arena.upload(drank, stream);
   G.dev.dv = arena.upload(dv, stream);
   G.dev.de = arena.upload(de, stream);
+  G.wide = wmax > wide_limit;
+  G.dev.len16 = G.wide ? arena.upload(len16, stream) : nullptr;
+  G.dev.drank16 = G.wide ? arena.upload(drank16, stream) : nullptr;
 }
 
 }  // namespace
@@ -644,7 +659,7 @@ void Solver::build_amg_host() {
         const uint32_t k = (uint32_t)(it - ghost.begin());
         return k < glo ? (int32_t)k - (int32_t)glo : (int32_t)(npad + (k - glo));
       };
-      level_image(HL.A, C0, n, rel, G, arena, stream);
+      level_image(HL.A, C0, n, rel, G, arena, stream, amg_wide_limit);
       G.plan = build_halo_plan(HL.part, rk, lrow.data(), n, lcol, ghost, G.glo, G.npad);
       make_plan_buffers(G.plan, 1);
       if (li == 0) {
@@ -662,7 +677,7 @@ void Solver::build_amg_host() {
       }
     } else {  // replicated (or single-GPU) level, global numbering
       const uint32_t n = (uint32_t)HL.A.rows;
-      level_image(HL.A, 0, n, [](uint32_t c) { return (int32_t)c; }, G, arena, stream);
+      level_image(HL.A, 0, n, [](uint32_t c) { return (int32_t)c; }, G, arena, stream, amg_wide_limit);
       G.npad = G.dev.stride;
       G.xt = zeroed(G.npad);
       G.r = zeroed(G.npad);
@@ -779,6 +794,25 @@ void Solver::ensure_amg() {
   const int lo = std::max(amg_g, 1);
   tail_first = L;
   while (tail_first > lo && levels[tail_first - 1].dev.n <= tail_rows) --tail_first;
+  // wide levels (16-bit row lengths) run only in the one-workgroup tail kernels
+  {
+    int bad = -1;  // first wide level the row kernels would run (level 0 or a row-partitioned level)
+    for (int li = 0; li < L; ++li)
+      if (levels[li].wide) {
+        if (li < lo)
+          bad = li;
+        else
+          tail_first = std::min(tail_first, li);
+        break;
+      }
+    // the width of a row-partitioned level is per rank: every rank throws together
+    uint64_t any_bad = bad >= 0 ? 1 : 0;
+    if (dist())
+      for (uint64_t f : allgather_u64(any_bad)) any_bad |= f;
+    if (any_bad)
+      throw std::invalid_argument("AMG: rows wider than 255 entries on a level the row kernels run (level 0 or a "
+                                  "row-partitioned level): unsupported layout");
+  }
   std::vector<AmgTailLevel> tl(L);
   for (int li = 0; li < L; ++li) {
     tl[li].L = levels[li].dev;
@@ -788,6 +822,7 @@ void Solver::ensure_amg() {
     tl[li].r = levels[li].r;
   }
   d_tail = arena.upload(tl, stream);
+  check_launch("AMG setup");
   const char* tb_env = std::getenv("CFD_AMG_TAIL_BLOB");
   if (tail_lds && !(tb_env && tb_env[0] == '0')) build_tail_blob(std::max({tail_first, 1, dist() ? amg_g : 0}));
   sync();
@@ -848,7 +883,7 @@ void Solver::build_tail_blob(int tf, bool reuse) {
   for (int l = tf; l < L; ++l) {
     const AmgLevelDev& d = levels[l].dev;
     const uint32_t n = d.n, st = d.stride;
-    if (n > 65535 || d.nc > 65535) return;
+    if (n > 65535 || d.nc > 65535 || levels[l].wide) return;  // the blob keeps u8 diagonal ranks
     const size_t slots = (size_t)std::max(d.w, 1) * st;
     std::vector<uint8_t> len(n), drank(n);
     std::vector<float> dv(n), de(n), val(slots);
@@ -903,7 +938,7 @@ void Solver::build_tail_blob(int tf, bool reuse) {
     vec += 4 * ((n + 3) & ~3u);
   }
   align4();
-  if (4 * ((size_t)vec + blob.size()) > kTailLdsMax) return;
+  if (4 * ((size_t)vec + blob.size()) > lds_budget) return;
   if (reuse && d_tail_blob && blob.size() == old_words) {  // same structure: new values in place
     CFD_HIP(hipMemcpyAsync(d_tail_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice, stream));
     CFD_HIP(hipMemcpyAsync(d_tail_desc, desc.data(), desc.size() * sizeof(TailBlobLevel), hipMemcpyHostToDevice,
@@ -1046,7 +1081,7 @@ void Solver::v_cycle() {
   } else if (tf < L) {
     size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL_LDS=0 disables)
     for (int l = tf; l < L; ++l) lds += 4 * (((size_t)levels[l].dev.n + 3) & ~(size_t)3) * sizeof(float);
-    if (lds > kTailLdsMax || !tail_lds) lds = 0;
+    if (lds > lds_budget || !tail_lds) lds = 0;
     launch_amg_tail(d_tail, tf, L, lds, stream);
   } else {
     for (int s = 0; s < 10; ++s) sm(L - 1, s == 0 && L > 1);
@@ -1180,6 +1215,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
       const auto rn = combine(partial_n, nchunks, 1);
       launch_norm_givens(rn.first, rn.second, j, H, m1, givens, g, binv, resid_hist, stream);
+      check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
       if (inner.pending >= 0) {
@@ -1212,6 +1248,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     }
     launch_solve_triangular(H, g, y, basis_size, m1, stream);
     launch_update_x(x, zvec, stride, y, basis_size, n, stream);
+    check_launch("FGMRES solution update");
     if (converged) {  // async_reader.flush()
       if (inner.pending >= 0) {
         CFD_HIP(hipEventSynchronize(ev_iter[inner.pending]));
@@ -1315,6 +1352,7 @@ void Solver::check_evolution() {
   launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, stream);
   double* out5 = partial_d + 5 * (size_t)nchunks;
   launch_evolution_final(partial_d, nchunks, out5, stream);
+  check_launch("check_evolution");
   double tot[5];
   if (dist()) {
     std::vector<double> gth(5 * (size_t)R);
@@ -1400,6 +1438,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
     info.total_linear_iterations += ls.iterations;
     if (std::isnan(ls.residual)) throw std::domain_error("Coupled Linear Solver Diverged: NaN detected in linear residual");
     launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, blockmax, maxbits, stream);
+    check_launch("update_fields");
     if (dist()) {
       halo_state(false);  // the next prepare reads neighbours' u, p
       comm->allgather(maxbits, mx_gather, 2 * sizeof(uint32_t), stream);

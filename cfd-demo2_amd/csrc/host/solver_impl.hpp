@@ -148,6 +148,7 @@ struct AmgGpuLevel {
   AmgLevelDev dev{};
   float* x = nullptr;   // level solution (level 0: external p_sol); owned base
   float* xt = nullptr;  // ping-pong partner for the out-of-place smoother
+  bool wide = false;    // rows wider than the u8 layout: 16-bit lengths, tail kernels only
   float* b = nullptr;   // level rhs (level 0: external temp_p)
   float* r = nullptr;   // residual scratch
   uint64_t nnz = 0;     // including diagonal (rows this rank stores)
@@ -253,6 +254,10 @@ struct Solver {
   int amg_setup_path = 0;          // 0 not built, 1 host, 2 device (build_amg_device)
   int tail_first = 1;              // first AMG level handled by k_amg_tail
   bool tail_lds = true;            // LDS-resident tail kernel when it fits
+  // rows with more off-diagonals than this use the 16-bit layout (<= 255;
+  // CFD_AMG_WIDE_LIMIT lowers it so that tests exercise the wide path)
+  int amg_wide_limit = 255;
+  size_t lds_budget = 0;           // dynamic LDS of the tail kernels on this device (init_kernel_attributes)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   // k_amg_tail_blob: LDS image of the tail levels [tail_blob_first, L) (-1: none)
@@ -356,6 +361,21 @@ struct Solver {
   float residual_into_v0_blocking();
   void check_evolution();
   void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
+ public:
+  // Launch-error check: hipGetLastError after each phase of the step (a host
+  // call, no synchronisation); with CFD_CHECK_SYNC=1 the stream is also
+  // synchronised there, so an asynchronous kernel fault is reported at the
+  // phase that caused it (debug runs).
+  void check_launch(const char* where) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw HipError(std::string("kernel launch in ") + where + ": " + hipGetErrorString(e));
+    if (check_sync) {
+      const hipError_t e2 = hipStreamSynchronize(stream);
+      if (e2 != hipSuccess) throw HipError(std::string("kernel execution in ") + where + ": " + hipGetErrorString(e2));
+    }
+  }
+  bool check_sync = false;
+ private:
   // cfg.log_level >= 1: the reference's println! progress lines, on stderr, rank 0
   void log(const char* fmt, ...) const __attribute__((format(printf, 2, 3)));
   CoupledMatrix cmat() const;

@@ -3,6 +3,8 @@
 #include <cstring>
 #include <stdexcept>
 #include <exception>
+#include <memory>
+#include <new>
 #include <string>
 
 #include "../../../include/cfd2_amd.h"
@@ -29,12 +31,51 @@ static bool wvec(FILE* f, const std::vector<T>& v) {
   if (fwrite(&n, 8, 1, f) != 1) return false;
   return n == 0 || fwrite(v.data(), sizeof(T), n, f) == n;
 }
+// `left` = bytes of the file not read yet: a count larger than what remains
+// is a truncated or corrupt file, refused before anything is allocated.
 template <class T>
-static bool rvec(FILE* f, std::vector<T>& v) {
+static bool rvec(FILE* f, std::vector<T>& v, uint64_t& left) {
   uint64_t n = 0;
-  if (fread(&n, 8, 1, f) != 1) return false;
+  if (left < 8 || fread(&n, 8, 1, f) != 1) return false;
+  left -= 8;
+  if (n > left / sizeof(T)) return false;
   v.resize(n);
-  return n == 0 || fread(v.data(), sizeof(T), n, f) == n;
+  if (n && fread(v.data(), sizeof(T), n, f) != n) return false;
+  left -= n * sizeof(T);
+  return true;
+}
+
+// Array lengths and offsets of a loaded mesh agree with each other (every
+// index array is checked again by build_topology when a solver is made).
+static const char* mesh_consistency(const cfd2::Mesh& m) {
+  const size_t nc = m.cell_cx.size(), nf = m.face_owner.size(), nv = m.vx.size();
+  if (m.cell_cy.size() != nc || m.cell_vol.size() != nc) return "cell arrays differ in length";
+  if (m.face_neighbor.size() != nf || m.face_boundary.size() != nf || m.face_nx.size() != nf ||
+      m.face_ny.size() != nf || m.face_area.size() != nf || m.face_cx.size() != nf || m.face_cy.size() != nf ||
+      m.face_v1.size() != nf || m.face_v2.size() != nf)
+    return "face arrays differ in length";
+  if (m.vy.size() != nv || m.v_fixed.size() != nv) return "vertex arrays differ in length";
+  if (m.cell_face_offsets.size() != nc + 1 || m.cell_vertex_offsets.size() != nc + 1)
+    return "offset arrays must hold num_cells + 1 entries";
+  auto monotone = [](const std::vector<uint32_t>& off, size_t total) {
+    if (off.empty() || off[0] != 0 || off.back() != total) return false;
+    for (size_t i = 1; i < off.size(); ++i)
+      if (off[i] < off[i - 1]) return false;
+    return true;
+  };
+  if (!monotone(m.cell_face_offsets, m.cell_faces.size())) return "cell_face_offsets not monotone / not ending at the face list";
+  if (!monotone(m.cell_vertex_offsets, m.cell_vertices.size()))
+    return "cell_vertex_offsets not monotone / not ending at the vertex list";
+  for (uint32_t fi : m.cell_faces)
+    if (fi >= nf) return "cell_faces index out of range";
+  for (uint32_t vi : m.cell_vertices)
+    if (vi >= nv) return "cell_vertices index out of range";
+  for (size_t k = 0; k < nf; ++k) {
+    if (m.face_owner[k] >= nc) return "face_owner out of range";
+    if (m.face_neighbor[k] != 0xFFFFFFFFu && m.face_neighbor[k] >= nc) return "face_neighbor out of range";
+    if (m.face_v1[k] >= nv || m.face_v2[k] >= nv) return "face vertex out of range";
+  }
+  return nullptr;
 }
 
 extern "C" {
@@ -183,21 +224,34 @@ cfd_status cfd_mesh_save(const cfd_mesh* m, const char* path) {
 
 cfd_status cfd_mesh_load(const char* path, cfd_mesh** out) {
   if (!out || !path) return set_error(CFD_ERR_INVALID, "null");
-  FILE* f = fopen(path, "rb");
-  if (!f) return set_error(CFD_ERR_INVALID, std::string("cannot open ") + path);
-  char magic[8];
-  bool ok = fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "CFDMESH1", 8) == 0;
-  auto* m = new cfd_mesh;
-#define R(name) ok = ok && rvec(f, m->m.name);
-  MESH_FIELDS(R)
+  try {
+    std::unique_ptr<FILE, int (*)(FILE*)> fh(fopen(path, "rb"), fclose);
+    FILE* f = fh.get();
+    if (!f) return set_error(CFD_ERR_INVALID, std::string("cannot open ") + path);
+    uint64_t left = 0;
+    if (fseek(f, 0, SEEK_END) == 0) {
+      const long end = ftell(f);
+      left = end > 0 ? (uint64_t)end : 0;
+    }
+    rewind(f);
+    char magic[8];
+    bool ok = left >= 8 && fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "CFDMESH1", 8) == 0;
+    left = left >= 8 ? left - 8 : 0;
+    std::unique_ptr<cfd_mesh> m(new cfd_mesh);
+#define R(name) ok = ok && rvec(f, m->m.name, left);
+    MESH_FIELDS(R)
 #undef R
-  fclose(f);
-  if (!ok) {
-    delete m;
-    return set_error(CFD_ERR_INVALID, "bad mesh file");
+    fh.reset();
+    if (!ok) return set_error(CFD_ERR_INVALID, std::string("bad mesh file (truncated or corrupt): ") + path);
+    if (const char* why = mesh_consistency(m->m))
+      return set_error(CFD_ERR_INVALID, std::string("inconsistent mesh file ") + path + ": " + why);
+    *out = m.release();
+    return CFD_OK;
+  } catch (const std::bad_alloc&) {
+    return set_error(CFD_ERR_INVALID, std::string("mesh file too large for host memory: ") + path);
+  } catch (const std::exception& e) {
+    return set_error(CFD_ERR_INTERNAL, e.what());
   }
-  *out = m;
-  return CFD_OK;
 }
 
 void cfd_mesh_destroy(cfd_mesh* m) { delete m; }

@@ -31,6 +31,10 @@ typedef enum cfd_status {
 } cfd_status;
 
 const char* cfd_last_error(void);
+/* Source hash of this build (sha256 prefix over csrc/ and include/, computed by
+ * __graft_entry__.source_hash()); no reference counterpart -- it ties every
+ * measured number to the code that produced it. */
+const char* cfd_build_id(void);
 
 /* ------------------------------------------------------------------------ */
 /* Mesh (input format).  Mirrors `Mesh` SoA, src/solver/mesh/structs.rs:12-42.

@@ -6,6 +6,7 @@ import os
 import tempfile
 
 import numpy as np
+import pytest
 
 from cfd2_amd.mesh import (BackwardsStep, ChannelWithObstacle, CircleObstacle, Mesh,
                            bench_channel, generate_cut_cell_mesh)
@@ -127,3 +128,44 @@ def test_shared_view_file_round_trip(tmp_path):
     v = mm.view()
     assert v.num_cells == m.num_cells() and v.num_faces == m.num_faces()
     assert v.cell_vol[0] == a["cell_vol"][0] and v.cell_faces[5] == a["cell_faces"][5]
+
+
+def test_load_rejects_truncated_and_inconsistent_files(tmp_path):
+    """cfd_mesh_load trusts nothing in the file: a truncated file, a count larger
+    than the file, and arrays whose lengths disagree are all CFD_ERR_INVALID
+    (no allocation from an unchecked count, no out-of-range reads later)."""
+    import struct
+    m = backwards_step()
+    p = str(tmp_path / "m.bin")
+    m.save(p)
+    raw = open(p, "rb").read()
+    # truncated
+    bad = str(tmp_path / "trunc.bin")
+    open(bad, "wb").write(raw[: len(raw) // 2])
+    with pytest.raises(RuntimeError, match="status 1"):
+        Mesh.load(bad)
+    # first array count (vx) blown up to 2^60 entries
+    bad2 = str(tmp_path / "count.bin")
+    open(bad2, "wb").write(raw[:8] + struct.pack("<Q", 1 << 60) + raw[16:])
+    with pytest.raises(RuntimeError, match="status 1"):
+        Mesh.load(bad2)
+    # a well-formed file whose cell arrays disagree in length: drop one cell_vol entry
+    a = m.arrays()
+    n = m.num_cells()
+    # field order of MESH_FIELDS: vx vy v_fixed face_v1 face_v2 face_owner face_neighbor face_boundary
+    # face_nx face_ny face_area face_cx face_cy cell_cx cell_cy cell_vol ...; walk to cell_vol
+    off = 8
+    sizes = {"vx": 8, "vy": 8, "v_fixed": 1, "face_v1": 4, "face_v2": 4, "face_owner": 4, "face_neighbor": 4,
+             "face_boundary": 4, "face_nx": 8, "face_ny": 8, "face_area": 8, "face_cx": 8, "face_cy": 8,
+             "cell_cx": 8, "cell_cy": 8}
+    for name, sz in sizes.items():
+        cnt = struct.unpack_from("<Q", raw, off)[0]
+        off += 8 + cnt * sz
+    cnt = struct.unpack_from("<Q", raw, off)[0]
+    assert cnt == n == len(a["cell_vol"])
+    body = raw[off + 8: off + 8 + (n - 1) * 8]
+    rest = raw[off + 8 + n * 8:]
+    bad3 = str(tmp_path / "len.bin")
+    open(bad3, "wb").write(raw[:off] + struct.pack("<Q", n - 1) + body + rest)
+    with pytest.raises(RuntimeError, match="inconsistent"):
+        Mesh.load(bad3)
