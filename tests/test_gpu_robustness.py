@@ -61,7 +61,7 @@ def test_wide_amg_rows_take_the_16bit_path_bitexact(monkeypatch, tail_lds):
     16-bit row lengths, the whole coarse cycle in the tail kernel (LDS-resident
     or global-memory); fields and step statistics bit-exact vs the oracle."""
     mesh = backwards_step()
-    monkeypatch.setenv("CFD_AMG_WIDE_LIMIT", "6")
+    monkeypatch.setenv("CFD_AMG_WIDE_LIMIT", "5")  # level 0: 4, coarse levels: 6
     monkeypatch.setenv("CFD_AMG_TAIL_LDS", tail_lds)
     g = GpuSolver(mesh, config=default_config())
     o = OracleSolver(mesh, config=default_config())
