@@ -94,44 +94,101 @@ inline unsigned rows2_grid(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) {
   return (unsigned)((t + 255) / 256);
 }
 
-// Halving tree over 256 per-thread values (canonical order): levels 128 and 64
-// through LDS, levels 32..1 by wavefront shuffles in wave 0.  Result valid in
-// thread 0.  `lds` must hold 256 floats; caller syncs before reusing it.
-__device__ __forceinline__ float block_tree(float v, float* lds) {
-  const int t = threadIdx.x;
-  lds[t] = v;
-  __syncthreads();
-  if (t < 128) lds[t] = lds[t] + lds[t + 128];
-  __syncthreads();
-  float x = 0.0f;
-  if (t < 64) {
-    x = lds[t] + lds[t + 64];
-    x = x + __shfl_down(x, 32);
-    x = x + __shfl_down(x, 16);
-    x = x + __shfl_down(x, 8);
-    x = x + __shfl_down(x, 4);
-    x = x + __shfl_down(x, 2);
-    x = x + __shfl_down(x, 1);
+// ---- canonical reduction order (kernels.hpp: leaf / chunk / segment / total) ----
+// Pairwise tree over the first `active` lanes of the wavefront (a power of
+// two <= 64); lane 0 holds the root.  Lane l adds lane l + s at strides
+// s = 1, 2, ...: at every level each surviving node is (left + right).
+template <class T>
+__device__ __forceinline__ T wave_tree(T v, uint32_t active = 64) {
+  for (uint32_t st = 1; st < active; st <<= 1) v = v + __shfl_down(v, st);
+  return v;
+}
+// chunk of this wavefront in a reduction kernel (4 chunks per 256-thread block)
+__device__ __forceinline__ uint32_t red_chunk() { return blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint32_t red_lane() { return threadIdx.x & 63; }
+
+// Segment values of U consecutive-in-steps segments s0, s0 + sstep, ... from
+// chunk partials pv[k] (k < nchunks, missing chunks +0): lane l holds chunk
+// slots [l K, l K + K) of the segment, K = min(4, G / 64) ... (G <= 256).
+template <class T, int U>
+__device__ __forceinline__ void seg_trees(const T* __restrict__ pv, uint32_t nchunks, uint32_t G, uint32_t s0,
+                                          uint32_t sstep, uint32_t nseg, T out[U]) {
+  const uint32_t lane = red_lane();
+  const uint32_t K = G >= 256 ? 4u : (G >= 128 ? 2u : 1u);
+  const uint32_t L = G / K;  // active lanes (power of two)
+  T e[U][4];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t sg = s0 + u * sstep;
+    const uint64_t k0 = (uint64_t)sg * G + (uint64_t)lane * K;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t k = k0 + q;
+      e[u][q] = (sg < nseg && lane < L && (uint32_t)q < K && k < nchunks) ? pv[k] : T(0);
+    }
   }
-  return x;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    T v;
+    if (K == 4)
+      v = (e[u][0] + e[u][1]) + (e[u][2] + e[u][3]);
+    else if (K == 2)
+      v = e[u][0] + e[u][1];
+    else
+      v = e[u][0];
+    out[u] = wave_tree(v, L);
+  }
 }
 
-// Canonical stage 2 over `np` partials by one 256-thread block.
-// (loads issued 8 at a time ahead of the sequential adds: same order, more
-// memory-level parallelism for the single-block stage-2 kernels)
-__device__ __forceinline__ float block_final(const float* partial, uint32_t np, float* lds) {
-  float acc = 0.0f;
-  uint32_t q = threadIdx.x;
-  for (; q + 7 * kBlock < np; q += 8 * kBlock) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = partial[q + u * kBlock];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc += v[u];
-  }
-  for (; q < np; q += kBlock) acc += partial[q];
-  return block_tree(acc, lds);
+__host__ __device__ __forceinline__ uint32_t pow2_ceil(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
 }
+
+// Total of vector v of reduction r by the whole block (NT threads): the
+// segment values into LDS a[0, P) (+0 padding to P = pow2 >= nseg), then the
+// pairwise tree over them (ping-pong a/b).  Every thread returns the total.
+template <class T, int NT>
+__device__ __forceinline__ T red_total(const RedSrcT<T>& r, uint32_t v, T* a, T* b) {
+  const uint32_t P = pow2_ceil(r.nseg);
+  if (r.seg_src) {  // distributed: gathered segment values
+    const size_t blk = (size_t)r.nvec * r.stride;
+    for (uint32_t sg = threadIdx.x; sg < P; sg += NT) {
+      T val = T(0);
+      if (sg < r.nseg) {
+        const uint32_t src = r.seg_src[sg];
+        val = r.p[(size_t)(src >> 20) * blk + (size_t)v * r.stride + (src & 0xFFFFFu)];
+      }
+      a[sg] = val;
+    }
+  } else {  // one GPU: segment trees of the chunk partials, 4 segments per wavefront pass
+    const T* pv = r.p + (size_t)v * r.stride;
+    constexpr uint32_t NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6;
+    for (uint32_t s0 = w; s0 < P; s0 += 4 * NW) {
+      T o[4];
+      seg_trees<T, 4>(pv, r.nchunks, r.G, s0, NW, r.nseg, o);
+      if (red_lane() == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (s0 + u * NW < P) a[s0 + u * NW] = o[u];
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
+    for (uint32_t i = threadIdx.x; i < len; i += NT) b[i] = a[2 * i] + a[2 * i + 1];
+    __syncthreads();
+    T* t = a;
+    a = b;
+    b = t;
+  }
+  const T tot = a[0];
+  __syncthreads();  // the caller may reuse the LDS
+  return tot;
+}
+constexpr int kRedFinalThreads = 1024;
 
 // ---------------------------------------------------------------------------
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
@@ -464,33 +521,57 @@ __global__ void __launch_bounds__(kBlock) k_maxdiff_final(const uint32_t* __rest
   }
 }
 
-// canonical chunk partial of dot(x, y) over 3-component cells
+__device__ __forceinline__ void load12(const float* p, float v[12]) {  // 3 float4 = 4 rows x (u,v,p)
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  const float4 c = *reinterpret_cast<const float4*>(p + 8);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
+}
+__device__ __forceinline__ void store12(float* p, const float v[12]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
+}
+
+// Four consecutive cells (12 floats) of a 3-component vector, zero past n
+// cells: one 48-byte run per lane (3 x dwordx4) when the whole group is inside.
+__device__ __forceinline__ void load12_upto(const float* p, uint32_t c0, uint32_t n, float v[12]) {
+  if (c0 + 3 < n) {
+    load12(p + 3 * (size_t)c0, v);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) v[e] = (c0 + (uint32_t)e / 3 < n) ? p[3 * (size_t)c0 + e] : 0.0f;
+  }
+}
+// lane value of a 3-component dot: leaf ((a0 b0 + a1 b1) + a2 b2) per cell,
+// ((c0 + c1) + (c2 + c3)) over the lane's cells (cells past n contribute +0
+// leaves: their zeros multiply to +0)
+__device__ __forceinline__ float lane_dot12(const float a[12], const float b[12]) {
+  float t[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t[q] = (a[3 * q] * b[3 * q] + a[3 * q + 1] * b[3 * q + 1]) + a[3 * q + 2] * b[3 * q + 2];
+  return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+// chunk partials of dot(x, y) over 3-component cells
 __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
                                                         const float* __restrict__ y, uint32_t N,
                                                         float* partial) {
-  __shared__ float lds[kBlock];
-  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
-  float acc = 0.0f;
-#pragma unroll
-  for (int q = 0; q < kRedCellsPerThread; ++q) {
-    const size_t c = base + (size_t)kBlock * q;
-    if (c < N) {
-      const float x0 = x[3 * c], x1 = x[3 * c + 1], x2 = x[3 * c + 2];
-      const float y0 = y[3 * c], y1 = y[3 * c + 1], y2 = y[3 * c + 2];
-      acc += x0 * y0;
-      acc += x1 * y1;
-      acc += x2 * y2;
-    }
-  }
-  const float s = block_tree(acc, lds);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  const uint32_t k = red_chunk();
+  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
+  float a[12], b[12];
+  load12_upto(x, c0, N, a);
+  load12_upto(y, c0, N, b);
+  const float r = wave_tree(lane_dot12(a, b));
+  if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
 }
 
-__global__ void __launch_bounds__(kBlock) k_reduce_final(const float* __restrict__ partial,
-                                                         uint32_t np, int mode, float* out,
-                                                         float* inv, float* g0) {
-  __shared__ float lds[kBlock];
-  const float s = block_final(partial, np, lds);
+__global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int mode, float* out, float* inv,
+                                                                   float* g0) {
+  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
+  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
   if (threadIdx.x == 0) {
     const float nrm = sqrtf(s);
     out[0] = nrm;
@@ -533,20 +614,6 @@ __device__ __forceinline__ void ccols4(const CoupledMatrix& A, size_t off, uint3
     c[3] = q.w;
   }
 }
-__device__ __forceinline__ void load12(const float* p, float v[12]) {  // 3 float4 = 4 rows x (u,v,p)
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  const float4 b = *reinterpret_cast<const float4*>(p + 4);
-  const float4 c = *reinterpret_cast<const float4*>(p + 8);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
-}
-__device__ __forceinline__ void store12(float* p, const float v[12]) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
-  *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
-}
-
 // Gathers of the 4-cells-per-thread kernels.  Unused ELL slots and padding
 // rows hold the row's own (valid) index, so a gather can be issued
 // unconditionally (ALWAYS): no branch per load, and the three loads of one
@@ -701,50 +768,73 @@ __device__ __forceinline__ void st_stream(float* p, float v) {
 #endif
 }
 
+typedef float f4a __attribute__((ext_vector_type(4)));
+// 12 floats (4 cells x 3) of a streamed-once basis vector (nontemporal when
+// CFD_CGS_NT), zero past n cells
+__device__ __forceinline__ void ld12_stream(const float* p, uint32_t c0, uint32_t n, float v[12]) {
+  if (c0 + 3 < n) {
+    const f4a* q = reinterpret_cast<const f4a*>(p + 3 * (size_t)c0);
+#if CFD_CGS_NT
+    const f4a a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1),
+              c = __builtin_nontemporal_load(q + 2);
+#else
+    const f4a a = q[0], b = q[1], c = q[2];
+#endif
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 12; ++e) v[e] = (c0 + (uint32_t)e / 3 < n) ? ld_stream(p + 3 * (size_t)c0 + e) : 0.0f;
+  }
+}
+__device__ __forceinline__ void st12_stream(float* p, uint32_t c0, uint32_t n, const float v[12]) {
+  if (c0 + 3 < n) {
+    f4a* q = reinterpret_cast<f4a*>(p + 3 * (size_t)c0);
+    const f4a a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]}, c = {v[8], v[9], v[10], v[11]};
+#if CFD_CGS_NT
+    __builtin_nontemporal_store(a, q);
+    __builtin_nontemporal_store(b, q + 1);
+    __builtin_nontemporal_store(c, q + 2);
+#else
+    q[0] = a;
+    q[1] = b;
+    q[2] = c;
+#endif
+  } else {
+#pragma unroll
+    for (int e = 0; e < 12; ++e)
+      if (c0 + (uint32_t)e / 3 < n) st_stream(p + 3 * (size_t)c0 + e, v[e]);
+  }
+}
+
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j,
-// V_ii = binv[ii] * W_ii
+// V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees only.
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
                                                      const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, float* partial, uint32_t np) {
-  __shared__ float lds[kBlock];
-  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
-  float wv[kRedCellsPerThread][3];
-  bool ok[kRedCellsPerThread];
-#pragma unroll
-  for (int q = 0; q < kRedCellsPerThread; ++q) {
-    const size_t c = base + (size_t)kBlock * q;
-    ok[q] = c < N;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) wv[q][s] = ok[q] ? w[3 * c + s] : 0.0f;
-  }
+  const uint32_t k = red_chunk();
+  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
+  const bool writer = red_lane() == 0 && k < np;
+  float wv[12];
+  load12_upto(w, c0, N, wv);
   for (int ii = 0; ii <= j; ++ii) {
-    const float* v = basis + (size_t)ii * stride;
     const float sc = binv[ii];
-    float acc = 0.0f;
+    float v[12];
+    ld12_stream(basis + (size_t)ii * stride, c0, N, v);
 #pragma unroll
-    for (int q = 0; q < kRedCellsPerThread; ++q) {
-      const size_t c = base + (size_t)kBlock * q;
-      if (ok[q]) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const float vv = sc * ld_stream(v + 3 * c + s);
-          acc += wv[q][s] * vv;
-        }
-      }
-    }
-    const float r = block_tree(acc, lds);
-    if (threadIdx.x == 0) partial[(size_t)ii * np + blockIdx.x] = r;
-    __syncthreads();
+    for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
+    const float r = wave_tree(lane_dot12(wv, v));
+    if (writer) partial[(size_t)ii * np + k] = r;
   }
 }
 
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
-__global__ void __launch_bounds__(kBlock) k_cgs_reduce(const float* __restrict__ partial,
-                                                       uint32_t np, int j, float* H, int m1) {
-  __shared__ float lds[kBlock];
+__global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
+  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
   const int ii = blockIdx.x;
-  const float s = block_final(partial + (size_t)ii * np, np, lds);
+  const float s = red_total<float, kRedFinalThreads>(r, (uint32_t)ii, la, lb);
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
 }
 
@@ -756,60 +846,40 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
                                                             uint32_t N, float* partial) {
-  __shared__ float lds[kBlock];
   __shared__ float hcol[64], scol[64];
   if (threadIdx.x <= (unsigned)j) {
     hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
     scol[threadIdx.x] = binv[threadIdx.x];
   }
   __syncthreads();
-  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
-  float corr[kRedCellsPerThread][3];
+  const uint32_t k = red_chunk();
+  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
+  float corr[12];
 #pragma unroll
-  for (int q = 0; q < kRedCellsPerThread; ++q)
-#pragma unroll
-    for (int s = 0; s < 3; ++s) corr[q][s] = 0.0f;
+  for (int e = 0; e < 12; ++e) corr[e] = 0.0f;
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
-    const float* v = basis + (size_t)ii * stride;
+    float v[12];
+    ld12_stream(basis + (size_t)ii * stride, c0, N, v);
 #pragma unroll
-    for (int q = 0; q < kRedCellsPerThread; ++q) {
-      const size_t c = base + (size_t)kBlock * q;
-      if (c < N) {
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const float vv = sc * ld_stream(v + 3 * c + s);
-          corr[q][s] += h * vv;
-        }
-      }
-    }
+    for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
   }
-  float* out = basis + (size_t)(j + 1) * stride;
-  float acc = 0.0f;
+  float wn[12];
+  load12_upto(w, c0, N, wn);
 #pragma unroll
-  for (int q = 0; q < kRedCellsPerThread; ++q) {
-    const size_t c = base + (size_t)kBlock * q;
-    if (c < N) {
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const float wn = w[3 * c + s] - corr[q][s];
-        st_stream(out + 3 * c + s, wn);
-        acc += wn * wn;
-      }
-    }
-  }
-  const float r = block_tree(acc, lds);
-  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+  for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
+  st12_stream(basis + (size_t)(j + 1) * stride, c0, N, wn);
+  const float r = wave_tree(lane_dot12(wn, wn));
+  if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
 }
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
-// (gmres_logic.wgsl:24-76).  scal[3] = ||w||, scal[4] = 1/||w||, scal[5] = |g[j+1]|.
-__global__ void __launch_bounds__(kBlock) k_norm_givens(const float* __restrict__ partial,
-                                                        uint32_t np, int j, float* H, int m1,
-                                                        float* givens, float* g, float* binv,
-                                                        float* resid_hist) {
-  __shared__ float lds[kBlock];
-  const float s = block_final(partial, np, lds);
+// (gmres_logic.wgsl:24-76).
+__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
+                                                                  float* givens, float* g, float* binv,
+                                                                  float* resid_hist) {
+  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
+  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
   if (threadIdx.x != 0) return;
   const float norm = sqrtf(s);
   H[(size_t)j * m1 + j + 1] = norm;
@@ -1363,13 +1433,15 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
     cx[stride_c + (g - glo)] = 0.0f;
 }
 
-// prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread
+// prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread.
+// agg is a signed local index on a distributed level (aggregates seeded on a
+// lower rank are ghosts of xc below 0).
 __global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* __restrict__ x,
                                                         const float* __restrict__ xc) {
   const uint32_t i0 = 4 * row_id();
   if (i0 >= L.n) return;
   float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const uint4 ag = *reinterpret_cast<const uint4*>(L.agg + i0);
+  const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;  // padding rows (>= n) get 0
   c0 += 1.0f * xc[ag.x];
   if (i0 + 1 < L.n) c1 += 1.0f * xc[ag.y];
@@ -1657,26 +1729,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
 // ---------------------- check_evolution statistics --------------------------
 // AoS view of the reference FluidState (coupled_solver.rs:504 reads the 32-byte
 // records as a flat f32 array): record r = {u.x, u.y, p, d_p, gp.x, gp.y, 0, 0}.
-__device__ __forceinline__ double block_tree_d(double v, double* lds) {
-  const int t = threadIdx.x;
-  lds[t] = v;
-  __syncthreads();
-  if (t < 128) lds[t] = lds[t] + lds[t + 128];
-  __syncthreads();
-  double x = 0.0;
-  if (t < 64) {
-    x = lds[t] + lds[t + 64];
-    x = x + __shfl_down(x, 32);
-    x = x + __shfl_down(x, 16);
-    x = x + __shfl_down(x, 8);
-    x = x + __shfl_down(x, 4);
-    x = x + __shfl_down(x, 2);
-    x = x + __shfl_down(x, 1);
-  }
-  __syncthreads();
-  return x;
-}
-
 __device__ __forceinline__ void view_pair(const StateView& v, uint32_t rec, int pair, float* a,
                                           float* b) {
   if (pair == 0) {
@@ -1699,58 +1751,59 @@ __device__ __forceinline__ void view_pair(const StateView& v, uint32_t rec, int 
 // `var` + (gbase, rec0): the records the variance part reads -- the record of
 // global index gbase + c is ((gbase + c) >> 2) - rec0 in `var` (on one GPU:
 // var = cur, gbase = rec0 = 0; distributed: records fetched from their owners).
+// Leaves per cell: evolution = the 8 squared differences added in field order
+// (u.x, u.y, p, d_p, grad_p.x, grad_p.y, and the unused grad_component pair,
+// which is 0 - 0), then u, v, u^2, v^2 of the (stride-bug) variance record;
+// chunk partials partial[f * np + k] in the canonical tree order.
 __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, StateView prev,
                                                               int have_prev, uint32_t N,
                                                               StateView var, uint64_t gbase,
-                                                              uint64_t rec0, double* partial) {
-  __shared__ double lds[kBlock];
-  const size_t base = (size_t)blockIdx.x * kRedChunkCells + threadIdx.x;
-  double evo = 0.0, su = 0.0, sv = 0.0, squ = 0.0, sqv = 0.0;
-  for (int q = 0; q < kRedCellsPerThread; ++q) {
-    const size_t c = base + (size_t)kBlock * q;
-    if (c >= N) continue;
-    if (have_prev) {
-      for (int pr = 0; pr < 4; ++pr) {
-        float a0, b0, a1, b1;
-        view_pair(cur, (uint32_t)c, pr, &a0, &b0);
-        view_pair(prev, (uint32_t)c, pr, &a1, &b1);
-        const float da = a0 - a1, db = b0 - b1;
-        evo += (double)(da * da);
-        evo += (double)(db * db);
+                                                              uint64_t rec0, double* partial, uint32_t np) {
+  const uint32_t k = red_chunk();
+  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
+  double lf[5][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t c = c0 + q;
+    double evo = 0.0, a_d = 0.0, b_d = 0.0;
+    if (c < N) {
+      if (have_prev) {
+        bool first = true;
+        for (int pr = 0; pr < 4; ++pr) {
+          float a0, b0, a1, b1;
+          view_pair(cur, c, pr, &a0, &b0);
+          view_pair(prev, c, pr, &a1, &b1);
+          const float da = a0 - a1, db = b0 - b1;
+          const double ta = (double)(da * da), tb = (double)(db * db);
+          evo = first ? ta : evo + ta;
+          evo = evo + tb;
+          first = false;
+        }
       }
+      float a, b;
+      const uint64_t gi = gbase + c;
+      view_pair(var, (uint32_t)((gi >> 2) - rec0), (int)(gi & 3), &a, &b);
+      a_d = (double)a;
+      b_d = (double)b;
     }
-    float a, b;
-    const uint64_t gi = gbase + c;
-    view_pair(var, (uint32_t)((gi >> 2) - rec0), (int)(gi & 3), &a, &b);
-    const double ad = (double)a, bd = (double)b;
-    su += ad;
-    sv += bd;
-    squ += ad * ad;
-    sqv += bd * bd;
+    lf[0][q] = evo;
+    lf[1][q] = a_d;
+    lf[2][q] = b_d;
+    lf[3][q] = a_d * a_d;
+    lf[4][q] = b_d * b_d;
   }
-  const double r0 = block_tree_d(evo, lds);
-  const double r1 = block_tree_d(su, lds);
-  const double r2 = block_tree_d(sv, lds);
-  const double r3 = block_tree_d(squ, lds);
-  const double r4 = block_tree_d(sqv, lds);
-  if (threadIdx.x == 0) {
-    double* o = partial + 5 * (size_t)blockIdx.x;
-    o[0] = r0;
-    o[1] = r1;
-    o[2] = r2;
-    o[3] = r3;
-    o[4] = r4;
+#pragma unroll
+  for (int f = 0; f < 5; ++f) {
+    const double r = wave_tree((lf[f][0] + lf[f][1]) + (lf[f][2] + lf[f][3]));
+    if (red_lane() == 0 && k < np) partial[(size_t)f * np + k] = r;
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_evolution_final(const double* __restrict__ partial,
-                                                            uint32_t np, double* out5) {
-  __shared__ double lds[kBlock];
+__global__ void __launch_bounds__(kRedFinalThreads) k_evolution_final(RedSrcD r, double* out5) {
+  __shared__ double la[kRedMaxSegments], lb[kRedMaxSegments];
   for (int f = 0; f < 5; ++f) {
-    double acc = 0.0;
-    for (uint32_t q = threadIdx.x; q < np; q += kBlock) acc += partial[5 * (size_t)q + f];
-    const double r = block_tree_d(acc, lds);
-    if (threadIdx.x == 0) out5[f] = r;
+    const double t = red_total<double, kRedFinalThreads>(r, (uint32_t)f, la, lb);
+    if (threadIdx.x == 0) out5[f] = t;
   }
 }
 
@@ -1768,22 +1821,17 @@ __global__ void __launch_bounds__(kBlock) k_pack(PackArgs a) {
   }
 }
 
-// Per-rank stage 2 of `nvec` canonical reductions: out[v] = tree(partial[v*np ...]).
-__global__ void __launch_bounds__(kBlock) k_stage2_multi(const float* __restrict__ partial,
-                                                         uint32_t np, float* out) {
-  __shared__ float lds[kBlock];
-  const int v = blockIdx.x;
-  const float s = block_final(partial + (size_t)v * np, np, lds);
-  if (threadIdx.x == 0) out[v] = s;
-}
-
-// Rank combine (distributed canonical order): out[v] = ((0 + s_0) + s_1) + ... in rank order.
-__global__ void k_rank_combine(const float* __restrict__ gathered, int R, int nvec, float* out) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= nvec) return;
-  float acc = 0.0f;
-  for (int r = 0; r < R; ++r) acc += gathered[(size_t)r * nvec + v];
-  out[v] = acc;
+// Distributed: this rank's segment values of nvec reductions, one wavefront
+// per segment: out[v * maxseg + s] (blockIdx.y = v).
+template <class T>
+__global__ void __launch_bounds__(kBlock) k_seg_reduce(const T* __restrict__ part, uint32_t np, uint32_t nchunks,
+                                                       uint32_t G, T* out, uint32_t maxseg) {
+  const uint32_t sg = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const uint32_t v = blockIdx.y;
+  const uint32_t nsl = (nchunks + G - 1) / G;
+  T o[1];
+  seg_trees<T, 1>(part + (size_t)v * np, nchunks, G, sg, 0, nsl, o);
+  if (red_lane() == 0 && sg < maxseg) out[(size_t)v * maxseg + sg] = o[0];
 }
 
 // max over ranks of the (u, p) max-diff bit patterns
@@ -1814,13 +1862,15 @@ void launch_update_fields(uint32_t N, float au, float ap, const float* x, float2
   hipLaunchKernelGGL(k_update_fields, dim3(nb), dim3(kBlock), 0, s, N, au, ap, x, u, p, blockmax);
   hipLaunchKernelGGL(k_maxdiff_final, dim3(1), dim3(kBlock), 0, s, blockmax, nb, maxbits);
 }
-void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s) {
-  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
-  if (nb) hipLaunchKernelGGL(k_dot_partial, dim3(nb), dim3(kBlock), 0, s, x, y, N, partial);
+inline unsigned red_blocks(uint32_t N) {  // 4 chunks of 256 cells per 256-thread block
+  const unsigned nch = (N + kRedChunkCells - 1) / kRedChunkCells;
+  return (nch + 3) / 4;
 }
-void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* inv, float* g0,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kBlock), 0, s, partial, np, mode, out, inv, g0);
+void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s) {
+  if (N) hipLaunchKernelGGL(k_dot_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, x, y, N, partial);
+}
+void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0);
 }
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
@@ -1835,21 +1885,20 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      float* partial, uint32_t np, hipStream_t s) {
-  if (np) hipLaunchKernelGGL(k_cgs_dots, dim3(np), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, partial, np);
+  if (N) hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, partial, np);
 }
-void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s) {
-  hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kBlock), 0, s, partial, np, j, H, m1);
+void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
+  hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
                             const float* H, int m1, uint32_t N, float* partial, hipStream_t s) {
-  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
-  if (nb)
-    hipLaunchKernelGGL(k_cgs_update_norm, dim3(nb), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N,
-                       partial);
+  if (N)
+    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1,
+                       N, partial);
 }
-void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
-                        float* g, float* binv, float* resid_hist, hipStream_t s) {
-  hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kBlock), 0, s, partial, np, j, H, m1, givens, g, binv,
+void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
+                        float* resid_hist, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kRedFinalThreads), 0, s, r, j, H, m1, givens, g, binv,
                      resid_hist);
 }
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
@@ -1965,26 +2014,35 @@ size_t init_kernel_attributes(int device) {
   return budget[device];
 }
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
-                              uint64_t gbase, uint64_t rec0, double* partial, hipStream_t s) {
-  const unsigned nb = (unsigned)((N + kRedChunkCells - 1) / kRedChunkCells);
-  if (nb)
-    hipLaunchKernelGGL(k_evolution_partial, dim3(nb), dim3(kBlock), 0, s, cur, prev, have_prev, N, var, gbase,
-                       rec0, partial);
+                              uint64_t gbase, uint64_t rec0, double* partial, uint32_t np, hipStream_t s) {
+  if (N)
+    hipLaunchKernelGGL(k_evolution_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, cur, prev, have_prev, N, var,
+                       gbase, rec0, partial, np);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(k_pack, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a);
 }
-void launch_stage2_multi(const float* partial, uint32_t np, int nvec, float* out, hipStream_t s) {
-  if (nvec > 0) hipLaunchKernelGGL(k_stage2_multi, dim3(nvec), dim3(kBlock), 0, s, partial, np, out);
+template <class T>
+static void seg_reduce(const T* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, T* out, uint32_t maxseg,
+                       hipStream_t s) {
+  if (nvec <= 0 || maxseg == 0) return;
+  const unsigned nb = (maxseg + 3) / 4;
+  hipLaunchKernelGGL(k_seg_reduce<T>, dim3(nb, (unsigned)nvec), dim3(kBlock), 0, s, part, np, nchunks, G, out,
+                     maxseg);
 }
-void launch_rank_combine(const float* gathered, int R, int nvec, float* out, hipStream_t s) {
-  if (nvec > 0) hipLaunchKernelGGL(k_rank_combine, dim3((nvec + 63) / 64), dim3(64), 0, s, gathered, R, nvec, out);
+void launch_seg_reduce(const float* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, float* out,
+                       uint32_t maxseg, hipStream_t s) {
+  seg_reduce(part, np, nchunks, G, nvec, out, maxseg, s);
+}
+void launch_seg_reduce_d(const double* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, double* out,
+                         uint32_t maxseg, hipStream_t s) {
+  seg_reduce(part, np, nchunks, G, nvec, out, maxseg, s);
 }
 void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_max_combine, dim3(1), dim3(64), 0, s, gathered, R, out);
 }
-void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s) {
-  hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kBlock), 0, s, partial, np, out5);
+void launch_evolution_final(const RedSrcD& r, double* out5, hipStream_t s) {
+  hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, out5);
 }
 
 void build_r_m4(const std::vector<uint32_t>& r_row, const std::vector<uint32_t>& r_col, std::vector<int32_t>& out) {

@@ -31,10 +31,62 @@ constexpr uint32_t kMetaDegen = 1u << 3;       // d_c + d_o <= 1e-6 (lambda fall
 constexpr uint32_t kMetaFluxFlip = 1u << 4;    // normal_flux = -stored normal
 constexpr uint32_t kMetaRankShift = 8;         // scalar-row rank of the neighbour (0xFF boundary)
 
-// Canonical reduction contract (mirrors oracle/oracle.cpp): 256 threads x 4 cells
-constexpr int kRedThreads = 256;
-constexpr int kRedCellsPerThread = 4;
-constexpr int kRedChunkCells = kRedThreads * kRedCellsPerThread;
+// Canonical reduction order (rank-invariant; mirrors oracle/oracle.cpp).  A
+// sum over cells is ONE fixed binary tree over global cell indices:
+//   leaf     cell c: its terms added left to right ((t_u + t_v) + t_p)
+//   chunk    256 consecutive cells [256k, 256k + 256): pairwise tree over the
+//            256 leaves (cells past the end: +0).  GPU: one wavefront, lane l
+//            holds cells 4l..4l+3 as ((c0 + c1) + (c2 + c3)), then lanes are
+//            paired at strides 1, 2, ..., 32
+//   segment  G = 2^g consecutive chunks: pairwise tree over G chunk slots
+//            (chunks past the end: +0).  g depends on the GLOBAL cell count
+//            only: g = clamp(floor(log2(N / 16384)), 0, 8)
+//   total    pairwise tree over the segment values, padded with +0 to a power
+//            of two.
+// A rank owns whole segments (partition_starts), so each segment value is
+// computed by one rank and the total from the all-gathered segment values: R
+// ranks produce exactly the bits of one GPU.
+constexpr uint32_t kRedChunkCells = 256;
+constexpr uint32_t kRedCellsPerLane = 4;
+constexpr uint32_t kRedMaxSegLog2 = 8;
+constexpr uint32_t kRedMaxSegments = 4096;  // the total's tree runs in LDS (N <= 268 M cells)
+
+struct RedGeom {
+  uint32_t g = 0;          // log2 chunks per segment
+  uint32_t G = 1;          // chunks per segment
+  uint64_t seg_cells = 256;
+  uint32_t nchunks = 0;    // global chunks
+  uint32_t nseg = 0;       // global segments
+};
+inline RedGeom red_geom(uint64_t nglob) {
+  RedGeom r;
+  uint32_t g = 0;
+  while (g < kRedMaxSegLog2 && (nglob >> (g + 1)) >= 16384u) ++g;
+  r.g = g;
+  r.G = 1u << g;
+  r.seg_cells = (uint64_t)kRedChunkCells << g;
+  r.nchunks = (uint32_t)((nglob + kRedChunkCells - 1) / kRedChunkCells);
+  r.nseg = (uint32_t)((r.nchunks + r.G - 1) / r.G);
+  return r;
+}
+
+// Source of a reduction's segment values for the kernels that finish it
+// (the total's tree).  One GPU: chunk partials p[v * stride + k], k < nchunks,
+// the segment trees are built from them.  Distributed: the all-gathered
+// segment values, rank q's block [q][v][local segment] of nvec x stride
+// values; seg_src[s] = (q << 20) | local segment of global segment s.
+template <class T>
+struct RedSrcT {
+  const T* p = nullptr;
+  uint32_t stride = 0;
+  uint32_t nchunks = 0;
+  uint32_t G = 1;
+  uint32_t nseg = 0;
+  uint32_t nvec = 1;
+  const uint32_t* seg_src = nullptr;
+};
+using RedSrc = RedSrcT<float>;
+using RedSrcD = RedSrcT<double>;
 
 // Local cell numbering: every per-cell device pointer points at the first
 // OWNED cell; neighbour indices are signed offsets from it.  On one GPU they
@@ -204,23 +256,25 @@ void launch_assemble(const AssembleArgs& a, hipStream_t s);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
                           float* p, uint32_t* blockmax, uint32_t* maxbits, hipStream_t s);
+// chunk partials of dot(x, y) over 3-component cells: partial[k], k < ceil(N / 256)
 void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s);
-// mode 1: out[0] = sqrt(sum); mode 2: out[0] = sqrt, *inv = 1.0f / sqrt (host-style)
-// and g0 (if non-null) = sqrt
-void launch_reduce_final(const float* partial, uint32_t np, int mode, float* out, float* inv,
-                         float* g0, hipStream_t s);
+// total of the reduction r (one vector): mode 1: out[0] = sqrt(total); mode 2:
+// also *inv = 1.0f / sqrt (host-style) and g0 (if non-null) = sqrt
+void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s);
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
-// basis: unnormalised W_i at basis + i*stride, scales binv[i]
+// basis: unnormalised W_i at basis + i*stride, scales binv[i]; chunk partials
+// partial[ii * np + k] of <w, V_ii>, ii = 0..j
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
                      uint32_t N, float* partial, uint32_t np, hipStream_t s);
-void launch_cgs_reduce(const float* partial, uint32_t np, int j, float* H, int m1, hipStream_t s);
-// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 partials
+// H[j][ii] = total of vector ii of r (r.nvec = j + 1)
+void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
+// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 chunk partials
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
                             const float* H, int m1, uint32_t N, float* partial, hipStream_t s);
-// ||W_{j+1}|| final -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|
-void launch_norm_givens(const float* partial, uint32_t np, int j, float* H, int m1, float* givens,
-                        float* g, float* binv, float* resid_hist, hipStream_t s);
+// ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|
+void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
+                        float* resid_hist, hipStream_t s);
 // r_in = binv[j] * W_j
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
@@ -264,19 +318,22 @@ void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, h
 // thread-safe; throws on failure) and returns their LDS budget there:
 // min(kTailLdsMax, the device's opt-in per-block LDS).  Call with `device` current.
 size_t init_kernel_attributes(int device);
-// check_evolution (coupled_solver.rs:501-580) statistics in canonical f64 order:
-// partial[5*chunk + {0..4}] = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
+// check_evolution (coupled_solver.rs:501-580) statistics in the canonical order (f64):
+// chunk partials partial[f * np + k], f = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
 // The variance part reads record ((gbase + c) >> 2) - rec0 of `var` (stride bug, §0.1-12).
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N,
-                              StateView var, uint64_t gbase, uint64_t rec0, double* partial,
+                              StateView var, uint64_t gbase, uint64_t rec0, double* partial, uint32_t np,
                               hipStream_t s);
 // ---- distributed helpers ----
 void launch_pack(const PackArgs& a, hipStream_t s);
-// out[v] = canonical stage 2 of partial[v*np .. v*np+np) (this rank's sum)
-void launch_stage2_multi(const float* partial, uint32_t np, int nvec, float* out, hipStream_t s);
-// out[v] = ((0 + g[0][v]) + g[1][v]) + ... (rank order)
-void launch_rank_combine(const float* gathered, int R, int nvec, float* out, hipStream_t s);
+// distributed: this rank's segment values out[v * maxseg + s] of nvec reductions
+// from their chunk partials part[v * np + k] (k < nchunks local, G chunks per segment)
+void launch_seg_reduce(const float* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, float* out,
+                       uint32_t maxseg, hipStream_t s);
+void launch_seg_reduce_d(const double* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, double* out,
+                         uint32_t maxseg, hipStream_t s);
 void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s);
-void launch_evolution_final(const double* partial, uint32_t np, double* out5, hipStream_t s);
+// out5[f] = total of the 5 check_evolution sums (r.nvec = 5)
+void launch_evolution_final(const RedSrcD& r, double* out5, hipStream_t s);
 
 }  // namespace cfd2

@@ -4,9 +4,10 @@
 //   transpose            amg.rs:141-185  R = P^T, fine indices ascending per row
 //   galerkin_product     amg.rs:187-235  (R*A)*P, f32 accumulation in visit order
 //   level loop           amg.rs:374-595  stop at n <= 100, no reduction, or 20 levels
-// Distributed solver: the aggregation runs part by part (rank ranges of the
-// level's rows) and never lets an aggregate cross a part; with
-// one part this is exactly the reference's greedy index-order aggregation.
+// Distributed solver: the same global aggregation (so the hierarchy, and every
+// result, does not depend on the rank count); a coarse row belongs to the rank
+// that owns its seed, the aggregate's first (smallest) fine row, so coarse rows
+// stay contiguous per rank and an aggregate may reach into the next ranks.
 // The hierarchy is built once (first AMG solve) and frozen.
 // P and R hold only 1.0 values, so they are stored as index arrays.
 #include <algorithm>
@@ -91,35 +92,23 @@ uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, co
   const uint32_t NONE = std::numeric_limits<uint32_t>::max();
   agg.assign(n, NONE);
   cpart.assign(part.size(), 0);
-  const size_t nparts = part.size() - 1;
-  std::vector<uint32_t> pcount(nparts, 0);
-  // greedy index-order aggregation, part by part: parts are independent
-  // (neighbours outside the part never join), so they run in parallel with
-  // local numbering, then are offset by the aggregates of earlier parts
-#pragma omp parallel for schedule(dynamic, 1)
-  for (long p = 0; p < (long)nparts; ++p) {
-    const uint64_t lo = part[p], hi = part[p + 1];
-    uint32_t na = 0;
-    for (size_t i = lo; i < hi; ++i) {
-      if (agg[i] != NONE) continue;
-      agg[i] = na;
-      for (uint32_t k = row[i]; k < row[i + 1]; ++k) {
-        const uint32_t j = col[k];
-        if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = na;
-      }
-      ++na;
-    }
-    pcount[p] = na;
-  }
+  // greedy index-order pass (amg.rs:84-116): a row still free becomes a seed
+  // and takes every free neighbour.  Rows before a seed are all taken, so the
+  // seed is its aggregate's smallest row and aggregates are numbered in seed
+  // order: cpart[q] = first aggregate seeded at or after part[q].
   uint32_t nagg = 0;
-  for (size_t p = 0; p < nparts; ++p) {
-    cpart[p] = nagg;
-    nagg += pcount[p];
+  size_t q = 0;
+  for (size_t i = 0; i < n; ++i) {
+    while (q + 1 < part.size() && part[q] <= i) cpart[q++] = nagg;
+    if (agg[i] != NONE) continue;
+    agg[i] = nagg;
+    for (uint32_t k = row[i]; k < row[i + 1]; ++k) {
+      const uint32_t j = col[k];
+      if (agg[j] == NONE) agg[j] = nagg;
+    }
+    ++nagg;
   }
-  cpart.back() = nagg;
-#pragma omp parallel for schedule(dynamic, 1)
-  for (long p = 0; p < (long)nparts; ++p)
-    for (size_t i = part[p]; i < part[p + 1]; ++i) agg[i] += (uint32_t)cpart[p];
+  while (q < part.size()) cpart[q++] = nagg;
   return nagg;
 }
 
@@ -138,8 +127,8 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
                                                const std::vector<uint64_t>& part0) {
   std::vector<AmgHostLevel> levels;
   HostCsr cur = fine;
-  // row partition of the current level (distributed solver): aggregates never
-  // cross a part, so coarse rows stay contiguous per rank (seed order = rank order)
+  // row partition of the current level (distributed solver): coarse rows
+  // follow their seeds (seed order = rank order)
   std::vector<uint64_t> part = part0.empty() ? std::vector<uint64_t>{0, (uint64_t)fine.rows} : part0;
   for (size_t li = 0; li < max_levels; ++li) {
     AmgHostLevel L;

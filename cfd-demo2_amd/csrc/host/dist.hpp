@@ -1,7 +1,7 @@
 // Slab partition and halo plans of the distributed solver.
 //
-// Rank r owns the contiguous global rows [start(r), start(r+1)), start(r) =
-// floor(n r / R).  The cut-cell mesher numbers cells x-major, so these are
+// Rank r owns the contiguous global rows [start(r), start(r+1)), whole
+// segments of the canonical reduction tree (partition_starts).  The cut-cell mesher numbers cells x-major, so these are
 // vertical slabs and a rank's ghosts come from its slab neighbours.  A rank
 // stores ghosts of lower ranks at local indices [-glo, 0) and of higher ranks
 // at [npad, npad + ghi) (npad = owned rows rounded up to 64), so local order
@@ -42,6 +42,18 @@ struct HaloPlan {
 // (row[0..n], col); returns glo (ghosts below c0).
 uint32_t collect_ghosts(uint64_t c0, uint64_t c1, const uint32_t* row, uint32_t n, const uint32_t* col,
                         std::vector<uint32_t>& ghost);
+
+// Rows of [0, n) that read lower ghosts end before lo_end, rows reading upper
+// ghosts start at hi_begin (multiples of 4; the rows between are interior).
+void interior_rows(const std::vector<uint64_t>& starts, int rank, const uint32_t* row, uint32_t n,
+                   const uint32_t* col, uint32_t& lo_end, uint32_t& hi_begin);
+
+// Halo plan from every rank's ghost list (ascending global ids): this rank
+// receives its ghosts owned by q from q and sends q the rows of q's list it
+// owns (general patterns: the AMG levels, whose ghosts include the coarse
+// rows their prolongation reads).  lo_end / hi_begin are left at 0.
+HaloPlan build_halo_plan_lists(const std::vector<uint64_t>& starts, int rank,
+                               const std::vector<std::vector<uint32_t>>& ghosts, uint32_t glo, uint32_t npad);
 
 // Halo plan for a symmetric pattern: the rows this rank sends to peer q are its
 // owned rows with a column owned by q (= q's ghosts from this rank).

@@ -68,6 +68,9 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   build_topology(mesh, topo, (uint32_t)starts[rk], (uint32_t)starts[rk + 1]);
   N = topo.N;
   F = topo.F;
+  red = red_geom(NG);
+  if (red.nseg > kRedMaxSegments)
+    throw std::invalid_argument("mesh too large for the reduction tree (at most 268 M cells)");
   nchunks = (N + kRedChunkCells - 1) / kRedChunkCells;
   shift = (topo.glo + 63) & ~63u;
   vlen = (size_t)shift + topo.npad + topo.ghi;
@@ -89,11 +92,21 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
     cell_plan = build_halo_plan(starts, rk, topo.srow.data(), N, topo.scol.data(), topo.ghost, topo.glo,
                                 topo.npad);
     make_plan_buffers(cell_plan, 8);
-    red_local = arena.alloc<float>(m1 + 1);
-    red_gather = arena.alloc<float>((size_t)R * (m1 + 1));
-    red_comb = arena.alloc<float>(m1 + 1);
+    // segments of every rank (ranks own whole segments: partition_starts)
+    std::vector<uint32_t> src(red.nseg);
+    for (int q = 0; q < R; ++q) {
+      const uint64_t s0 = starts[q] / red.seg_cells;
+      const uint64_t s1 = (starts[q + 1] + red.seg_cells - 1) / red.seg_cells;
+      maxseg = std::max(maxseg, (uint32_t)(s1 - s0));
+      for (uint64_t sg = s0; sg < s1; ++sg) src[sg] = ((uint32_t)q << 20) | (uint32_t)(sg - s0);
+    }
+    if (maxseg >= (1u << 20) || R >= (1 << 12)) throw std::invalid_argument("too many segments / ranks");
+    d_seg_src = arena.upload(src, stream);
+    red_local = arena.alloc<float>((size_t)m1 * maxseg);
+    red_gather = arena.alloc<float>((size_t)R * m1 * maxseg);
+    red_local_d = arena.alloc<double>((size_t)5 * maxseg);
+    red_gather_d = arena.alloc<double>((size_t)R * 5 * maxseg);
     mx_gather = arena.alloc<uint32_t>(2 * (size_t)R);
-    ev_gather = arena.alloc<double>(5 * (size_t)R);
     d_u64 = arena.alloc<uint64_t>((size_t)R + 1);  // not lazily: the AMG build runs on amg_arena
     // check_evolution's stride bug reads records (i >> 2) of the global state
     ev_a = (uint64_t)topo.c0 >> 2;
@@ -349,14 +362,45 @@ void Solver::halo_state(bool all) {
     halo(cell_plan, {{(float*)s.u, 2}, {s.p, 1}});
 }
 
-// Distributed canonical reduction: per-rank stage 2, all-gather, rank-ordered
-// sum; the final kernels then read (combined, np = 1).
-std::pair<const float*, uint32_t> Solver::combine(const float* partial, uint32_t np, int nvec) {
-  if (!dist()) return {partial, np};
-  launch_stage2_multi(partial, np, nvec, red_local, stream);
-  comm->allgather(red_local, red_gather, (size_t)nvec * sizeof(float), stream);
-  launch_rank_combine(red_gather, R, nvec, red_comb, stream);
-  return {red_comb, 1u};
+// Canonical reductions (kernels.hpp): one GPU hands the chunk partials to the
+// finishing kernel; a distributed rank reduces its own segments, all-gathers
+// the segment values, and every rank finishes the same global tree.
+RedSrc Solver::combine(const float* part, int nvec) {
+  RedSrc r;
+  r.G = red.G;
+  r.nseg = red.nseg;
+  r.nvec = (uint32_t)nvec;
+  if (!dist()) {
+    r.p = part;
+    r.stride = nchunks;
+    r.nchunks = nchunks;
+    return r;
+  }
+  launch_seg_reduce(part, nchunks, nchunks, red.G, nvec, red_local, maxseg, stream);
+  comm->allgather(red_local, red_gather, (size_t)nvec * maxseg * sizeof(float), stream);
+  r.p = red_gather;
+  r.stride = maxseg;
+  r.seg_src = d_seg_src;
+  return r;
+}
+
+RedSrcD Solver::combine_d(const double* part, int nvec) {
+  RedSrcD r;
+  r.G = red.G;
+  r.nseg = red.nseg;
+  r.nvec = (uint32_t)nvec;
+  if (!dist()) {
+    r.p = part;
+    r.stride = nchunks;
+    r.nchunks = nchunks;
+    return r;
+  }
+  launch_seg_reduce_d(part, nchunks, nchunks, red.G, nvec, red_local_d, maxseg, stream);
+  comm->allgather(red_local_d, red_gather_d, (size_t)nvec * maxseg * sizeof(double), stream);
+  r.p = red_gather_d;
+  r.stride = maxseg;
+  r.seg_src = d_seg_src;
+  return r;
 }
 
 // ------------------------------------------------------------------ kernels
@@ -539,10 +583,10 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 
 // ensure_amg_resources (coupled_solver_fgmres.rs:174-209): read back the live
 // scalar matrix, build the frozen hierarchy on the host, upload it.  A
-// distributed rank all-gathers the scalar matrix, builds the same partition-
-// aware hierarchy as every other rank, and keeps its rows of the levels with
-// more than CFD_AMG_REPLICATE_ROWS rows (default 262144); the small levels are
-// replicated on every rank.
+// distributed rank all-gathers the scalar matrix, builds the GLOBAL hierarchy
+// (the one a single GPU builds, so results do not depend on the rank count)
+// and keeps its rows of the levels with more than CFD_AMG_REPLICATE_ROWS rows
+// (default 262144); the small levels are replicated on every rank.
 // Unconditional slot loads (kernels.hip gather_group) on level 0 (the face
 // stencil: rows fill the ELL width) and on latency-bound small levels;
 // predicated loads on the big coarse levels, whose row lengths vary (same-box
@@ -628,39 +672,79 @@ void Solver::build_amg_host() {
         break;
       }
   }
+  // Ghost lists of every rank on the distributed levels (the halo plans need
+  // both directions): the matrix columns outside the rank's rows, plus on a
+  // coarse level the aggregates of the rank's finer rows that another rank
+  // owns (an aggregate belongs to its seed's rank and may reach into the next
+  // ranks: the prolongation reads those coarse values, the restriction the
+  // fine residuals of members owned by the next ranks, which are matrix
+  // neighbours of the seed and so already ghosts of the seed's rank).
+  std::vector<std::vector<std::vector<uint32_t>>> ghosts(amg_g);
+  for (int li = 0; li < amg_g; ++li) {
+    const AmgHostLevel& HL = H[li];
+    ghosts[li].resize(R);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int q = 0; q < R; ++q) {
+      auto& gq = ghosts[li][q];
+      const uint64_t C0 = HL.part[q], C1 = HL.part[q + 1];
+      for (uint64_t i = C0; i < C1; ++i)
+        for (uint32_t k = HL.A.row[i]; k < HL.A.row[i + 1]; ++k) {
+          const uint32_t c = HL.A.col[k];
+          if (c < C0 || c >= C1) gq.push_back(c);
+        }
+      if (li > 0) {
+        const AmgHostLevel& HF = H[li - 1];
+        for (uint64_t i = HF.part[q]; i < HF.part[q + 1]; ++i) {
+          const uint32_t a = HF.agg[i];
+          if (a < C0 || a >= C1) gq.push_back(a);
+        }
+      }
+      std::sort(gq.begin(), gq.end());
+      gq.erase(std::unique(gq.begin(), gq.end()), gq.end());
+    }
+  }
+  // signed local index of global row c of distributed level li on this rank
+  auto rel_of = [&](int li, uint64_t c) -> int32_t {
+    const AmgGpuLevel& G = levels[li];
+    if (c >= G.C0 && c < G.C1) return (int32_t)(c - G.C0);
+    const auto& gh = ghosts[li][rk];
+    const auto it = std::lower_bound(gh.begin(), gh.end(), (uint32_t)c);
+    if (it == gh.end() || *it != c) throw std::logic_error("AMG: row is neither owned nor a ghost");
+    const uint32_t k = (uint32_t)(it - gh.begin());
+    return k < G.glo ? (int32_t)k - (int32_t)G.glo : (int32_t)(G.npad + (k - G.glo));
+  };
   levels.assign(L, AmgGpuLevel{});
   auto zeroed = [&](size_t cnt) {
     float* p = arena.alloc<float>(cnt + 64);
     CFD_HIP(hipMemsetAsync(p, 0, (cnt + 64) * sizeof(float), stream));
     return p;
   };
-  for (int li = 0; li < L; ++li) {
+  for (int li = 0; li < L; ++li) {  // layouts first: P of level li needs level li + 1's
     const AmgHostLevel& HL = H[li];
     AmgGpuLevel& G = levels[li];
     G.nglob = HL.A.rows;
     G.part = HL.part;
     G.C0 = HL.part[rk];
     G.C1 = HL.part[rk + 1];
-    if (li < amg_g) {  // distributed level: owned rows + ghosts
+    if (li < amg_g) {
       G.dist = true;
+      const auto& gh = ghosts[li][rk];
+      G.glo = (uint32_t)(std::lower_bound(gh.begin(), gh.end(), (uint32_t)G.C0) - gh.begin());
+      G.ghi = (uint32_t)gh.size() - G.glo;
+      G.npad = (uint32_t)(((G.C1 - G.C0) + 63) & ~(uint64_t)63);
+    }
+  }
+  for (int li = 0; li < L; ++li) {
+    const AmgHostLevel& HL = H[li];
+    AmgGpuLevel& G = levels[li];
+    if (G.dist) {  // distributed level: owned rows + ghosts
       const uint32_t n = (uint32_t)(G.C1 - G.C0);
-      std::vector<uint32_t> ghost;
       std::vector<uint32_t> lrow(n + 1);
       for (uint32_t i = 0; i <= n; ++i) lrow[i] = HL.A.row[G.C0 + i] - HL.A.row[G.C0];
       const uint32_t* lcol = HL.A.col.data() + HL.A.row[G.C0];
-      G.glo = collect_ghosts(G.C0, G.C1, lrow.data(), n, lcol, ghost);
-      G.ghi = (uint32_t)ghost.size() - G.glo;
-      G.npad = (n + 63) & ~63u;
-      const uint64_t C0 = G.C0, C1 = G.C1;
-      const uint32_t glo = G.glo, npad = G.npad;
-      auto rel = [&](uint32_t c) -> int32_t {
-        if (c >= C0 && c < C1) return (int32_t)(c - C0);
-        const auto it = std::lower_bound(ghost.begin(), ghost.end(), c);
-        const uint32_t k = (uint32_t)(it - ghost.begin());
-        return k < glo ? (int32_t)k - (int32_t)glo : (int32_t)(npad + (k - glo));
-      };
-      level_image(HL.A, C0, n, rel, G, arena, stream, amg_wide_limit);
-      G.plan = build_halo_plan(HL.part, rk, lrow.data(), n, lcol, ghost, G.glo, G.npad);
+      level_image(HL.A, G.C0, n, [&](uint32_t c) { return rel_of(li, c); }, G, arena, stream, amg_wide_limit);
+      G.plan = build_halo_plan_lists(HL.part, rk, ghosts[li], G.glo, G.npad);
+      interior_rows(HL.part, rk, lrow.data(), n, lcol, G.plan.lo_end, G.plan.hi_begin);
       make_plan_buffers(G.plan, 1);
       if (li == 0) {
         if (G.glo != topo.glo || G.ghi != topo.ghi || G.npad != topo.npad)
@@ -687,19 +771,26 @@ void Solver::build_amg_host() {
       }
     }
     set_amg_full_policy(G, li);
-    // coarsening operators: P as an aggregate index per stored fine row, R = P^T
+    // coarsening operators: P as an aggregate index per stored fine row
+    // (signed local coarse index into a distributed next level, global id into
+    // a replicated one), R = P^T rows of this rank's aggregates with local fine
+    // members (owned, or ghosts of the next ranks)
     if (HL.has_op) {
       const AmgHostLevel& HC = H[li + 1];
-      const bool next_dist = (li + 1 < amg_g);
+      const bool next_dist = levels[li + 1].dist;
       std::vector<uint32_t> agg(G.dev.stride, 0), r_row, r_col;
       if (G.dist) {
-        const uint64_t cbase = next_dist ? HC.part[rk] : 0;  // replicated next: global ids
-        for (uint64_t i = G.C0; i < G.C1; ++i) agg[i - G.C0] = (uint32_t)(HL.agg[i] - cbase);
+        for (uint64_t i = G.C0; i < G.C1; ++i)
+          agg[i - G.C0] = next_dist ? (uint32_t)rel_of(li + 1, HL.agg[i]) : HL.agg[i];
         const uint64_t I0 = HC.part[rk], I1 = HC.part[rk + 1];
         r_row.resize(I1 - I0 + 1);
         for (uint64_t I = I0; I <= I1; ++I) r_row[I - I0] = HL.r_row[I] - HL.r_row[I0];
         r_col.assign(HL.r_col.begin() + HL.r_row[I0], HL.r_col.begin() + HL.r_row[I1]);
-        for (auto& f : r_col) f -= (uint32_t)G.C0;
+        for (auto& f : r_col) {
+          const int32_t lf = rel_of(li, f);
+          if (lf < 0) throw std::logic_error("AMG: aggregate member below its seed's rank");
+          f = (uint32_t)lf;
+        }
         G.dev.nc = (uint32_t)(I1 - I0);
       } else {
         std::copy(HL.agg.begin(), HL.agg.end(), agg.begin());
@@ -1060,6 +1151,8 @@ void Solver::v_cycle() {
     else
       sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
     res(i);
+    // the restriction sums members owned by the next ranks too (their residuals are ghosts)
+    if (Lv.dist) halo(Lv.plan, {{Lv.r, 1}});
     AmgGpuLevel& C = levels[i + 1];
     // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
     presmoothed = fuse_presmooth && (i + 1 < down) && (!Lv.dist || C.dist);
@@ -1087,6 +1180,8 @@ void Solver::v_cycle() {
     for (int s = 0; s < 10; ++s) sm(L - 1, s == 0 && L > 1);
   }
   for (int ii = down - 1; ii >= 0; --ii) {
+    // the prolongation reads aggregates seeded on lower ranks (ghosts of the coarse x)
+    if (levels[ii + 1].dist) halo(levels[ii + 1].plan, {{levels[ii + 1].x, 1}});
     launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
     sm(ii, false);
   }
@@ -1137,8 +1232,7 @@ void Solver::precondition(int j, float* z) {
 
 float Solver::norm_blocking(const float* v, int mode, int slot) {
   launch_dot_partial(v, v, N, partial_n, stream);
-  const auto red = combine(partial_n, nchunks, 1);
-  launch_reduce_final(red.first, red.second, mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
+  launch_reduce_final(combine(partial_n, 1), mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
   CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   return h_pin[0];
@@ -1210,11 +1304,9 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         launch_spmv(A, zj, w, stream);
       });
       launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);
-      const auto rd = combine(partial, nchunks, j + 1);
-      launch_cgs_reduce(rd.first, rd.second, j, H, m1, stream);
+      launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
-      const auto rn = combine(partial_n, nchunks, 1);
-      launch_norm_givens(rn.first, rn.second, j, H, m1, givens, g, binv, resid_hist, stream);
+      launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, stream);
       check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
@@ -1349,27 +1441,14 @@ void Solver::check_evolution() {
     gbase = topo.c0;
     rec0 = ev_a;
   }
-  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, stream);
+  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, nchunks, stream);
   double* out5 = partial_d + 5 * (size_t)nchunks;
-  launch_evolution_final(partial_d, nchunks, out5, stream);
+  launch_evolution_final(combine_d(partial_d, 5), out5, stream);
   check_launch("check_evolution");
   double tot[5];
-  if (dist()) {
-    std::vector<double> gth(5 * (size_t)R);
-    comm->allgather(out5, ev_gather, 5 * sizeof(double), stream);
-    CFD_HIP(hipMemcpyAsync(gth.data(), ev_gather, gth.size() * sizeof(double), hipMemcpyDeviceToHost, stream));
-    copy_state(S(), prev, 0, N, stream);
-    sync();
-    for (int f = 0; f < 5; ++f) {  // rank-ordered combine
-      double acc = 0.0;
-      for (int q = 0; q < R; ++q) acc += gth[5 * (size_t)q + f];
-      tot[f] = acc;
-    }
-  } else {
-    CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
-    copy_state(S(), prev, 0, N, stream);
-    sync();
-  }
+  CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
+  copy_state(S(), prev, 0, N, stream);
+  sync();
   const double nn = (double)NG;
   const double mean_u = tot[1] / nn, mean_v = tot[2] / nn;
   const double var_u = std::fmax(tot[3] / nn - mean_u * mean_u, 0.0);

@@ -136,8 +136,9 @@ struct AmgHostLevel {
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
                                                const std::vector<uint64_t>& part = {});
 // Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
-// n rows, part by part (aggregates never cross a part); returns the aggregate
-// count, agg[i] = aggregate of row i, cpart = aggregate partition.
+// n rows; returns the aggregate count, agg[i] = aggregate of row i, and
+// cpart = the aggregate partition induced by the row partition `part` (an
+// aggregate belongs to the part of its seed, its smallest row).
 uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, const std::vector<uint64_t>& part,
                           std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart);
 // R = P^T of piecewise-constant P: rows = aggregates, fine indices ascending
@@ -184,11 +185,17 @@ struct Solver {
   size_t vlen = 0;               // elements per component of a per-cell vector
   HaloPlan cell_plan;
   uint64_t* d_u64 = nullptr;     // [R + 1] all-gather scratch of allgather_u64
-  float* red_local = nullptr;    // [m1] this rank's reduction results
-  float* red_gather = nullptr;   // [R * m1]
-  float* red_comb = nullptr;     // [m1]
+  // canonical reductions (kernels.hpp): geometry of the global tree; a
+  // distributed rank all-gathers its segment values ([v][local segment],
+  // maxseg slots per vector) and every rank finishes the same tree
+  RedGeom red;
+  uint32_t maxseg = 0;           // most segments any rank owns
+  uint32_t* d_seg_src = nullptr; // [nseg] (owner << 20) | local segment
+  float* red_local = nullptr;    // [m1 * maxseg]
+  float* red_gather = nullptr;   // [R * m1 * maxseg]
+  double* red_local_d = nullptr; // [5 * maxseg] check_evolution
+  double* red_gather_d = nullptr;
   uint32_t* mx_gather = nullptr; // [2R]
-  double* ev_gather = nullptr;   // [5R]
   StateView evrec{};             // check_evolution records fetched from their owners
   uint64_t ev_a = 0, ev_b = 0;   // record range [ev_a, ev_b) this rank's variance reads
   int amg_g = 0;                 // first replicated AMG level (distributed)
@@ -233,7 +240,7 @@ struct Solver {
   float* temp = nullptr;
   float* temp_p = nullptr;
   float* p_sol = nullptr;
-  float* partial = nullptr;      // [(m+1) * nchunks]
+  float* partial = nullptr;      // [(m+1) * nchunks] chunk partials (256 cells each)
   float* partial_n = nullptr;    // [nchunks]
   double* partial_d = nullptr;   // [5 * nchunks] check_evolution
   float* dsc = nullptr;          // device scalars
@@ -289,9 +296,6 @@ struct Solver {
     uint32_t* col_c = nullptr;
     float* val_c = nullptr;
     size_t nnz_own = 0;
-    float* val_all = nullptr;            // first replicated level: all-gathered values
-    std::vector<size_t> coff;            // byte offsets of each rank's values in val_all
-    size_t e_own = 0;                    // this rank's first value in val_all
   };
   std::vector<AmgRefreshLevel> amg_refresh;
   uint32_t* amg_setup_flag = nullptr;  // k_galerkin overflow flag (amg_arena)
@@ -434,7 +438,11 @@ struct Solver {
   hipStream_t cstream = nullptr;  // RCCL / peer-copy stream of the halo exchanges
   hipEvent_t hev_pack = nullptr, hev_done = nullptr;
   void halo_state(bool all);
-  std::pair<const float*, uint32_t> combine(const float* partial, uint32_t np, int nvec);
+  // the source the finishing kernels read for nvec reductions of chunk
+  // partials part[v * nchunks + k]: the partials themselves on one GPU; on a
+  // distributed rank its segment values are computed and all-gathered first
+  RedSrc combine(const float* part, int nvec);
+  RedSrcD combine_d(const double* part, int nvec);
   void make_plan_buffers(HaloPlan& p, int max_comps);
   void build_dist_amg(std::vector<AmgHostLevel>& H);
 };

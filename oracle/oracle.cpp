@@ -39,71 +39,77 @@ int fail(const std::string& m) {
 }
 
 // ---------------------------------------------------------------------------
-// Canonical reduction order (shared contract with the HIP kernels):
-//   vectors of 3 floats per cell; chunk = 1024 cells; 256 "threads" per chunk,
-//   thread t serially sums cells c = 1024*k + t + 256*q (q = 0..3, c < N),
-//   components s = 0..2 in order; then a halving tree (128,64,...,1) over the
-//   256 thread sums.  Stage 2: thread t sums partials t, t+256, ... serially,
-//   then the same halving tree.
-constexpr int kThreads = 256;
-constexpr int kCellsPerThread = 4;
-constexpr int kChunkCells = kThreads * kCellsPerThread;
+// Canonical reduction order (shared contract with the HIP kernels,
+// cfd-demo2_amd/csrc/hip/kernels.hpp).  The reference sums with 64-lane
+// workgroup trees plus a serial single-thread pass (gmres_ops.wgsl:159-293);
+// any fixed order is a valid restatement, and this one is a single binary
+// tree over GLOBAL cell indices, so a distributed solver reproduces it
+// exactly on any rank count:
+//   leaf     cell c: its terms added left to right ((t0 + t1) + t2)
+//   chunk    256 cells: pairwise tree over the 256 leaves (missing: +0)
+//   segment  G = 2^g chunks: pairwise tree over G chunk slots (missing: +0),
+//            g = clamp(floor(log2(N / 16384)), 0, 8) for the global N
+//   total    pairwise tree over the segment values padded to a power of two
+constexpr size_t kChunkCells = 256;
 
-inline float tree256(float* s) {
-  for (int h = kThreads / 2; h >= 1; h >>= 1)
-    for (int t = 0; t < h; ++t) s[t] = s[t] + s[t + h];
-  return s[0];
+struct RedGeom {
+  size_t G = 1, nchunks = 0, nseg = 0;
+};
+inline RedGeom red_geom(size_t n) {
+  RedGeom r;
+  unsigned g = 0;
+  while (g < 8 && (n >> (g + 1)) >= 16384u) ++g;
+  r.G = (size_t)1 << g;
+  r.nchunks = (n + kChunkCells - 1) / kChunkCells;
+  r.nseg = (r.nchunks + r.G - 1) / r.G;
+  return r;
 }
 
-inline size_t num_chunks(size_t ncells) { return (ncells + kChunkCells - 1) / kChunkCells; }
+// pairwise tree over v[0, n), n a power of two: ((v0 + v1) + (v2 + v3)) + ...
+template <class T>
+T pairwise(T* v, size_t n) {
+  for (size_t len = n / 2; len >= 1; len /= 2)
+    for (size_t i = 0; i < len; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+  return v[0];
+}
 
-template <class F>  // F(cell, comp) -> float term
-float canon_partial(size_t chunk, size_t ncells, F term) {
-  float s[kThreads];
-  for (int t = 0; t < kThreads; ++t) {
-    float acc = 0.0f;
-    for (int q = 0; q < kCellsPerThread; ++q) {
-      const size_t c = chunk * kChunkCells + t + (size_t)kThreads * q;
-      if (c < ncells)
-        for (int comp = 0; comp < 3; ++comp) acc += term(c, comp);
+// canonical sum over `ncells` cells of the leaves leaf(c) (T = float / double)
+template <class T, class Leaf>
+T canon_sum(size_t ncells, Leaf leaf) {
+  const RedGeom g = red_geom(ncells);
+  std::vector<T> chunk(g.nchunks);
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < (long)g.nchunks; ++k) {
+    T lv[kChunkCells];
+    for (size_t i = 0; i < kChunkCells; ++i) {
+      const size_t c = (size_t)k * kChunkCells + i;
+      lv[i] = c < ncells ? leaf(c) : T(0);
     }
-    s[t] = acc;
+    chunk[k] = pairwise(lv, kChunkCells);
   }
-  return tree256(s);
-}
-
-inline float canon_final(const float* partials, size_t np) {
-  float s[kThreads];
-  for (int t = 0; t < kThreads; ++t) {
-    float acc = 0.0f;
-    for (size_t q = t; q < np; q += kThreads) acc += partials[q];
-    s[t] = acc;
+  size_t P = 1;
+  while (P < g.nseg) P *= 2;
+  std::vector<T> seg(P, T(0)), slots(g.G);
+  for (size_t sg = 0; sg < g.nseg; ++sg) {
+    for (size_t i = 0; i < g.G; ++i) {
+      const size_t k = sg * g.G + i;
+      slots[i] = k < g.nchunks ? chunk[k] : T(0);
+    }
+    seg[sg] = pairwise(slots.data(), g.G);
   }
-  return tree256(s);
+  return pairwise(seg.data(), P);
 }
 
 float canon_dot(const float* x, const float* y, size_t ncells) {
-  const size_t nc = num_chunks(ncells);
-  std::vector<float> part(nc);
-#pragma omp parallel for schedule(static)
-  for (long k = 0; k < (long)nc; ++k)
-    part[k] = canon_partial(k, ncells, [&](size_t c, int s) { return x[3 * c + s] * y[3 * c + s]; });
-  return canon_final(part.data(), nc);
+  return canon_sum<float>(ncells, [&](size_t c) {
+    return (x[3 * c] * y[3 * c] + x[3 * c + 1] * y[3 * c + 1]) + x[3 * c + 2] * y[3 * c + 2];
+  });
 }
 
-// Distributed canonical order (R ranks, contiguous cell ranges starts[r]..):
-// each rank reduces its own cells in the order above (chunks restart at its
-// first cell), then the per-rank results are added in rank order from +0.
-// R = 1 is the plain canonical order.
+// The distributed solver's reductions give these same bits on any rank count
+// (ranks own whole segments, kernels.hpp), so there is no per-rank order.
 float dist_dot(const float* x, const float* y, const std::vector<uint64_t>& starts) {
-  const int R = (int)starts.size() - 1;
-  if (R == 1) return canon_dot(x, y, starts[1]);
-  float acc = 0.0f;
-  for (int r = 0; r < R; ++r) {
-    const size_t o = starts[r];
-    acc += canon_dot(x + 3 * o, y + 3 * o, starts[r + 1] - o);
-  }
-  return acc;
+  return canon_dot(x, y, starts.back());
 }
 
 // WGSL builtins (WGSL spec formulas).
@@ -138,29 +144,22 @@ struct AmgLevel {
   size_t n = 0;
 };
 
-// amg.rs:84-116.  Distributed: the greedy pass runs part by
-// part (the ranks' row ranges) and a neighbour joins only within its part;
-// `cpart` returns the coarse rows' partition.  One part = the reference.
-void aggregate(const Csr& m, const std::vector<uint64_t>& part, std::vector<size_t>& agg, size_t& nagg,
-               std::vector<uint64_t>& cpart) {
+// amg.rs:84-116: greedy, index order, no strength test.  The distributed
+// solver runs this same global pass (its hierarchy does not depend on the
+// rank count).
+void aggregate(const Csr& m, std::vector<size_t>& agg, size_t& nagg) {
   const size_t n = m.rows, NONE = std::numeric_limits<size_t>::max();
   agg.assign(n, NONE);
   nagg = 0;
-  cpart.assign(part.size(), 0);
-  for (size_t p = 0; p + 1 < part.size(); ++p) {
-    cpart[p] = nagg;
-    const size_t lo = part[p], hi = part[p + 1];
-    for (size_t i = lo; i < hi; ++i) {
-      if (agg[i] != NONE) continue;
-      agg[i] = nagg;
-      for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
-        const size_t j = m.col[k];
-        if (j != i && j >= lo && j < hi && agg[j] == NONE) agg[j] = nagg;
-      }
-      ++nagg;
+  for (size_t i = 0; i < n; ++i) {
+    if (agg[i] != NONE) continue;
+    agg[i] = nagg;
+    for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
+      const size_t j = m.col[k];
+      if (j != i && agg[j] == NONE) agg[j] = nagg;
     }
+    ++nagg;
   }
-  cpart.back() = nagg;
 }
 
 Csr build_prolongation(const std::vector<size_t>& agg, size_t nagg, size_t nf) {  // :118-139
@@ -242,7 +241,7 @@ Csr mat_mat_mult(const Csr& a, const Csr& b) {  // :187-229, f32 accumulation in
 struct Amg {
   std::vector<AmgLevel> levels;
 
-  void build(const Csr& fine, size_t max_levels, std::vector<uint64_t> part) {  // amg.rs:246-595
+  void build(const Csr& fine, size_t max_levels) {  // amg.rs:246-595
     Csr cur = fine;
     for (size_t li = 0; li < max_levels; ++li) {
       AmgLevel L;
@@ -255,10 +254,8 @@ struct Amg {
       if (li < max_levels - 1 && L.n > 100) {
         std::vector<size_t> agg;
         size_t nagg;
-        std::vector<uint64_t> cpart;
-        aggregate(cur, part, agg, nagg, cpart);
+        aggregate(cur, agg, nagg);
         if (nagg < L.n) {
-          part = cpart;
           L.P = build_prolongation(agg, nagg, L.n);
           L.R = transpose(L.P);
           cur = mat_mat_mult(mat_mat_mult(L.R, cur), L.P);
@@ -1095,7 +1092,7 @@ cfd_linear_stats solve(oracle_solver* s) {
   ensure_fgmres(s);
   if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
     s->amg.reset(new Amg);
-    s->amg->build(s->scalar, 20, s->starts);
+    s->amg->build(s->scalar, 20);
     s->amg_age = 0;
   }
   const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts));
@@ -1258,67 +1255,37 @@ void update_fields(oracle_solver* s, float* mdu, float* mdp) {
 }
 
 // coupled_solver.rs:501-580 (stride bug §0.1-12 reproduced: AoS view, floats 2i, 2i+1).
-// The f64 sums use the canonical chunk order (1024 records per chunk, 256
-// threads x 4, halving tree) instead of the reference's serial order: the two
-// differ only by f64 reassociation (~1e-16 relative).
-double tree256d(double* s) {
-  for (int h = kThreads / 2; h >= 1; h >>= 1)
-    for (int t = 0; t < h; ++t) s[t] = s[t] + s[t + h];
-  return s[0];
-}
-
+// The f64 sums use the canonical tree (leaves per cell: the 8 squared
+// differences added in field order; u, v, u^2, v^2 of the variance record)
+// instead of the reference's serial order: the two differ only by f64
+// reassociation (~1e-16 relative).
 void check_evolution(oracle_solver* s) {
   const uint32_t N = s->N;
   const float* u_data = reinterpret_cast<const float*>(s->S());
   const size_t len = 8 * (size_t)N;
   const bool have = s->have_prev && s->prev_u_cpu.size() == len;
-  // per rank segment (distributed order: chunks restart at the rank's first
-  // cell, rank results added in rank order from +0; one rank = plain order)
-  const int R = (int)s->starts.size() - 1;
-  double tot[5] = {0, 0, 0, 0, 0};
-  for (int r = 0; r < R; ++r) {
-    const size_t c0 = s->starts[r], nr = s->starts[r + 1] - c0;
-    const size_t nc = num_chunks(nr);
-    std::vector<double> part(5 * nc);
-#pragma omp parallel for schedule(static)
-    for (long k = 0; k < (long)nc; ++k) {
-      double acc[5][kThreads];
-      for (int t = 0; t < kThreads; ++t) {
-        double evo = 0, su = 0, sv = 0, squ = 0, sqv = 0;
-        for (int q = 0; q < kCellsPerThread; ++q) {
-          const size_t lc = (size_t)k * kChunkCells + t + (size_t)kThreads * q;
-          if (lc >= nr) continue;
-          const size_t c = c0 + lc;
-          if (have)
-            for (int f = 0; f < 8; ++f) {
-              const float d = u_data[8 * c + f] - s->prev_u_cpu[8 * c + f];
-              evo += (double)(d * d);
-            }
-          const double u = (double)u_data[2 * c], v = (double)u_data[2 * c + 1];
-          su += u;
-          sv += v;
-          squ += u * u;
-          sqv += v * v;
-        }
-        acc[0][t] = evo;
-        acc[1][t] = su;
-        acc[2][t] = sv;
-        acc[3][t] = squ;
-        acc[4][t] = sqv;
-      }
-      for (int f = 0; f < 5; ++f) part[5 * k + f] = tree256d(acc[f]);
+  const float* prev = have ? s->prev_u_cpu.data() : nullptr;
+  double tot[5];
+  tot[0] = canon_sum<double>(N, [&](size_t c) {
+    if (!have) return 0.0;
+    double e = 0.0;
+    for (int f = 0; f < 8; ++f) {
+      const float d = u_data[8 * c + f] - prev[8 * c + f];
+      const double t = (double)(d * d);
+      e = f == 0 ? t : e + t;
     }
-    for (int f = 0; f < 5; ++f) {
-      double acc[kThreads];
-      for (int t = 0; t < kThreads; ++t) {
-        double a = 0.0;
-        for (size_t q = t; q < nc; q += kThreads) a += part[5 * q + f];
-        acc[t] = a;
-      }
-      const double seg = tree256d(acc);
-      tot[f] = (R == 1) ? seg : tot[f] + seg;
-    }
-  }
+    return e;
+  });
+  tot[1] = canon_sum<double>(N, [&](size_t c) { return (double)u_data[2 * c]; });
+  tot[2] = canon_sum<double>(N, [&](size_t c) { return (double)u_data[2 * c + 1]; });
+  tot[3] = canon_sum<double>(N, [&](size_t c) {
+    const double u = (double)u_data[2 * c];
+    return u * u;
+  });
+  tot[4] = canon_sum<double>(N, [&](size_t c) {
+    const double v = (double)u_data[2 * c + 1];
+    return v * v;
+  });
   const double n = (double)N;
   const double mean_u = tot[1] / n, mean_v = tot[2] / n;
   const double var_u = std::fmax(tot[3] / n - mean_u * mean_u, 0.0);

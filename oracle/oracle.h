@@ -22,9 +22,9 @@ extern "C" {
 typedef struct oracle_solver oracle_solver;
 
 oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg);
-/* The distributed solver's semantics on `nranks` contiguous cell ranges
- * (partition-aware AMG aggregation, rank-segmented reductions summed in rank
- * order); nranks = 1 is oracle_create.                                      */
+/* Kept for the distributed tests: the distributed solver is rank-count
+ * invariant (global AMG hierarchy, canonical reduction tree whose segments
+ * ranks own whole), so `nranks` changes no result; = oracle_create.       */
 oracle_solver* oracle_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg, int nranks);
 void oracle_destroy(oracle_solver* s);
 void oracle_set_threads(int n);

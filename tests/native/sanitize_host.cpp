@@ -39,7 +39,7 @@ void check(bool ok, const char* what) {
 void run(const char* name, const cfd2::Mesh& m) {
   const cfd_mesh_view v = view_of(m);
   const uint32_t n = m.num_cells();
-  for (int R = 1; R <= 4; ++R) {
+  for (int R = 1; R <= 4 && (uint32_t)R <= cfd2::red_geom(n).nseg; ++R) {
     const auto starts = cfd2::partition_starts(n, R);
     uint64_t rows = 0, nnz = 0, sends = 0, recvs = 0;
     for (int r = 0; r < R; ++r) {
@@ -71,6 +71,10 @@ void run(const char* name, const cfd2::Mesh& m) {
     check(!H.empty() && H[0].A.rows == n, "empty hierarchy");
     for (size_t l = 0; l + 1 < H.size(); ++l)
       check(H[l].has_op && H[l + 1].A.rows == H[l].nc, "level sizes");
+    for (size_t l = 0; l < H.size(); ++l) {  // coarse rows follow their seeds: a partition in rank order
+      check(H[l].part.size() == (size_t)R + 1 && H[l].part[0] == 0 && H[l].part[R] == H[l].A.rows, "level partition");
+      for (int q = 0; q < R; ++q) check(H[l].part[q] <= H[l].part[q + 1], "level partition order");
+    }
     std::printf("%s: %u cells, %d rank(s): nnz %llu, halo %llu, %zu AMG levels: ok\n", name, n, R,
                 (unsigned long long)nnz, (unsigned long long)sends, H.size());
   }

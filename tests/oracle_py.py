@@ -67,7 +67,8 @@ class OracleSolver:
     """Same surface as cfd2_amd.GpuSolver, backed by the CPU oracle."""
 
     def __init__(self, mesh, config=None, nranks=1, **cfg_overrides):
-        """nranks > 1: the distributed solver's semantics on nranks cell ranges."""
+        """nranks: accepted for the distributed tests; results do not depend on it
+        (the distributed solver reproduces the single-GPU bits)."""
         self._mesh = mesh  # keep the mesh alive (view borrows its arrays)
         cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
         self._cfg = cfg

@@ -84,3 +84,13 @@ def broken(kind):
         for k in a:
             a[k] = a[k][:0] if k != "cell_face_offsets" else np.zeros(1, np.uint32)
     return ArrayMesh(**a)
+
+
+def max_ranks(n):
+    """Most ranks a mesh of n cells can take: one segment of the canonical
+    reduction tree each (kernels.hpp red_geom)."""
+    g = 0
+    while g < 8 and (n >> (g + 1)) >= 16384:
+        g += 1
+    nch = -(-n // 256)
+    return -(-nch // (1 << g))

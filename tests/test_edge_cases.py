@@ -1,6 +1,6 @@
 """Edge cases the reference's solver tests do not reach but a drop-in must
 survive: degenerate sizes (1 cell, 1-D strips), broken meshes rejected with a
-status instead of a crash, partition extremes (as many ranks as cells)."""
+status instead of a crash, partition extremes (as many ranks as reduction segments)."""
 import ctypes as C
 
 import numpy as np
@@ -42,13 +42,26 @@ def test_more_ranks_than_cells_rejected():
     assert st == 1
 
 
-def test_one_cell_per_rank_plans():
-    m = strip(6)
+def test_more_ranks_than_segments_rejected():
+    """Ranks own whole segments of the reduction tree (256 cells at this size):
+    300 cells are 2 segments, so 3 ranks are refused with a status."""
+    L = _bind()
+    z = C.c_uint32()
+    st = L.cfd_dist_plan(C.byref(strip(300).view()), 3, 0, C.byref(z), C.byref(z), C.byref(z), C.byref(z),
+                         C.byref(z), None, None, None, None, None)
+    assert st == 1 and "segments" in L.cfd_last_error().decode()
+
+
+def test_one_segment_per_rank_plans():
+    """As many ranks as reduction segments: each rank owns exactly one 256-cell
+    segment of the strip and exchanges one ghost with each slab neighbour."""
+    m = strip(6 * 256)
     plans = [dist_plan(m, 6, r) for r in range(6)]
     for r, P in enumerate(plans):
-        assert P["c1"] - P["c0"] == 1
+        assert (P["c0"], P["c1"]) == (256 * r, 256 * (r + 1))
         want = [q for q in (r - 1, r + 1) if 0 <= q < 6]
-        assert P["peers"] == want and list(P["ghost"]) == want
+        assert P["peers"] == want
+        assert list(P["ghost"]) == [g for g in (256 * r - 1, 256 * (r + 1)) if 0 <= g < 6 * 256]
         assert P["recv"] == [1] * len(want) and P["send"] == [1] * len(want)
 
 

@@ -13,6 +13,7 @@ from cfd2_amd import GpuGroup, GpuSolver, default_config
 from cfd2_amd.mesh import (BackwardsStep, ChannelWithObstacle, RectangularChannel, generate_cut_cell_mesh,
                            generate_delaunay_mesh, generate_voronoi_mesh)
 from tests.oracle_py import OracleSolver
+from tests.synthetic import max_ranks
 from tests.test_gpu_parity import _assert_same_fields, _assert_same_info
 
 pytestmark = pytest.mark.gpu
@@ -84,6 +85,8 @@ def _setup(s, mesh, phys, useed):
 @pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
     kind, mesh, cfg, phys, nranks, useed = _case(seed)
+    # ranks own whole reduction segments (>= 256 cells): small meshes take fewer ranks
+    nranks = min(nranks, max_ranks(mesh.num_cells()))
     monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "200")  # distributed coarse levels on these small meshes
     c = default_config(**cfg)
     g = GpuSolver(mesh, config=c) if nranks == 1 else GpuGroup(mesh, nranks, config=c)

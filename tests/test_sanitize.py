@@ -45,4 +45,7 @@ def test_host_setup_code_under_asan_ubsan(tmp_path):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    assert r.stdout.count(": ok") == 12, r.stdout
+    # every mesh: 1 rank up to min(4, its reduction segments of 256 cells) ranks
+    for mesh in ("cut-cell step", "voronoi channel", "delaunay channel"):
+        assert all(f"{mesh}: " in r.stdout and f", {R} rank(s):" in r.stdout for R in (1, 2, 3)), r.stdout
+    assert r.stdout.count(": ok") >= 9, r.stdout
