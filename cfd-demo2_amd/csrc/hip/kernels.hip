@@ -121,6 +121,17 @@ __device__ __forceinline__ void seg_trees(const T* __restrict__ pv, uint32_t nch
   for (int u = 0; u < U; ++u) {
     const uint32_t sg = s0 + u * sstep;
     const uint64_t k0 = (uint64_t)sg * G + (uint64_t)lane * K;
+    if constexpr (sizeof(T) == 4) {
+      // 4 chunk slots in one 16-byte load (per-vector strides are multiples of 4)
+      if (K == 4 && sg < nseg && k0 + 3 < nchunks) {
+        const float4 q = *reinterpret_cast<const float4*>(pv + k0);
+        e[u][0] = q.x;
+        e[u][1] = q.y;
+        e[u][2] = q.z;
+        e[u][3] = q.w;
+        continue;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint64_t k = k0 + q;
@@ -535,24 +546,37 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
   *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-// Four consecutive cells (12 floats) of a 3-component vector, zero past n
-// cells: one 48-byte run per lane (3 x dwordx4) when the whole group is inside.
-__device__ __forceinline__ void load12_upto(const float* p, uint32_t c0, uint32_t n, float v[12]) {
-  if (c0 + 3 < n) {
-    load12(p + 3 * (size_t)c0, v);
-  } else {
+// A 256-cell chunk of a 3-component vector is 768 consecutive floats: three
+// 256-float parts, each read by the wavefront as one coalesced dwordx4 per
+// lane (lane l: floats 256 i + 4 l .. + 3 of the chunk).  v[4 i + e] = part i,
+// element e of this lane; floats past n3 (= 3 N) read as 0.
+__device__ __forceinline__ void load_chunk3(const float* p, uint32_t k, uint32_t n3, float v[12]) {
+  const size_t base = (size_t)k * 768u + 4u * red_lane();
 #pragma unroll
-    for (int e = 0; e < 12; ++e) v[e] = (c0 + (uint32_t)e / 3 < n) ? p[3 * (size_t)c0 + e] : 0.0f;
+  for (int i = 0; i < 3; ++i) {
+    const size_t e0 = base + 256u * i;
+    if (e0 + 3 < n3) {
+      const float4 q = *reinterpret_cast<const float4*>(p + e0);
+      v[4 * i] = q.x;
+      v[4 * i + 1] = q.y;
+      v[4 * i + 2] = q.z;
+      v[4 * i + 3] = q.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * i + e] = (e0 + e < n3) ? p[e0 + e] : 0.0f;
+    }
   }
 }
-// lane value of a 3-component dot: leaf ((a0 b0 + a1 b1) + a2 b2) per cell,
-// ((c0 + c1) + (c2 + c3)) over the lane's cells (cells past n contribute +0
-// leaves: their zeros multiply to +0)
-__device__ __forceinline__ float lane_dot12(const float a[12], const float b[12]) {
-  float t[4];
+// chunk value of a dot over 3-component cells (kernels.hpp, 3-component
+// leaves): part i = pairwise tree over its 256 products (lane: (p0 + p1) +
+// (p2 + p3), then the wavefront tree), chunk = (part0 + part1) + part2; valid in lane 0
+__device__ __forceinline__ float chunk_dot3(const float a[12], const float b[12]) {
+  float t[3];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) t[q] = (a[3 * q] * b[3 * q] + a[3 * q + 1] * b[3 * q + 1]) + a[3 * q + 2] * b[3 * q + 2];
-  return (t[0] + t[1]) + (t[2] + t[3]);
+  for (int i = 0; i < 3; ++i)
+    t[i] = wave_tree((a[4 * i] * b[4 * i] + a[4 * i + 1] * b[4 * i + 1]) +
+                     (a[4 * i + 2] * b[4 * i + 2] + a[4 * i + 3] * b[4 * i + 3]));
+  return (t[0] + t[1]) + t[2];
 }
 
 // chunk partials of dot(x, y) over 3-component cells
@@ -560,11 +584,10 @@ __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict_
                                                         const float* __restrict__ y, uint32_t N,
                                                         float* partial) {
   const uint32_t k = red_chunk();
-  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
   float a[12], b[12];
-  load12_upto(x, c0, N, a);
-  load12_upto(y, c0, N, b);
-  const float r = wave_tree(lane_dot12(a, b));
+  load_chunk3(x, k, 3 * N, a);
+  load_chunk3(y, k, 3 * N, b);
+  const float r = chunk_dot3(a, b);
   if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
 }
 
@@ -769,42 +792,46 @@ __device__ __forceinline__ void st_stream(float* p, float v) {
 }
 
 typedef float f4a __attribute__((ext_vector_type(4)));
-// 12 floats (4 cells x 3) of a streamed-once basis vector (nontemporal when
-// CFD_CGS_NT), zero past n cells
-__device__ __forceinline__ void ld12_stream(const float* p, uint32_t c0, uint32_t n, float v[12]) {
-  if (c0 + 3 < n) {
-    const f4a* q = reinterpret_cast<const f4a*>(p + 3 * (size_t)c0);
-#if CFD_CGS_NT
-    const f4a a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1),
-              c = __builtin_nontemporal_load(q + 2);
-#else
-    const f4a a = q[0], b = q[1], c = q[2];
-#endif
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
-  } else {
+// load_chunk3 / its store for a streamed-once basis vector (nontemporal when CFD_CGS_NT)
+__device__ __forceinline__ void ld_chunk3_stream(const float* p, uint32_t k, uint32_t n3, float v[12]) {
+  const size_t base = (size_t)k * 768u + 4u * red_lane();
 #pragma unroll
-    for (int e = 0; e < 12; ++e) v[e] = (c0 + (uint32_t)e / 3 < n) ? ld_stream(p + 3 * (size_t)c0 + e) : 0.0f;
+  for (int i = 0; i < 3; ++i) {
+    const size_t e0 = base + 256u * i;
+    if (e0 + 3 < n3) {
+      const f4a* q = reinterpret_cast<const f4a*>(p + e0);
+#if CFD_CGS_NT
+      const f4a a = __builtin_nontemporal_load(q);
+#else
+      const f4a a = *q;
+#endif
+      v[4 * i] = a.x;
+      v[4 * i + 1] = a.y;
+      v[4 * i + 2] = a.z;
+      v[4 * i + 3] = a.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * i + e] = (e0 + e < n3) ? ld_stream(p + e0 + e) : 0.0f;
+    }
   }
 }
-__device__ __forceinline__ void st12_stream(float* p, uint32_t c0, uint32_t n, const float v[12]) {
-  if (c0 + 3 < n) {
-    f4a* q = reinterpret_cast<f4a*>(p + 3 * (size_t)c0);
-    const f4a a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]}, c = {v[8], v[9], v[10], v[11]};
-#if CFD_CGS_NT
-    __builtin_nontemporal_store(a, q);
-    __builtin_nontemporal_store(b, q + 1);
-    __builtin_nontemporal_store(c, q + 2);
-#else
-    q[0] = a;
-    q[1] = b;
-    q[2] = c;
-#endif
-  } else {
+__device__ __forceinline__ void st_chunk3_stream(float* p, uint32_t k, uint32_t n3, const float v[12]) {
+  const size_t base = (size_t)k * 768u + 4u * red_lane();
 #pragma unroll
-    for (int e = 0; e < 12; ++e)
-      if (c0 + (uint32_t)e / 3 < n) st_stream(p + 3 * (size_t)c0 + e, v[e]);
+  for (int i = 0; i < 3; ++i) {
+    const size_t e0 = base + 256u * i;
+    if (e0 + 3 < n3) {
+      const f4a a = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+#if CFD_CGS_NT
+      __builtin_nontemporal_store(a, reinterpret_cast<f4a*>(p + e0));
+#else
+      *reinterpret_cast<f4a*>(p + e0) = a;
+#endif
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e0 + e < n3) st_stream(p + e0 + e, v[4 * i + e]);
+    }
   }
 }
 
@@ -815,17 +842,16 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, float* partial, uint32_t np) {
   const uint32_t k = red_chunk();
-  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
   const bool writer = red_lane() == 0 && k < np;
   float wv[12];
-  load12_upto(w, c0, N, wv);
+  load_chunk3(w, k, 3 * N, wv);
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[12];
-    ld12_stream(basis + (size_t)ii * stride, c0, N, v);
+    ld_chunk3_stream(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
-    const float r = wave_tree(lane_dot12(wv, v));
+    const float r = chunk_dot3(wv, v);
     if (writer) partial[(size_t)ii * np + k] = r;
   }
 }
@@ -853,23 +879,22 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   }
   __syncthreads();
   const uint32_t k = red_chunk();
-  const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
   float corr[12];
 #pragma unroll
   for (int e = 0; e < 12; ++e) corr[e] = 0.0f;
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[12];
-    ld12_stream(basis + (size_t)ii * stride, c0, N, v);
+    ld_chunk3_stream(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
   }
   float wn[12];
-  load12_upto(w, c0, N, wn);
+  load_chunk3(w, k, 3 * N, wn);
 #pragma unroll
   for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
-  st12_stream(basis + (size_t)(j + 1) * stride, c0, N, wn);
-  const float r = wave_tree(lane_dot12(wn, wn));
+  st_chunk3_stream(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
+  const float r = chunk_dot3(wn, wn);
   if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
 }
 

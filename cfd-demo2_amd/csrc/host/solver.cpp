@@ -72,6 +72,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (red.nseg > kRedMaxSegments)
     throw std::invalid_argument("mesh too large for the reduction tree (at most 268 M cells)");
   nchunks = (N + kRedChunkCells - 1) / kRedChunkCells;
+  pstride = (nchunks + 3) & ~3u;
   shift = (topo.glo + 63) & ~63u;
   vlen = (size_t)shift + topo.npad + topo.ghi;
   CFD_HIP(hipSetDevice(device));
@@ -170,7 +171,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   x = valloc<float>(3);
   dinv_uv = valloc<float>(1);
   dinv_p = valloc<float>(1);
-  partial_d = arena.alloc<double>(5 * (size_t)nchunks + 5);
+  partial_d = arena.alloc<double>(5 * (size_t)pstride + 5);
   maxbits = arena.alloc<uint32_t>(4);
   blockmax = arena.alloc<uint32_t>(2 * (((size_t)N + 255) / 256) + 2);
   CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float), hipHostMallocDefault));
@@ -372,11 +373,11 @@ RedSrc Solver::combine(const float* part, int nvec) {
   r.nvec = (uint32_t)nvec;
   if (!dist()) {
     r.p = part;
-    r.stride = nchunks;
+    r.stride = pstride;
     r.nchunks = nchunks;
     return r;
   }
-  launch_seg_reduce(part, nchunks, nchunks, red.G, nvec, red_local, maxseg, stream);
+  launch_seg_reduce(part, pstride, nchunks, red.G, nvec, red_local, maxseg, stream);
   comm->allgather(red_local, red_gather, (size_t)nvec * maxseg * sizeof(float), stream);
   r.p = red_gather;
   r.stride = maxseg;
@@ -391,11 +392,11 @@ RedSrcD Solver::combine_d(const double* part, int nvec) {
   r.nvec = (uint32_t)nvec;
   if (!dist()) {
     r.p = part;
-    r.stride = nchunks;
+    r.stride = pstride;
     r.nchunks = nchunks;
     return r;
   }
-  launch_seg_reduce_d(part, nchunks, nchunks, red.G, nvec, red_local_d, maxseg, stream);
+  launch_seg_reduce_d(part, pstride, nchunks, red.G, nvec, red_local_d, maxseg, stream);
   comm->allgather(red_local_d, red_gather_d, (size_t)nvec * maxseg * sizeof(double), stream);
   r.p = red_gather_d;
   r.stride = maxseg;
@@ -476,8 +477,8 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   temp = valloc<float>(1);
   temp_p = valloc<float>(1);
   p_sol = valloc<float>(1);
-  partial = arena.alloc<float>((size_t)m1 * nchunks);
-  partial_n = arena.alloc<float>(nchunks);
+  partial = arena.alloc<float>((size_t)m1 * pstride);
+  partial_n = arena.alloc<float>(pstride);
   const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
   dsc = arena.alloc<float>(nsc);
   CFD_HIP(hipMemsetAsync(dsc, 0, nsc * sizeof(float), stream));
@@ -1303,7 +1304,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         A.r3 = b2;
         launch_spmv(A, zj, w, stream);
       });
-      launch_cgs_dots(w, basis, binv, stride, j, N, partial, nchunks, stream);
+      launch_cgs_dots(w, basis, binv, stride, j, N, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
       launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, stream);
@@ -1441,8 +1442,8 @@ void Solver::check_evolution() {
     gbase = topo.c0;
     rec0 = ev_a;
   }
-  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, nchunks, stream);
-  double* out5 = partial_d + 5 * (size_t)nchunks;
+  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, pstride, stream);
+  double* out5 = partial_d + 5 * (size_t)pstride;
   launch_evolution_final(combine_d(partial_d, 5), out5, stream);
   check_launch("check_evolution");
   double tot[5];

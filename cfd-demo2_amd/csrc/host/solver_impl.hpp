@@ -240,9 +240,10 @@ struct Solver {
   float* temp = nullptr;
   float* temp_p = nullptr;
   float* p_sol = nullptr;
-  float* partial = nullptr;      // [(m+1) * nchunks] chunk partials (256 cells each)
+  uint32_t pstride = 0;          // chunk partials per vector (nchunks rounded up to 4: 16-byte loads)
+  float* partial = nullptr;      // [(m+1) * pstride] chunk partials (256 cells each)
   float* partial_n = nullptr;    // [nchunks]
-  double* partial_d = nullptr;   // [5 * nchunks] check_evolution
+  double* partial_d = nullptr;   // [5 * pstride] check_evolution
   float* dsc = nullptr;          // device scalars
   float* H = nullptr;
   float* givens = nullptr;

@@ -45,8 +45,10 @@ int fail(const std::string& m) {
 // any fixed order is a valid restatement, and this one is a single binary
 // tree over GLOBAL cell indices, so a distributed solver reproduces it
 // exactly on any rank count:
-//   leaf     cell c: its terms added left to right ((t0 + t1) + t2)
-//   chunk    256 cells: pairwise tree over the 256 leaves (missing: +0)
+//   chunk    256 cells: 1-value cells: pairwise tree over the 256 cell terms;
+//            3-component vectors: the chunk's 768 floats in three parts of 256,
+//            each a pairwise tree over its element terms, (part0 + part1) + part2
+//            (missing cells / elements: +0)
 //   segment  G = 2^g chunks: pairwise tree over G chunk slots (missing: +0),
 //            g = clamp(floor(log2(N / 16384)), 0, 8) for the global N
 //   total    pairwise tree over the segment values padded to a power of two
@@ -73,20 +75,9 @@ T pairwise(T* v, size_t n) {
   return v[0];
 }
 
-// canonical sum over `ncells` cells of the leaves leaf(c) (T = float / double)
-template <class T, class Leaf>
-T canon_sum(size_t ncells, Leaf leaf) {
-  const RedGeom g = red_geom(ncells);
-  std::vector<T> chunk(g.nchunks);
-#pragma omp parallel for schedule(static)
-  for (long k = 0; k < (long)g.nchunks; ++k) {
-    T lv[kChunkCells];
-    for (size_t i = 0; i < kChunkCells; ++i) {
-      const size_t c = (size_t)k * kChunkCells + i;
-      lv[i] = c < ncells ? leaf(c) : T(0);
-    }
-    chunk[k] = pairwise(lv, kChunkCells);
-  }
+// segment trees over the chunk values, then the total over the segments
+template <class T>
+T canon_total(const std::vector<T>& chunk, const RedGeom& g) {
   size_t P = 1;
   while (P < g.nseg) P *= 2;
   std::vector<T> seg(P, T(0)), slots(g.G);
@@ -100,10 +91,42 @@ T canon_sum(size_t ncells, Leaf leaf) {
   return pairwise(seg.data(), P);
 }
 
+// canonical sum over `ncells` cells of the cell terms leaf(c) (T = float / double)
+template <class T, class Leaf>
+T canon_sum(size_t ncells, Leaf leaf) {
+  const RedGeom g = red_geom(ncells);
+  std::vector<T> chunk(g.nchunks);
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < (long)g.nchunks; ++k) {
+    T lv[kChunkCells];
+    for (size_t i = 0; i < kChunkCells; ++i) {
+      const size_t c = (size_t)k * kChunkCells + i;
+      lv[i] = c < ncells ? leaf(c) : T(0);
+    }
+    chunk[k] = pairwise(lv, kChunkCells);
+  }
+  return canon_total(chunk, g);
+}
+
+// canonical dot over 3-component cells
 float canon_dot(const float* x, const float* y, size_t ncells) {
-  return canon_sum<float>(ncells, [&](size_t c) {
-    return (x[3 * c] * y[3 * c] + x[3 * c + 1] * y[3 * c + 1]) + x[3 * c + 2] * y[3 * c + 2];
-  });
+  const RedGeom g = red_geom(ncells);
+  const size_t n3 = 3 * ncells;
+  std::vector<float> chunk(g.nchunks);
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < (long)g.nchunks; ++k) {
+    float part[3];
+    for (int i = 0; i < 3; ++i) {
+      float lv[kChunkCells];
+      for (size_t e = 0; e < kChunkCells; ++e) {
+        const size_t d = (size_t)k * 3 * kChunkCells + (size_t)i * kChunkCells + e;
+        lv[e] = d < n3 ? x[d] * y[d] : 0.0f;
+      }
+      part[i] = pairwise(lv, kChunkCells);
+    }
+    chunk[k] = (part[0] + part[1]) + part[2];
+  }
+  return canon_total(chunk, g);
 }
 
 // The distributed solver's reductions give these same bits on any rank count
