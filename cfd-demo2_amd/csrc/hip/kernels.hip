@@ -21,6 +21,9 @@ namespace cfd2 {
 
 namespace {
 
+#ifndef CFD_CGS_NT
+#define CFD_CGS_NT 1
+#endif
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ float wsmoothstep(float lo, float hi, float x) {
@@ -549,21 +552,51 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
 // A 256-cell chunk of a 3-component vector is 768 consecutive floats: three
 // 256-float parts, each read by the wavefront as one coalesced dwordx4 per
 // lane (lane l: floats 256 i + 4 l .. + 3 of the chunk).  v[4 i + e] = part i,
-// element e of this lane; floats past n3 (= 3 N) read as 0.
+// element e of this lane; floats past n3 (= 3 N) read as 0.  FULL: the chunk
+// lies inside n3 (every chunk but the last): no range checks.  NT: nontemporal
+// (streamed-once basis vectors, CFD_CGS_NT).
+template <bool FULL, bool NT = false>
 __device__ __forceinline__ void load_chunk3(const float* p, uint32_t k, uint32_t n3, float v[12]) {
   const size_t base = (size_t)k * 768u + 4u * red_lane();
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const size_t e0 = base + 256u * i;
-    if (e0 + 3 < n3) {
-      const float4 q = *reinterpret_cast<const float4*>(p + e0);
-      v[4 * i] = q.x;
-      v[4 * i + 1] = q.y;
-      v[4 * i + 2] = q.z;
-      v[4 * i + 3] = q.w;
+    if (FULL || e0 + 3 < n3) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v* q = reinterpret_cast<const f4v*>(p + e0);
+      f4v a;
+      if constexpr (NT && CFD_CGS_NT)
+        a = __builtin_nontemporal_load(q);
+      else
+        a = *q;
+      v[4 * i] = a.x;
+      v[4 * i + 1] = a.y;
+      v[4 * i + 2] = a.z;
+      v[4 * i + 3] = a.w;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[4 * i + e] = (e0 + e < n3) ? p[e0 + e] : 0.0f;
+    }
+  }
+}
+template <bool FULL>
+__device__ __forceinline__ void store_chunk3_stream(float* p, uint32_t k, uint32_t n3, const float v[12]) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const size_t base = (size_t)k * 768u + 4u * red_lane();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const size_t e0 = base + 256u * i;
+    if (FULL || e0 + 3 < n3) {
+      const f4v a = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+#if CFD_CGS_NT
+      __builtin_nontemporal_store(a, reinterpret_cast<f4v*>(p + e0));
+#else
+      *reinterpret_cast<f4v*>(p + e0) = a;
+#endif
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e0 + e < n3) p[e0 + e] = v[4 * i + e];
     }
   }
 }
@@ -578,17 +611,33 @@ __device__ __forceinline__ float chunk_dot3(const float a[12], const float b[12]
                      (a[4 * i + 2] * b[4 * i + 2] + a[4 * i + 3] * b[4 * i + 3]));
   return (t[0] + t[1]) + t[2];
 }
+// Units of the block's 4 chunk values l[0..3] (kernels.hpp): unit u of U chunks
+// = the pairwise tree over them
+template <class T>
+__device__ __forceinline__ T unit_value(const T* l, uint32_t U, uint32_t u) {
+  if (U == 4) return (l[0] + l[1]) + (l[2] + l[3]);
+  if (U == 2) return l[2 * u] + l[2 * u + 1];
+  return l[u];
+}
+// the block's chunks are all inside the mesh
+__device__ __forceinline__ bool block_full(uint32_t N) {
+  return (size_t)(blockIdx.x + 1) * 4u * kRedChunkCells <= N;
+}
 
-// chunk partials of dot(x, y) over 3-component cells
+// unit partials of dot(x, y) over 3-component cells
 __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
-                                                        const float* __restrict__ y, uint32_t N,
+                                                        const float* __restrict__ y, uint32_t N, uint32_t U,
                                                         float* partial) {
+  __shared__ float lds[4];
   const uint32_t k = red_chunk();
   float a[12], b[12];
-  load_chunk3(x, k, 3 * N, a);
-  load_chunk3(y, k, 3 * N, b);
+  load_chunk3<false>(x, k, 3 * N, a);
+  load_chunk3<false>(y, k, 3 * N, b);
   const float r = chunk_dot3(a, b);
-  if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
+  if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
+  __syncthreads();
+  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
+  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value(lds, U, threadIdx.x);
 }
 
 __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int mode, float* out, float* inv,
@@ -772,87 +821,40 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   store12(y + 3 * (size_t)i0, o);
 }
 
-#ifndef CFD_CGS_NT
-#define CFD_CGS_NT 1
-#endif
-// streamed-once basis reads / new basis vector stores (nontemporal when CFD_CGS_NT)
-__device__ __forceinline__ float ld_stream(const float* p) {
-#if CFD_CGS_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
-__device__ __forceinline__ void st_stream(float* p, float v) {
-#if CFD_CGS_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-
-typedef float f4a __attribute__((ext_vector_type(4)));
-// load_chunk3 / its store for a streamed-once basis vector (nontemporal when CFD_CGS_NT)
-__device__ __forceinline__ void ld_chunk3_stream(const float* p, uint32_t k, uint32_t n3, float v[12]) {
-  const size_t base = (size_t)k * 768u + 4u * red_lane();
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const size_t e0 = base + 256u * i;
-    if (e0 + 3 < n3) {
-      const f4a* q = reinterpret_cast<const f4a*>(p + e0);
-#if CFD_CGS_NT
-      const f4a a = __builtin_nontemporal_load(q);
-#else
-      const f4a a = *q;
-#endif
-      v[4 * i] = a.x;
-      v[4 * i + 1] = a.y;
-      v[4 * i + 2] = a.z;
-      v[4 * i + 3] = a.w;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * i + e] = (e0 + e < n3) ? ld_stream(p + e0 + e) : 0.0f;
-    }
-  }
-}
-__device__ __forceinline__ void st_chunk3_stream(float* p, uint32_t k, uint32_t n3, const float v[12]) {
-  const size_t base = (size_t)k * 768u + 4u * red_lane();
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const size_t e0 = base + 256u * i;
-    if (e0 + 3 < n3) {
-      const f4a a = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
-#if CFD_CGS_NT
-      __builtin_nontemporal_store(a, reinterpret_cast<f4a*>(p + e0));
-#else
-      *reinterpret_cast<f4a*>(p + e0) = a;
-#endif
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e0 + e < n3) st_stream(p + e0 + e, v[4 * i + e]);
-    }
-  }
-}
-
-// calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + chunk] = <w, V_ii>, ii = 0..j,
-// V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees only.
-__global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
-                                                     const float* __restrict__ basis,
-                                                     const float* __restrict__ binv, size_t stride,
-                                                     int j, uint32_t N, float* partial, uint32_t np) {
+// calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + unit] = <w, V_ii>, ii = 0..j,
+// V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees;
+// the block's 4 chunk values per ii meet in LDS and become units at the end.
+template <bool FULL>
+__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ basis,
+                                               const float* __restrict__ binv, size_t stride, int j, uint32_t N,
+                                               float* lds) {
   const uint32_t k = red_chunk();
-  const bool writer = red_lane() == 0 && k < np;
   float wv[12];
-  load_chunk3(w, k, 3 * N, wv);
+  load_chunk3<FULL>(w, k, 3 * N, wv);
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[12];
-    ld_chunk3_stream(basis + (size_t)ii * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
     const float r = chunk_dot3(wv, v);
-    if (writer) partial[(size_t)ii * np + k] = r;
+    if (red_lane() == 0) lds[4 * ii + (threadIdx.x >> 6)] = r;
+  }
+}
+__global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
+                                                     const float* __restrict__ basis,
+                                                     const float* __restrict__ binv, size_t stride,
+                                                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
+  __shared__ float lds[4 * 64];
+  if (block_full(N))
+    cgs_dots_chunk<true>(w, basis, binv, stride, j, N, lds);
+  else
+    cgs_dots_chunk<false>(w, basis, binv, stride, j, N, lds);
+  __syncthreads();
+  const uint32_t UB = 4 / U;
+  for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
+    const uint32_t ii = idx / UB, u = idx % UB, unit = blockIdx.x * UB + u;
+    if ((size_t)unit * U * kRedChunkCells < N) partial[(size_t)ii * np + unit] = unit_value(lds + 4 * ii, U, u);
   }
 }
 
@@ -864,20 +866,11 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
 }
 
-// update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 chunk partial; the
+// update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
 // updated w is written straight into basis slot j+1 (unnormalised, see binv).
-__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
-                                                            float* basis,
-                                                            const float* __restrict__ binv,
-                                                            size_t stride, int j,
-                                                            const float* __restrict__ H, int m1,
-                                                            uint32_t N, float* partial) {
-  __shared__ float hcol[64], scol[64];
-  if (threadIdx.x <= (unsigned)j) {
-    hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
-    scol[threadIdx.x] = binv[threadIdx.x];
-  }
-  __syncthreads();
+template <bool FULL>
+__device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, float* basis, size_t stride, int j,
+                                                  const float* hcol, const float* scol, uint32_t N) {
   const uint32_t k = red_chunk();
   float corr[12];
 #pragma unroll
@@ -885,17 +878,35 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[12];
-    ld_chunk3_stream(basis + (size_t)ii * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
   }
   float wn[12];
-  load_chunk3(w, k, 3 * N, wn);
+  load_chunk3<FULL>(w, k, 3 * N, wn);
 #pragma unroll
   for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
-  st_chunk3_stream(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
-  const float r = chunk_dot3(wn, wn);
-  if (red_lane() == 0 && (size_t)k * kRedChunkCells < N) partial[k] = r;
+  store_chunk3_stream<FULL>(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
+  return chunk_dot3(wn, wn);
+}
+__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
+                                                            float* basis,
+                                                            const float* __restrict__ binv,
+                                                            size_t stride, int j,
+                                                            const float* __restrict__ H, int m1,
+                                                            uint32_t N, uint32_t U, float* partial) {
+  __shared__ float hcol[64], scol[64], lds[4];
+  if (threadIdx.x <= (unsigned)j) {
+    hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
+    scol[threadIdx.x] = binv[threadIdx.x];
+  }
+  __syncthreads();
+  const float r = block_full(N) ? cgs_update_chunk<true>(w, basis, stride, j, hcol, scol, N)
+                                : cgs_update_chunk<false>(w, basis, stride, j, hcol, scol, N);
+  if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
+  __syncthreads();
+  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
+  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value(lds, U, threadIdx.x);
 }
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
@@ -1783,7 +1794,9 @@ __device__ __forceinline__ void view_pair(const StateView& v, uint32_t rec, int 
 __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, StateView prev,
                                                               int have_prev, uint32_t N,
                                                               StateView var, uint64_t gbase,
-                                                              uint64_t rec0, double* partial, uint32_t np) {
+                                                              uint64_t rec0, uint32_t U, double* partial,
+                                                              uint32_t np) {
+  __shared__ double lds[5 * 4];
   const uint32_t k = red_chunk();
   const uint32_t c0 = k * kRedChunkCells + 4 * red_lane();
   double lf[5][4];
@@ -1820,7 +1833,13 @@ __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, Sta
 #pragma unroll
   for (int f = 0; f < 5; ++f) {
     const double r = wave_tree((lf[f][0] + lf[f][1]) + (lf[f][2] + lf[f][3]));
-    if (red_lane() == 0 && k < np) partial[(size_t)f * np + k] = r;
+    if (red_lane() == 0) lds[4 * f + (threadIdx.x >> 6)] = r;
+  }
+  __syncthreads();
+  const uint32_t UB = 4 / U;
+  if (threadIdx.x < 5 * UB) {
+    const uint32_t f = threadIdx.x / UB, u = threadIdx.x % UB, unit = blockIdx.x * UB + u;
+    if ((size_t)unit * U * kRedChunkCells < N && unit < np) partial[(size_t)f * np + unit] = unit_value(lds + 4 * f, U, u);
   }
 }
 
@@ -1891,8 +1910,8 @@ inline unsigned red_blocks(uint32_t N) {  // 4 chunks of 256 cells per 256-threa
   const unsigned nch = (N + kRedChunkCells - 1) / kRedChunkCells;
   return (nch + 3) / 4;
 }
-void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s) {
-  if (N) hipLaunchKernelGGL(k_dot_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, x, y, N, partial);
+void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
+  if (N) hipLaunchKernelGGL(k_dot_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, x, y, N, U, partial);
 }
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0);
@@ -1909,17 +1928,19 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
     hipLaunchKernelGGL(k_spmv<false>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
-                     float* partial, uint32_t np, hipStream_t s) {
-  if (N) hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, partial, np);
+                     uint32_t U, float* partial, uint32_t np, hipStream_t s) {
+  if (N)
+    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U, partial,
+                       np);
 }
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, float* partial, hipStream_t s) {
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
   if (N)
     hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1,
-                       N, partial);
+                       N, U, partial);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, hipStream_t s) {
@@ -2039,10 +2060,11 @@ size_t init_kernel_attributes(int device) {
   return budget[device];
 }
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N, StateView var,
-                              uint64_t gbase, uint64_t rec0, double* partial, uint32_t np, hipStream_t s) {
+                              uint64_t gbase, uint64_t rec0, uint32_t U, double* partial, uint32_t np,
+                              hipStream_t s) {
   if (N)
     hipLaunchKernelGGL(k_evolution_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, cur, prev, have_prev, N, var,
-                       gbase, rec0, partial, np);
+                       gbase, rec0, U, partial, np);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n) hipLaunchKernelGGL(k_pack, dim3(grid_for(a.n)), dim3(kBlock), 0, s, a);

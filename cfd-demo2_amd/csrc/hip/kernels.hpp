@@ -47,7 +47,10 @@ constexpr uint32_t kMetaRankShift = 8;         // scalar-row rank of the neighbo
 //            of two.
 // A rank owns whole segments (partition_starts), so each segment value is
 // computed by one rank and the total from the all-gathered segment values: R
-// ranks produce exactly the bits of one GPU.
+// ranks produce exactly the bits of one GPU.  The chunk kernels combine the
+// 4 chunks of their block as far as a segment allows: they write "units" of
+// U = min(G, 4) chunks (the first log2(U) levels of the segment tree), so a
+// segment is G / U units.
 constexpr uint32_t kRedChunkCells = 256;
 constexpr uint32_t kRedCellsPerLane = 4;
 constexpr uint32_t kRedMaxSegLog2 = 8;
@@ -56,6 +59,7 @@ constexpr uint32_t kRedMaxSegments = 4096;  // the total's tree runs in LDS (N <
 struct RedGeom {
   uint32_t g = 0;          // log2 chunks per segment
   uint32_t G = 1;          // chunks per segment
+  uint32_t U = 1;          // chunks per unit written by the chunk kernels: min(G, 4)
   uint64_t seg_cells = 256;
   uint32_t nchunks = 0;    // global chunks
   uint32_t nseg = 0;       // global segments
@@ -66,6 +70,7 @@ inline RedGeom red_geom(uint64_t nglob) {
   while (g < kRedMaxSegLog2 && (nglob >> (g + 1)) >= 16384u) ++g;
   r.g = g;
   r.G = 1u << g;
+  r.U = r.G < 4 ? r.G : 4;
   r.seg_cells = (uint64_t)kRedChunkCells << g;
   r.nchunks = (uint32_t)((nglob + kRedChunkCells - 1) / kRedChunkCells);
   r.nseg = (uint32_t)((r.nchunks + r.G - 1) / r.G);
@@ -73,8 +78,8 @@ inline RedGeom red_geom(uint64_t nglob) {
 }
 
 // Source of a reduction's segment values for the kernels that finish it
-// (the total's tree).  One GPU: chunk partials p[v * stride + k], k < nchunks,
-// the segment trees are built from them.  Distributed: the all-gathered
+// (the total's tree).  One GPU: unit partials p[v * stride + k], k < nchunks
+// (here: units), G units per segment; the segment trees are built from them.  Distributed: the all-gathered
 // segment values, rank q's block [q][v][local segment] of nvec x stride
 // values; seg_src[s] = (q << 20) | local segment of global segment s.
 template <class T>
@@ -258,22 +263,22 @@ void launch_assemble(const AssembleArgs& a, hipStream_t s);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
                           float* p, uint32_t* blockmax, uint32_t* maxbits, hipStream_t s);
-// chunk partials of dot(x, y) over 3-component cells: partial[k], k < ceil(N / 256)
-void launch_dot_partial(const float* x, const float* y, uint32_t N, float* partial, hipStream_t s);
+// unit partials (U chunks of 256 cells each) of dot(x, y) over 3-component cells
+void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s);
 // total of the reduction r (one vector): mode 1: out[0] = sqrt(total); mode 2:
 // also *inv = 1.0f / sqrt (host-style) and g0 (if non-null) = sqrt
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s);
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
-// basis: unnormalised W_i at basis + i*stride, scales binv[i]; chunk partials
+// basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
-                     uint32_t N, float* partial, uint32_t np, hipStream_t s);
+                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
-// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 chunk partials
+// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, float* partial, hipStream_t s);
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s);
 // ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, hipStream_t s);
@@ -324,12 +329,12 @@ size_t init_kernel_attributes(int device);
 // chunk partials partial[f * np + k], f = {evolution, sum_u, sum_v, sumsq_u, sumsq_v}
 // The variance part reads record ((gbase + c) >> 2) - rec0 of `var` (stride bug, §0.1-12).
 void launch_evolution_partial(StateView cur, StateView prev, int have_prev, uint32_t N,
-                              StateView var, uint64_t gbase, uint64_t rec0, double* partial, uint32_t np,
+                              StateView var, uint64_t gbase, uint64_t rec0, uint32_t U, double* partial, uint32_t np,
                               hipStream_t s);
 // ---- distributed helpers ----
 void launch_pack(const PackArgs& a, hipStream_t s);
 // distributed: this rank's segment values out[v * maxseg + s] of nvec reductions
-// from their chunk partials part[v * np + k] (k < nchunks local, G chunks per segment)
+// from their unit partials part[v * np + k] (k < nunits local, G units per segment)
 void launch_seg_reduce(const float* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, float* out,
                        uint32_t maxseg, hipStream_t s);
 void launch_seg_reduce_d(const double* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, double* out,

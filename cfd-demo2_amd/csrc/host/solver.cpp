@@ -72,7 +72,8 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (red.nseg > kRedMaxSegments)
     throw std::invalid_argument("mesh too large for the reduction tree (at most 268 M cells)");
   nchunks = (N + kRedChunkCells - 1) / kRedChunkCells;
-  pstride = (nchunks + 3) & ~3u;
+  nunits = (nchunks + red.U - 1) / red.U;
+  pstride = (nunits + 3) & ~3u;
   shift = (topo.glo + 63) & ~63u;
   vlen = (size_t)shift + topo.npad + topo.ghi;
   CFD_HIP(hipSetDevice(device));
@@ -368,16 +369,16 @@ void Solver::halo_state(bool all) {
 // the segment values, and every rank finishes the same global tree.
 RedSrc Solver::combine(const float* part, int nvec) {
   RedSrc r;
-  r.G = red.G;
+  r.G = red.G / red.U;  // units per segment
   r.nseg = red.nseg;
   r.nvec = (uint32_t)nvec;
   if (!dist()) {
     r.p = part;
     r.stride = pstride;
-    r.nchunks = nchunks;
+    r.nchunks = nunits;
     return r;
   }
-  launch_seg_reduce(part, pstride, nchunks, red.G, nvec, red_local, maxseg, stream);
+  launch_seg_reduce(part, pstride, nunits, r.G, nvec, red_local, maxseg, stream);
   comm->allgather(red_local, red_gather, (size_t)nvec * maxseg * sizeof(float), stream);
   r.p = red_gather;
   r.stride = maxseg;
@@ -387,16 +388,16 @@ RedSrc Solver::combine(const float* part, int nvec) {
 
 RedSrcD Solver::combine_d(const double* part, int nvec) {
   RedSrcD r;
-  r.G = red.G;
+  r.G = red.G / red.U;  // units per segment
   r.nseg = red.nseg;
   r.nvec = (uint32_t)nvec;
   if (!dist()) {
     r.p = part;
     r.stride = pstride;
-    r.nchunks = nchunks;
+    r.nchunks = nunits;
     return r;
   }
-  launch_seg_reduce_d(part, pstride, nchunks, red.G, nvec, red_local_d, maxseg, stream);
+  launch_seg_reduce_d(part, pstride, nunits, r.G, nvec, red_local_d, maxseg, stream);
   comm->allgather(red_local_d, red_gather_d, (size_t)nvec * maxseg * sizeof(double), stream);
   r.p = red_gather_d;
   r.stride = maxseg;
@@ -1232,7 +1233,7 @@ void Solver::precondition(int j, float* z) {
 }
 
 float Solver::norm_blocking(const float* v, int mode, int slot) {
-  launch_dot_partial(v, v, N, partial_n, stream);
+  launch_dot_partial(v, v, N, red.U, partial_n, stream);
   launch_reduce_final(combine(partial_n, 1), mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
   CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
@@ -1304,9 +1305,9 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         A.r3 = b2;
         launch_spmv(A, zj, w, stream);
       });
-      launch_cgs_dots(w, basis, binv, stride, j, N, partial, pstride, stream);
+      launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, partial_n, stream);
+      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream);
       launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, stream);
       check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;
@@ -1442,7 +1443,7 @@ void Solver::check_evolution() {
     gbase = topo.c0;
     rec0 = ev_a;
   }
-  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, partial_d, pstride, stream);
+  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, red.U, partial_d, pstride, stream);
   double* out5 = partial_d + 5 * (size_t)pstride;
   launch_evolution_final(combine_d(partial_d, 5), out5, stream);
   check_launch("check_evolution");

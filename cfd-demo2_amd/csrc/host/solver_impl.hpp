@@ -240,7 +240,8 @@ struct Solver {
   float* temp = nullptr;
   float* temp_p = nullptr;
   float* p_sol = nullptr;
-  uint32_t pstride = 0;          // chunk partials per vector (nchunks rounded up to 4: 16-byte loads)
+  uint32_t nunits = 0;           // unit partials (red.U chunks each) of this rank's cells
+  uint32_t pstride = 0;          // unit partials per vector (nunits rounded up to 4: 16-byte loads)
   float* partial = nullptr;      // [(m+1) * pstride] chunk partials (256 cells each)
   float* partial_n = nullptr;    // [nchunks]
   double* partial_d = nullptr;   // [5 * pstride] check_evolution
