@@ -129,9 +129,58 @@ float canon_dot(const float* x, const float* y, size_t ncells) {
   return canon_total(chunk, g);
 }
 
+// ---------------------------------------------------------------------------
+// Reference-semantics sensitivity mode (test infrastructure, oracle_set_semantics):
+// each flag replaces one deterministic resolution of SURVEY §0.1 by the
+// reference's own (non-deterministic or bug-for-bug) behaviour under one
+// plausible schedule, so tests can measure how far the canonical choices move
+// the fields.  0 = the canonical semantics the HIP path reproduces.
+constexpr int kSemInplaceSmoother = 1;  // amg.wgsl:36-49 in-place, 64-row workgroups in order
+constexpr int kSemRacyPrepare = 2;      // prepare_coupled.wgsl:140-143 vs :328-337, workgroups in order
+constexpr int kSemRefReductions = 4;    // gmres_ops.wgsl:159-293 / gmres_cgs.wgsl:28-120 order
+constexpr int kSemRestrictClamp = 8;    // amg.rs:707-719 + wgpu's Restrict bounds policy
+constexpr int kSemReverseOrder = 16;    // flags 1 / 2 with the workgroups run last-to-first:
+                                        // a second plausible schedule of the same reference
+
+// The reference's reduction over the 3N DOFs: 64-element workgroups reduced by
+// a halving tree (stride 32 .. 1, gmres_ops.wgsl:171-180), then either one
+// thread adding the partials in order (reduce_final*, :241-293; gpu_norm) or
+// 64 threads adding partials t, t+64, ... followed by the same halving tree
+// (reduce_dots_cgs, gmres_cgs.wgsl:86-120).
+float ref_dot(const float* x, const float* y, size_t n3, bool cgs_final) {
+  const size_t ng = (n3 + 63) / 64;
+  std::vector<float> part(ng);
+  for (size_t gi = 0; gi < ng; ++gi) {
+    float sdat[64];
+    for (size_t l = 0; l < 64; ++l) {
+      const size_t idx = gi * 64 + l;
+      sdat[l] = idx < n3 ? x[idx] * y[idx] : 0.0f;
+    }
+    for (size_t st = 32; st > 0; st >>= 1)
+      for (size_t l = 0; l < st; ++l) sdat[l] += sdat[l + st];
+    part[gi] = sdat[0];
+  }
+  if (!cgs_final) {
+    float tot = 0.0f;
+    for (float p : part) tot += p;
+    return tot;
+  }
+  float sdat[64];
+  for (size_t t = 0; t < 64; ++t) {
+    float a = 0.0f;
+    for (size_t k = t; k < ng; k += 64) a += part[k];
+    sdat[t] = a;
+  }
+  for (size_t st = 32; st > 0; st >>= 1)
+    for (size_t l = 0; l < st; ++l) sdat[l] += sdat[l + st];
+  return sdat[0];
+}
+
 // The distributed solver's reductions give these same bits on any rank count
 // (ranks own whole segments, kernels.hpp), so there is no per-rank order.
-float dist_dot(const float* x, const float* y, const std::vector<uint64_t>& starts) {
+float dist_dot(const float* x, const float* y, const std::vector<uint64_t>& starts, int sem = 0,
+               bool cgs_final = false) {
+  if (sem & kSemRefReductions) return ref_dot(x, y, 3 * starts.back(), cgs_final);
   return canon_dot(x, y, starts.back());
 }
 
@@ -263,6 +312,7 @@ Csr mat_mat_mult(const Csr& a, const Csr& b) {  // :187-229, f32 accumulation in
 
 struct Amg {
   std::vector<AmgLevel> levels;
+  int sem = 0;  // kSemInplaceSmoother | kSemRestrictClamp
 
   void build(const Csr& fine, size_t max_levels) {  // amg.rs:246-595
     Csr cur = fine;
@@ -291,12 +341,23 @@ struct Amg {
     }
   }
 
-  // smooth_op (amg.wgsl:24-50), restated out-of-place: x <- mix(x, (b - sigma)/diag, 0.8)
-  static void smooth(AmgLevel& L, float* x, const float* b) {
+  // smooth_op (amg.wgsl:24-50), restated out-of-place: x <- mix(x, (b - sigma)/diag, 0.8).
+  // inplace (kSemInplaceSmoother): the reference's in-place sweep with its
+  // 64-row workgroups run one after another (rows of earlier workgroups read
+  // new values, rows of the same workgroup all read before any writes).
+  static void smooth(AmgLevel& L, float* x, const float* b, bool inplace = false, bool reverse = false) {
+    const size_t blk = inplace ? 64 : std::max<size_t>(L.n, 1);
+    const size_t nb = (L.n + blk - 1) / blk;
+    for (size_t q = 0; q < nb; ++q) {
+      const size_t b0 = (reverse ? nb - 1 - q : q) * blk;
+      smooth_rows(L, x, b, b0, std::min(L.n, b0 + blk));
+    }
+  }
+  static void smooth_rows(AmgLevel& L, float* x, const float* b, size_t r0, size_t r1) {
     const float omega = 0.8f;
     const Csr& A = L.A;
-#pragma omp parallel for schedule(static)
-    for (long i = 0; i < (long)L.n; ++i) {
+#pragma omp parallel for schedule(static) if (r1 - r0 > 4096)
+    for (long i = (long)r0; i < (long)r1; ++i) {
       float sigma = 0.0f, diag = 1.0f;
       for (uint32_t k = A.row[i]; k < A.row[i + 1]; ++k) {
         const uint32_t col = A.col[k];
@@ -310,7 +371,7 @@ struct Amg {
       const float x_new = (b[i] - sigma) / diag;
       L.tmp[i] = wmix(x[i], x_new, omega);
     }
-    std::memcpy(x, L.tmp.data(), L.n * sizeof(float));
+    std::memcpy(x + r0, L.tmp.data() + r0, (r1 - r0) * sizeof(float));
   }
 
   // restrict_residual (amg.wgsl:80-111) for coarse rows < n_coarse (§0.1-7: skip the rest)
@@ -344,17 +405,26 @@ struct Amg {
   // amg.rs:666-770 with level 0 bound to (x = p_sol, b = temp_p)
   void v_cycle(float* x0, const float* b0) {
     const size_t L = levels.size();
+    const bool inplace = (sem & kSemInplaceSmoother) != 0, rev = (sem & kSemReverseOrder) != 0;
     auto X = [&](size_t i) { return i == 0 ? x0 : levels[i].x.data(); };
     auto B = [&](size_t i) { return i == 0 ? b0 : levels[i].b.data(); };
     for (size_t i = 0; i + 1 < L; ++i) {
-      smooth(levels[i], X(i), B(i));
-      if (levels[i].has_op) restrict_residual(levels[i], X(i), B(i), levels[i + 1].b.data());
+      smooth(levels[i], X(i), B(i), inplace, rev);
+      if (levels[i].has_op) {
+        restrict_residual(levels[i], X(i), B(i), levels[i + 1].b.data());
+        // kSemRestrictClamp: the threads of rows [n_c, 64 ceil(n_c / 64)) pass the
+        // fine-size guard (amg.rs:707-719); under wgpu's default Restrict policy their
+        // out-of-range loads clamp to an empty row and their store of 0 clamps onto the
+        // last coarse entry, in the same wavefront as its own thread (highest lane wins)
+        const size_t nc = levels[i + 1].n;
+        if ((sem & kSemRestrictClamp) && nc % 64 != 0) levels[i + 1].b[nc - 1] = 0.0f;
+      }
       std::fill(levels[i + 1].x.begin(), levels[i + 1].x.end(), 0.0f);
     }
-    for (int s = 0; s < 10; ++s) smooth(levels[L - 1], X(L - 1), B(L - 1));
+    for (int s = 0; s < 10; ++s) smooth(levels[L - 1], X(L - 1), B(L - 1), inplace, rev);
     for (size_t ii = L - 1; ii-- > 0;) {
       if (levels[ii].has_op) prolongate(levels[ii], X(ii), levels[ii + 1].x.data());
-      smooth(levels[ii], X(ii), B(ii));
+      smooth(levels[ii], X(ii), B(ii), inplace, rev);
     }
   }
 };
@@ -365,6 +435,7 @@ struct Amg {
 struct oracle_solver {
   // config
   cfd_config cfg;
+  int sem = 0;  // reference-semantics sensitivity flags (kSem*); 0 = canonical
   std::vector<uint64_t> starts;  // rank partition of the cells (one rank: {0, N})
   // mesh (f32 upload, init/mesh.rs)
   uint32_t N = 0, F = 0;
@@ -533,13 +604,28 @@ bool build(oracle_solver* s, const cfd_mesh_view* mv) {
 // ---------------------------------------------------------------------------
 // prepare_coupled.wgsl:63-348.  Snapshot semantics (§0.1-3): every read of
 // state comes from the pre-kernel state; d_p / grad_p are committed after.
+void prepare_cells(oracle_solver* s, uint32_t c0, uint32_t c1);
+
+// kSemRacyPrepare: the reference's race instead -- 64-cell workgroups run one
+// after another, each committing its d_p / grad_p before the next reads them
+// (a cell reads the NEW values of neighbours in earlier workgroups).
 void prepare(oracle_solver* s) {
+  const uint32_t N = s->N;
+  const uint32_t blk = (s->sem & kSemRacyPrepare) ? 64u : std::max(N, 1u);
+  const uint32_t nb = (N + blk - 1) / blk;
+  for (uint32_t q = 0; q < nb; ++q) {
+    const uint32_t b0 = ((s->sem & kSemReverseOrder) ? nb - 1 - q : q) * blk;
+    prepare_cells(s, b0, std::min(N, b0 + blk));
+  }
+}
+
+void prepare_cells(oracle_solver* s, uint32_t c0, uint32_t c1) {
   const cfd_constants c = s->constants;
   const uint32_t N = s->N;
   FluidState* st = s->S();
-  std::vector<float> new_dp(N), new_gpx(N), new_gpy(N);
-#pragma omp parallel for schedule(static)
-  for (long li = 0; li < (long)N; ++li) {
+  std::vector<float> new_dp(c1 - c0), new_gpx(c1 - c0), new_gpy(c1 - c0);
+#pragma omp parallel for schedule(static) if (c1 - c0 > 4096)
+  for (long li = (long)c0; li < (long)c1; ++li) {
     const uint32_t idx = (uint32_t)li;
     const float cx = s->cell_cx[idx], cy = s->cell_cy[idx];
     const float vol = s->cell_vols[idx];
@@ -693,18 +779,18 @@ void prepare(oracle_solver* s) {
       gvx += vfv * nx * area;
       gvy += vfv * ny * area;
     }
-    new_dp[idx] = (std::fabs(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
-    new_gpx[idx] = gpx / vol;
-    new_gpy[idx] = gpy / vol;
+    new_dp[idx - c0] = (std::fabs(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
+    new_gpx[idx - c0] = gpx / vol;
+    new_gpy[idx - c0] = gpy / vol;
     s->grad_u[2 * idx] = gux / vol;
     s->grad_u[2 * idx + 1] = guy / vol;
     s->grad_v[2 * idx] = gvx / vol;
     s->grad_v[2 * idx + 1] = gvy / vol;
   }
-  for (uint32_t i = 0; i < N; ++i) {
-    st[i].d_p = new_dp[i];
-    st[i].gpx = new_gpx[i];
-    st[i].gpy = new_gpy[i];
+  for (uint32_t i = c0; i < c1; ++i) {
+    st[i].d_p = new_dp[i - c0];
+    st[i].gpx = new_gpx[i - c0];
+    st[i].gpy = new_gpy[i - c0];
   }
 }
 
@@ -1094,7 +1180,7 @@ float residual_into_v0(oracle_solver* s) {
   const float alpha = 1.0f, beta = -1.0f;
 #pragma omp parallel for schedule(static)
   for (long i = 0; i < (long)n; ++i) v0[i] = alpha * s->rhs[i] + beta * s->w[i];
-  return std::sqrt(dist_dot(v0, v0, s->starts));
+  return std::sqrt(dist_dot(v0, v0, s->starts, s->sem));
 }
 
 void scale_in_place(float* v, size_t n, float a) {
@@ -1115,10 +1201,11 @@ cfd_linear_stats solve(oracle_solver* s) {
   ensure_fgmres(s);
   if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
     s->amg.reset(new Amg);
+    s->amg->sem = s->sem;
     s->amg->build(s->scalar, 20);
     s->amg_age = 0;
   }
-  const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts));
+  const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts, s->sem));
   // The two early exits are kept even under the fixed schedule: the first
   // step of a run at t=0 has b == 0 (inlet ramp smoothstep(0,ramp,0) = 0).
   if (rhs_norm < abstol || !std::isfinite(rhs_norm)) {
@@ -1159,7 +1246,7 @@ cfd_linear_stats solve(oracle_solver* s) {
       spmv(s, zj, s->w.data());
       // CGS (gmres_cgs.wgsl): H[i,j] = <w, V_i>, then w -= sum_i H[i,j] V_i
       for (int i = 0; i <= j; ++i)
-        s->H[(size_t)j * m1 + i] = dist_dot(s->w.data(), s->basis.data() + (size_t)i * n, s->starts);
+        s->H[(size_t)j * m1 + i] = dist_dot(s->w.data(), s->basis.data() + (size_t)i * n, s->starts, s->sem, true);
       {
         const float* Hc = s->H.data() + (size_t)j * m1;
         float* wv = s->w.data();
@@ -1171,7 +1258,7 @@ cfd_linear_stats solve(oracle_solver* s) {
           wv[e] = wv[e] - corr;
         }
       }
-      const float norm = std::sqrt(dist_dot(s->w.data(), s->w.data(), s->starts));
+      const float norm = std::sqrt(dist_dot(s->w.data(), s->w.data(), s->starts, s->sem));
       s->H[(size_t)j * m1 + j + 1] = norm;
       const float inv = norm > 1e-20f ? 1.0f / norm : 0.0f;
       {
@@ -1289,6 +1376,26 @@ void check_evolution(oracle_solver* s) {
   const bool have = s->have_prev && s->prev_u_cpu.size() == len;
   const float* prev = have ? s->prev_u_cpu.data() : nullptr;
   double tot[5];
+  if (s->sem & kSemRefReductions) {  // coupled_solver.rs:504-545: serial f64 loops
+    double e = 0.0, a = 0.0, b = 0.0, aa = 0.0, bb = 0.0;
+    if (have)
+      for (size_t k = 0; k < len; ++k) {
+        const float d = u_data[k] - prev[k];
+        e += (double)(d * d);
+      }
+    for (size_t c = 0; c < N; ++c) {
+      const double u = (double)u_data[2 * c], v = (double)u_data[2 * c + 1];
+      a += u;
+      b += v;
+      aa += u * u;
+      bb += v * v;
+    }
+    tot[0] = e;
+    tot[1] = a;
+    tot[2] = b;
+    tot[3] = aa;
+    tot[4] = bb;
+  } else {
   tot[0] = canon_sum<double>(N, [&](size_t c) {
     if (!have) return 0.0;
     double e = 0.0;
@@ -1309,6 +1416,7 @@ void check_evolution(oracle_solver* s) {
     const double v = (double)u_data[2 * c + 1];
     return v * v;
   });
+  }
   const double n = (double)N;
   const double mean_u = tot[1] / n, mean_v = tot[2] / n;
   const double var_u = std::fmax(tot[3] / n - mean_u * mean_u, 0.0);
@@ -1446,6 +1554,12 @@ oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg) {
 }
 
 void oracle_destroy(oracle_solver* s) { delete s; }
+
+int oracle_set_semantics(oracle_solver* s, int flags) {
+  s->sem = flags;
+  if (s->amg) s->amg->sem = flags;
+  return 0;
+}
 
 int oracle_set_u(oracle_solver* s, const double* uv) {  // solver.rs:9-21
   FluidState* st = s->S();

@@ -26,6 +26,16 @@ oracle_solver* oracle_create(const cfd_mesh_view* mesh, const cfd_config* cfg);
  * invariant (global AMG hierarchy, canonical reduction tree whose segments
  * ranks own whole), so `nranks` changes no result; = oracle_create.       */
 oracle_solver* oracle_create_dist(const cfd_mesh_view* mesh, const cfd_config* cfg, int nranks);
+/* Reference-semantics sensitivity mode: bit flags replacing the canonical
+ * deterministic resolutions of SURVEY §0.1 by the reference's behaviour under
+ * one plausible schedule: 1 in-place AMG smoother (64-row workgroups in
+ * order), 2 racy prepare_coupled reads (workgroups in order), 4 the
+ * reference's reduction order (64-wide trees + serial / strided finals, serial
+ * f64 check_evolution), 8 restrict_residual's out-of-bounds rows under wgpu's
+ * Restrict policy (last coarse entry zeroed when n_c % 64 != 0), 16 flags 1
+ * and 2 with the workgroups run last-to-first (a second plausible schedule).
+ * 0 = canonical (what the HIP path reproduces).                              */
+int oracle_set_semantics(oracle_solver* s, int flags);
 void oracle_destroy(oracle_solver* s);
 void oracle_set_threads(int n);
 int oracle_set_u(oracle_solver* s, const double* uv);

@@ -50,6 +50,7 @@ def olib():
         L.oracle_amg_levels.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_uint64)]
         L.oracle_last_error.restype = C.c_char_p
+        L.oracle_set_semantics.argtypes = [vp, C.c_int]
         _olib = L
     return _olib
 
@@ -79,6 +80,12 @@ class OracleSolver:
         self._h = C.c_void_p(h)
         self.num_cells = int(view.num_cells)
         self.num_faces = int(view.num_faces)
+
+    # reference-semantics sensitivity flags (oracle/oracle.h oracle_set_semantics)
+    SEM_INPLACE_SMOOTHER, SEM_RACY_PREPARE, SEM_REF_REDUCTIONS, SEM_RESTRICT_CLAMP = 1, 2, 4, 8
+
+    def set_semantics(self, flags: int) -> None:
+        olib().oracle_set_semantics(self._h, int(flags))
 
     def __del__(self):
         h = getattr(self, "_h", None)
