@@ -24,6 +24,12 @@ namespace {
 #ifndef CFD_CGS_NT
 #define CFD_CGS_NT 1
 #endif
+#ifndef CFD_CGS_NT_ST
+#define CFD_CGS_NT_ST CFD_CGS_NT  // nontemporal stores of the new basis vector
+#endif
+#ifndef CFD_RED_SEGS
+#define CFD_RED_SEGS 4  // independent partial loads per lane in the finishing kernels
+#endif
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ float wsmoothstep(float lo, float hi, float x) {
@@ -160,9 +166,83 @@ __host__ __device__ __forceinline__ uint32_t pow2_ceil(uint32_t n) {
   return p;
 }
 
+// Segment values of one vector's unit partials pv[0, nunits) into LDS a[0, P)
+// (P = pow2 >= nseg; segments past nseg are +0): segment sg = pairwise tree over
+// its GU unit values pv[sg GU ..] (missing units +0).  A group of LS = GU / K
+// lanes serves one segment, each lane K = min(4, GU) consecutive units (one
+// 16-byte load when K = 4), then the tree over the group's lanes.  A wavefront
+// iterates as a whole, so every shuffle reads a live lane.
+template <class T, int NT>
+__device__ __forceinline__ void seg_values(const T* __restrict__ pv, uint32_t nunits, uint32_t GU, uint32_t nseg,
+                                           uint32_t P, T* a) {
+  const uint32_t K = GU >= 4 ? 4u : GU;
+  const uint32_t LS = GU / K;
+  const uint32_t slots = P * LS;  // a multiple of 64 when >= 64
+  constexpr int R = CFD_RED_SEGS;  // independent loads in flight per lane
+  for (uint32_t base = threadIdx.x & ~63u; base < slots; base += R * NT) {
+    T e[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t t = base + r * NT + red_lane();
+      const uint32_t sg = t / LS;
+      const uint64_t k0 = (uint64_t)sg * GU + (uint64_t)(t % LS) * K;
+      if constexpr (sizeof(T) == 4) {
+        if (K == 4 && sg < nseg && k0 + 3 < nunits) {
+          const float4 q = *reinterpret_cast<const float4*>(pv + k0);
+          e[r][0] = q.x;
+          e[r][1] = q.y;
+          e[r][2] = q.z;
+          e[r][3] = q.w;
+          continue;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        e[r][q] = (sg < nseg && (uint32_t)q < K && k0 + q < nunits) ? pv[k0 + q] : T(0);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      T v = K == 4 ? (e[r][0] + e[r][1]) + (e[r][2] + e[r][3]) : (K == 2 ? e[r][0] + e[r][1] : e[r][0]);
+      for (uint32_t st = 1; st < LS; st <<= 1) v = v + __shfl_down(v, st);
+      const uint32_t t = base + r * NT + red_lane();
+      if (t < slots && t % LS == 0) a[t / LS] = v;
+    }
+  }
+}
+
+// Pairwise tree over a[0, P) (P a power of two <= kRedMaxSegments): blocks of
+// 64 by wavefront trees, then the <= 64 block values by one wavefront -- the
+// same bits as halving level by level.  b needs 65 entries.  Every thread
+// returns the total.
+template <class T, int NT>
+__device__ __forceinline__ T total_tree(const T* a, uint32_t P, T* b) {
+  constexpr uint32_t NW = NT / 64;
+  const uint32_t w = threadIdx.x >> 6, lane = red_lane();
+  __syncthreads();  // a[] complete
+  uint32_t Q = P;
+  const T* src = a;
+  if (P > 64) {
+    for (uint32_t gi = w; gi < P / 64; gi += NW) {
+      const T v = wave_tree(a[64 * gi + lane], 64);
+      if (lane == 0) b[gi] = v;
+    }
+    __syncthreads();
+    Q = P / 64;
+    src = b;
+  }
+  if (w == 0) {
+    const T v = wave_tree(lane < Q ? src[lane] : T(0), Q);
+    if (lane == 0) b[64] = v;
+  }
+  __syncthreads();
+  const T tot = b[64];
+  __syncthreads();  // the caller may reuse the LDS
+  return tot;
+}
+
 // Total of vector v of reduction r by the whole block (NT threads): the
 // segment values into LDS a[0, P) (+0 padding to P = pow2 >= nseg), then the
-// pairwise tree over them (ping-pong a/b).  Every thread returns the total.
+// pairwise tree over them.  Every thread returns the total.
 template <class T, int NT>
 __device__ __forceinline__ T red_total(const RedSrcT<T>& r, uint32_t v, T* a, T* b) {
   const uint32_t P = pow2_ceil(r.nseg);
@@ -176,33 +256,15 @@ __device__ __forceinline__ T red_total(const RedSrcT<T>& r, uint32_t v, T* a, T*
       }
       a[sg] = val;
     }
-  } else {  // one GPU: segment trees of the chunk partials, 4 segments per wavefront pass
-    const T* pv = r.p + (size_t)v * r.stride;
-    constexpr uint32_t NW = NT / 64;
-    const uint32_t w = threadIdx.x >> 6;
-    for (uint32_t s0 = w; s0 < P; s0 += 4 * NW) {
-      T o[4];
-      seg_trees<T, 4>(pv, r.nchunks, r.G, s0, NW, r.nseg, o);
-      if (red_lane() == 0) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (s0 + u * NW < P) a[s0 + u * NW] = o[u];
-      }
-    }
+  } else {  // one GPU: segment trees of the unit partials
+    seg_values<T, NT>(r.p + (size_t)v * r.stride, r.nchunks, r.G, r.nseg, P, a);
   }
-  __syncthreads();
-  for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
-    for (uint32_t i = threadIdx.x; i < len; i += NT) b[i] = a[2 * i] + a[2 * i + 1];
-    __syncthreads();
-    T* t = a;
-    a = b;
-    b = t;
-  }
-  const T tot = a[0];
-  __syncthreads();  // the caller may reuse the LDS
-  return tot;
+  return total_tree<T, NT>(a, P, b);
 }
-constexpr int kRedFinalThreads = 1024;
+#ifndef CFD_RED_FINAL_THREADS
+#define CFD_RED_FINAL_THREADS 1024
+#endif
+constexpr int kRedFinalThreads = CFD_RED_FINAL_THREADS;
 
 // ---------------------------------------------------------------------------
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
@@ -588,7 +650,7 @@ __device__ __forceinline__ void store_chunk3_stream(float* p, uint32_t k, uint32
     const size_t e0 = base + 256u * i;
     if (FULL || e0 + 3 < n3) {
       const f4v a = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
-#if CFD_CGS_NT
+#if CFD_CGS_NT_ST
       __builtin_nontemporal_store(a, reinterpret_cast<f4v*>(p + e0));
 #else
       *reinterpret_cast<f4v*>(p + e0) = a;
@@ -625,6 +687,16 @@ __device__ __forceinline__ bool block_full(uint32_t N) {
 }
 
 // unit partials of dot(x, y) over 3-component cells
+// norm outputs of a finished dot: mode 1: out = sqrt(s); mode 2: also inv, g0
+__device__ __forceinline__ void norm_out(float s, int mode, float* out, float* inv, float* g0) {
+  const float nrm = sqrtf(s);
+  out[0] = nrm;
+  if (mode == 2) {
+    inv[0] = 1.0f / nrm;  // host-side `1.0 / residual_norm` (coupled_solver_fgmres.rs:1872)
+    if (g0) g0[0] = nrm;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
                                                         const float* __restrict__ y, uint32_t N, uint32_t U,
                                                         float* partial) {
@@ -642,16 +714,9 @@ __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict_
 
 __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int mode, float* out, float* inv,
                                                                    float* g0) {
-  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
+  __shared__ float la[kRedMaxSegments], lb[65];
   const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
-  if (threadIdx.x == 0) {
-    const float nrm = sqrtf(s);
-    out[0] = nrm;
-    if (mode == 2) {
-      inv[0] = 1.0f / nrm;  // host-side `1.0 / residual_norm` (coupled_solver_fgmres.rs:1872)
-      if (g0) g0[0] = nrm;
-    }
-  }
+  if (threadIdx.x == 0) norm_out(s, mode, out, inv, g0);
 }
 
 // axpby (gmres_ops.wgsl:108-117) with alpha = 1, beta = -1: V0 = b - A x
@@ -825,16 +890,16 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
 // V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees;
 // the block's 4 chunk values per ii meet in LDS and become units at the end.
 template <bool FULL>
-__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ basis,
-                                               const float* __restrict__ binv, size_t stride, int j, uint32_t N,
-                                               float* lds) {
+__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ pool,
+                                               const uint8_t* slot, const float* __restrict__ binv, size_t stride,
+                                               int j, uint32_t N, float* lds) {
   const uint32_t k = red_chunk();
   float wv[12];
   load_chunk3<FULL>(w, k, 3 * N, wv);
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[12];
-    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(pool + (size_t)slot[ii] * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
     const float r = chunk_dot3(wv, v);
@@ -842,14 +907,17 @@ __device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, cons
   }
 }
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
-                                                     const float* __restrict__ basis,
+                                                     const float* __restrict__ pool, BasisMap map,
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
   __shared__ float lds[4 * 64];
+  __shared__ uint8_t slot[64];
+  if (threadIdx.x <= (unsigned)j) slot[threadIdx.x] = map.s[threadIdx.x];
+  __syncthreads();
   if (block_full(N))
-    cgs_dots_chunk<true>(w, basis, binv, stride, j, N, lds);
+    cgs_dots_chunk<true>(w, pool, slot, binv, stride, j, N, lds);
   else
-    cgs_dots_chunk<false>(w, basis, binv, stride, j, N, lds);
+    cgs_dots_chunk<false>(w, pool, slot, binv, stride, j, N, lds);
   __syncthreads();
   const uint32_t UB = 4 / U;
   for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
@@ -860,17 +928,19 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
 
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
 __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
-  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
+  __shared__ float la[kRedMaxSegments], lb[65];
   const int ii = blockIdx.x;
   const float s = red_total<float, kRedFinalThreads>(r, (uint32_t)ii, la, lb);
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
 }
 
 // update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
-// updated w is written straight into basis slot j+1 (unnormalised, see binv).
+// updated w (W_{j+1}, unnormalised, see binv) is written in place: each
+// wavefront reads its chunk of w and then overwrites it.
 template <bool FULL>
-__device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, float* basis, size_t stride, int j,
-                                                  const float* hcol, const float* scol, uint32_t N) {
+__device__ __forceinline__ float cgs_update_chunk(float* w, const float* __restrict__ pool, const uint8_t* slot,
+                                                  size_t stride, int j, const float* hcol, const float* scol,
+                                                  uint32_t N) {
   const uint32_t k = red_chunk();
   float corr[12];
 #pragma unroll
@@ -878,7 +948,7 @@ __device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, f
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[12];
-    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(pool + (size_t)slot[ii] * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
   }
@@ -886,23 +956,24 @@ __device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, f
   load_chunk3<FULL>(w, k, 3 * N, wn);
 #pragma unroll
   for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
-  store_chunk3_stream<FULL>(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
+  store_chunk3_stream<FULL>(w, k, 3 * N, wn);
   return chunk_dot3(wn, wn);
 }
-__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
-                                                            float* basis,
+__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w, const float* __restrict__ pool, BasisMap map,
                                                             const float* __restrict__ binv,
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
                                                             uint32_t N, uint32_t U, float* partial) {
   __shared__ float hcol[64], scol[64], lds[4];
+  __shared__ uint8_t slot[64];
   if (threadIdx.x <= (unsigned)j) {
     hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
     scol[threadIdx.x] = binv[threadIdx.x];
+    slot[threadIdx.x] = map.s[threadIdx.x];
   }
   __syncthreads();
-  const float r = block_full(N) ? cgs_update_chunk<true>(w, basis, stride, j, hcol, scol, N)
-                                : cgs_update_chunk<false>(w, basis, stride, j, hcol, scol, N);
+  const float r = block_full(N) ? cgs_update_chunk<true>(w, pool, slot, stride, j, hcol, scol, N)
+                                : cgs_update_chunk<false>(w, pool, slot, stride, j, hcol, scol, N);
   if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
@@ -911,12 +982,8 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
 // (gmres_logic.wgsl:24-76).
-__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
-                                                                  float* givens, float* g, float* binv,
-                                                                  float* resid_hist) {
-  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
-  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
-  if (threadIdx.x != 0) return;
+__device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens, float* g, float* binv,
+                                float* resid_hist) {
   const float norm = sqrtf(s);
   H[(size_t)j * m1 + j + 1] = norm;
   binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
@@ -942,6 +1009,13 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int 
   g[j] = cc * gj + ss * gj1;
   g[j + 1] = -ss * gj + cc * gj1;
   resid_hist[j] = fabsf(g[j + 1]);
+}
+__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
+                                                                  float* givens, float* g, float* binv,
+                                                                  float* resid_hist) {
+  __shared__ float la[kRedMaxSegments], lb[65];
+  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
+  if (threadIdx.x == 0) norm_givens_out(s, j, H, m1, givens, g, binv, resid_hist);
 }
 
 // predict_and_form_schur (schur_precond.wgsl:142-188), 4 cells per thread.
@@ -1844,7 +1918,7 @@ __global__ void __launch_bounds__(kBlock) k_evolution_partial(StateView cur, Sta
 }
 
 __global__ void __launch_bounds__(kRedFinalThreads) k_evolution_final(RedSrcD r, double* out5) {
-  __shared__ double la[kRedMaxSegments], lb[kRedMaxSegments];
+  __shared__ double la[kRedMaxSegments], lb[65];
   for (int f = 0; f < 5; ++f) {
     const double t = red_total<double, kRedFinalThreads>(r, (uint32_t)f, la, lb);
     if (threadIdx.x == 0) out5[f] = t;
@@ -1927,20 +2001,20 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
   else
     hipLaunchKernelGGL(k_spmv<false>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
 }
-void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
-                     uint32_t U, float* partial, uint32_t np, hipStream_t s) {
+void launch_cgs_dots(const float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
+                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s) {
   if (N)
-    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U, partial,
-                       np);
+    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, pool, map, binv, stride, j, N, U,
+                       partial, np);
 }
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
-void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
+void launch_cgs_update_norm(float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
+                            int j, const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
   if (N)
-    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1,
-                       N, U, partial);
+    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, pool, map, binv, stride, j,
+                       H, m1, N, U, partial);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, hipStream_t s) {

@@ -7,7 +7,7 @@ CFG=${CFG:-c2}
 for spec in "$@"; do
   name=${spec%%:*}
   envs=${spec#*:}
-  timeout -k 10 400 env ${envs//,/ } python bench.py --config $CFG --no-cpu-baseline --mesh-cache /tmp/ab_mesh_$CFG.bin > gpurun_out/abe_$name.json 2> gpurun_out/abe_$name.log || exit $?
+  timeout -k 10 400 env ${envs//,/ } python bench.py --config $CFG --no-cpu-baseline --ref-workloads 0 --mesh-cache /tmp/ab_mesh_$CFG.bin > gpurun_out/abe_$name.json 2> gpurun_out/abe_$name.log || exit $?
   python -c "
 import json
 d=json.load(open('gpurun_out/abe_$name.json')); r=d['roofline']
