@@ -890,16 +890,16 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
 // V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees;
 // the block's 4 chunk values per ii meet in LDS and become units at the end.
 template <bool FULL>
-__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ pool,
-                                               const uint8_t* slot, const float* __restrict__ binv, size_t stride,
-                                               int j, uint32_t N, float* lds) {
+__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ basis,
+                                               const float* __restrict__ binv, size_t stride, int j, uint32_t N,
+                                               float* lds) {
   const uint32_t k = red_chunk();
   float wv[12];
   load_chunk3<FULL>(w, k, 3 * N, wv);
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[12];
-    load_chunk3<FULL, true>(pool + (size_t)slot[ii] * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
     const float r = chunk_dot3(wv, v);
@@ -907,17 +907,14 @@ __device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, cons
   }
 }
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
-                                                     const float* __restrict__ pool, BasisMap map,
+                                                     const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
   __shared__ float lds[4 * 64];
-  __shared__ uint8_t slot[64];
-  if (threadIdx.x <= (unsigned)j) slot[threadIdx.x] = map.s[threadIdx.x];
-  __syncthreads();
   if (block_full(N))
-    cgs_dots_chunk<true>(w, pool, slot, binv, stride, j, N, lds);
+    cgs_dots_chunk<true>(w, basis, binv, stride, j, N, lds);
   else
-    cgs_dots_chunk<false>(w, pool, slot, binv, stride, j, N, lds);
+    cgs_dots_chunk<false>(w, basis, binv, stride, j, N, lds);
   __syncthreads();
   const uint32_t UB = 4 / U;
   for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
@@ -928,19 +925,17 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
 
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
 __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
-  __shared__ float la[kRedMaxSegments], lb[65];
+  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
   const int ii = blockIdx.x;
   const float s = red_total<float, kRedFinalThreads>(r, (uint32_t)ii, la, lb);
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
 }
 
 // update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
-// updated w (W_{j+1}, unnormalised, see binv) is written in place: each
-// wavefront reads its chunk of w and then overwrites it.
+// updated w is written straight into basis slot j+1 (unnormalised, see binv).
 template <bool FULL>
-__device__ __forceinline__ float cgs_update_chunk(float* w, const float* __restrict__ pool, const uint8_t* slot,
-                                                  size_t stride, int j, const float* hcol, const float* scol,
-                                                  uint32_t N) {
+__device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, float* basis, size_t stride, int j,
+                                                  const float* hcol, const float* scol, uint32_t N) {
   const uint32_t k = red_chunk();
   float corr[12];
 #pragma unroll
@@ -948,7 +943,7 @@ __device__ __forceinline__ float cgs_update_chunk(float* w, const float* __restr
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[12];
-    load_chunk3<FULL, true>(pool + (size_t)slot[ii] * stride, k, 3 * N, v);
+    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
 #pragma unroll
     for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
   }
@@ -956,24 +951,23 @@ __device__ __forceinline__ float cgs_update_chunk(float* w, const float* __restr
   load_chunk3<FULL>(w, k, 3 * N, wn);
 #pragma unroll
   for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
-  store_chunk3_stream<FULL>(w, k, 3 * N, wn);
+  store_chunk3_stream<FULL>(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
   return chunk_dot3(wn, wn);
 }
-__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(float* w, const float* __restrict__ pool, BasisMap map,
+__global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
+                                                            float* basis,
                                                             const float* __restrict__ binv,
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
                                                             uint32_t N, uint32_t U, float* partial) {
   __shared__ float hcol[64], scol[64], lds[4];
-  __shared__ uint8_t slot[64];
   if (threadIdx.x <= (unsigned)j) {
     hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
     scol[threadIdx.x] = binv[threadIdx.x];
-    slot[threadIdx.x] = map.s[threadIdx.x];
   }
   __syncthreads();
-  const float r = block_full(N) ? cgs_update_chunk<true>(w, pool, slot, stride, j, hcol, scol, N)
-                                : cgs_update_chunk<false>(w, pool, slot, stride, j, hcol, scol, N);
+  const float r = block_full(N) ? cgs_update_chunk<true>(w, basis, stride, j, hcol, scol, N)
+                                : cgs_update_chunk<false>(w, basis, stride, j, hcol, scol, N);
   if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
@@ -2001,20 +1995,20 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
   else
     hipLaunchKernelGGL(k_spmv<false>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
 }
-void launch_cgs_dots(const float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
-                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s) {
+void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
+                     uint32_t U, float* partial, uint32_t np, hipStream_t s) {
   if (N)
-    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, pool, map, binv, stride, j, N, U,
-                       partial, np);
+    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U, partial,
+                       np);
 }
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
-void launch_cgs_update_norm(float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
-                            int j, const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
   if (N)
-    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, pool, map, binv, stride, j,
-                       H, m1, N, U, partial);
+    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1,
+                       N, U, partial);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, hipStream_t s) {

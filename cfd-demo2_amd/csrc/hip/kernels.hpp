@@ -270,22 +270,15 @@ void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, 
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s);
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
-// basis: unnormalised W_i in pool slot map.s[i], scales binv[i]; unit partials
+// basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
-// Krylov basis pool: logical vector i lives in physical slot s[i] of the pool
-// (pool + s[i] * stride).  The CGS update writes W_{j+1} in place over w (the
-// DRAM pages it has just read: a fresh region costs the C2 update 356 -> 319
-// us) and the host moves w's slot into the basis (Solver::solve).
-struct BasisMap {
-  uint8_t s[64];
-};
-void launch_cgs_dots(const float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
-                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s);
+void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
+                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
-// W_{j+1} = w - sum_i H[i,j] V_i  (written over w) + ||W_{j+1}||^2 unit partials
-void launch_cgs_update_norm(float* w, const float* pool, const BasisMap& map, const float* binv, size_t stride,
-                            int j, const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s);
+// W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s);
 // ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, hipStream_t s);

@@ -466,16 +466,13 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   // Krylov vectors in the per-cell layout (ghost space: V_j and Z_j are read at
   // neighbours by the Schur prediction and the SpMV); 256-byte aligned slots
   stride = (3 * vlen + 63) & ~(size_t)63;
-  if (m1 + 1 > (int)sizeof(bmap.s)) throw std::invalid_argument("FGMRES restart length too large");
-  float* braw = arena.alloc<float>((size_t)(m1 + 1) * stride + 64);
+  float* braw = arena.alloc<float>((size_t)m1 * stride + 64);
   float* zraw = arena.alloc<float>((size_t)m * stride + 64);
-  CFD_HIP(hipMemsetAsync(braw, 0, ((size_t)(m1 + 1) * stride + 64) * sizeof(float), stream));
+  CFD_HIP(hipMemsetAsync(braw, 0, ((size_t)m1 * stride + 64) * sizeof(float), stream));
   CFD_HIP(hipMemsetAsync(zraw, 0, ((size_t)m * stride + 64) * sizeof(float), stream));
-  pool = braw + 3 * (size_t)shift;
-  for (int i = 0; i < m1; ++i) bmap.s[i] = (uint8_t)i;
-  wslot = (uint32_t)m1;
-  w = pool + (size_t)wslot * stride;
+  basis = braw + 3 * (size_t)shift;
   zvec = zraw + 3 * (size_t)shift;
+  w = valloc<float>(3);
   // pressure vectors: padded to a multiple of 64 owned rows (the AMG level-0
   // kernels process 4 rows per thread with 16-byte loads), plus ghosts
   temp = valloc<float>(1);
@@ -1198,7 +1195,7 @@ void Solver::v_cycle() {
 void Solver::precondition(int j, float* z) {
   const CoupledMatrix A = cmat();
   const bool jacobi = constants.precond_type != 1;
-  float* v = bvec(j);  // V_j = binv[j] * W_j
+  float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
   // the prediction reads neighbours' r_u, r_v
   overlapped(cell_plan, {{v, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix Ar = A;
@@ -1256,8 +1253,8 @@ float Solver::residual_into_v0_blocking() {
     A.r3 = b2;
     launch_spmv(A, x, w, stream);
   });
-  launch_residual_axpby(rhs, w, bvec(0), 3 * (size_t)N, stream);
-  return norm_blocking(bvec(0), 2, 1);
+  launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
+  return norm_blocking(basis, 2, 1);
 }
 
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
@@ -1308,15 +1305,9 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         A.r3 = b2;
         launch_spmv(A, zj, w, stream);
       });
-      launch_cgs_dots(w, pool, bmap, binv, stride, j, N, red.U, partial, pstride, stream);
+      launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-      launch_cgs_update_norm(w, pool, bmap, binv, stride, j, H, m1, N, red.U, partial_n, stream);
-      {  // W_{j+1} now lives in w's slot; w takes the slot logical j+1 held
-        const uint8_t freed = bmap.s[j + 1];
-        bmap.s[j + 1] = (uint8_t)wslot;
-        wslot = freed;
-        w = pool + (size_t)wslot * stride;
-      }
+      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream);
       launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, stream);
       check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;

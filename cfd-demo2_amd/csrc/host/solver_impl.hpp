@@ -233,16 +233,10 @@ struct Solver {
   float* dinv_p = nullptr;
   // FGMRES
   bool fgmres_ready = false;
-  // Krylov basis pool of m + 2 slots: logical basis vector i in slot bmap.s[i],
-  // the SpMV output w in slot wslot; the CGS update turns w into W_{j+1} in
-  // place and the slots are swapped (BasisMap, kernels.hpp)
-  float* pool = nullptr;
-  BasisMap bmap{};
-  uint32_t wslot = 0;
+  float* basis = nullptr;
   size_t stride = 0;
   float* zvec = nullptr;
   float* w = nullptr;
-  float* bvec(int i) const { return pool + (size_t)bmap.s[i] * stride; }
   float* temp = nullptr;
   float* temp_p = nullptr;
   float* p_sol = nullptr;
