@@ -611,67 +611,71 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
   *reinterpret_cast<float4*>(p + 8) = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-// A 256-cell chunk of a 3-component vector is 768 consecutive floats: three
-// 256-float parts, each read by the wavefront as one coalesced dwordx4 per
-// lane (lane l: floats 256 i + 4 l .. + 3 of the chunk).  v[4 i + e] = part i,
-// element e of this lane; floats past n3 (= 3 N) read as 0.  FULL: the chunk
-// lies inside n3 (every chunk but the last): no range checks.  NT: nontemporal
-// (streamed-once basis vectors, CFD_CGS_NT).
-template <bool FULL, bool NT = false>
-__device__ __forceinline__ void load_chunk3(const float* p, uint32_t k, uint32_t n3, float v[12]) {
-  const size_t base = (size_t)k * 768u + 4u * red_lane();
+// 3-component cell vectors in the reduction kernels (kernels.hpp: the cell
+// term of a dot is (x_u y_u + x_v y_v) + x_p y_p).  Block b covers the 4
+// chunks of cells [1024 b, 1024 b + 1024); lane l of wavefront w holds cell
+// c_q = 1024 b + 256 q + 64 w + l of chunk q (q = 0..3), its 3 floats by one
+// 12-byte access, so the block's 4 wavefronts read one chunk together (768
+// contiguous bytes per instruction).  A chunk value is the pairwise tree over
+// its 256 cells: each wavefront's 64 (a quarter, wave_tree), then the 4
+// quarters (quarter_chunk).  Cells past N: 0.  SER: every load completes
+// before the next issues -- for these kernels, which stream up to 51 vectors
+// at once, measured faster than keeping a wavefront's loads in flight
+// together (same-box A/B at C2: CGS update 349 -> 294 us, dots 300 -> 289).
+__device__ __forceinline__ size_t cell_q(uint32_t q) {
+  return (size_t)blockIdx.x * 1024u + 256u * q + (threadIdx.x & ~63u) + red_lane();
+}
+template <bool FULL, bool NT = false, bool SER = false>
+__device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[4][3]) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const size_t e0 = base + 256u * i;
-    if (FULL || e0 + 3 < n3) {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      const f4v* q = reinterpret_cast<const f4v*>(p + e0);
-      f4v a;
-      if constexpr (NT && CFD_CGS_NT)
-        a = __builtin_nontemporal_load(q);
-      else
-        a = *q;
-      v[4 * i] = a.x;
-      v[4 * i + 1] = a.y;
-      v[4 * i + 2] = a.z;
-      v[4 * i + 3] = a.w;
+  for (int q = 0; q < 4; ++q) {
+    const size_t c = cell_q(q);
+    if (FULL || c < N) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if constexpr (NT && CFD_CGS_NT)
+          v[q][e] = __builtin_nontemporal_load(p + 3 * c + e);
+        else
+          v[q][e] = p[3 * c + e];
+      }
+      if constexpr (SER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * i + e] = (e0 + e < n3) ? p[e0 + e] : 0.0f;
+      v[q][0] = v[q][1] = v[q][2] = 0.0f;
     }
   }
 }
 template <bool FULL>
-__device__ __forceinline__ void store_chunk3_stream(float* p, uint32_t k, uint32_t n3, const float v[12]) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const size_t base = (size_t)k * 768u + 4u * red_lane();
+__device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const float v[4][3]) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const size_t e0 = base + 256u * i;
-    if (FULL || e0 + 3 < n3) {
-      const f4v a = {v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+  for (int q = 0; q < 4; ++q) {
+    const size_t c = cell_q(q);
+    if (FULL || c < N) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
 #if CFD_CGS_NT_ST
-      __builtin_nontemporal_store(a, reinterpret_cast<f4v*>(p + e0));
+        __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
 #else
-      *reinterpret_cast<f4v*>(p + e0) = a;
+        p[3 * c + e] = v[q][e];
 #endif
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e0 + e < n3) p[e0 + e] = v[4 * i + e];
+      }
     }
   }
 }
-// chunk value of a dot over 3-component cells (kernels.hpp, 3-component
-// leaves): part i = pairwise tree over its 256 products (lane: (p0 + p1) +
-// (p2 + p3), then the wavefront tree), chunk = (part0 + part1) + part2; valid in lane 0
-__device__ __forceinline__ float chunk_dot3(const float a[12], const float b[12]) {
-  float t[3];
+__device__ __forceinline__ float cell_dot3(const float a[3], const float b[3]) {
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+// quarters of the block's chunks: lds[4 q + w] = wave_tree of wavefront w's
+// cell terms t[q] (written by lane 0)
+__device__ __forceinline__ void quarter_trees(const float t[4], float* lds) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
-    t[i] = wave_tree((a[4 * i] * b[4 * i] + a[4 * i + 1] * b[4 * i + 1]) +
-                     (a[4 * i + 2] * b[4 * i + 2] + a[4 * i + 3] * b[4 * i + 3]));
-  return (t[0] + t[1]) + t[2];
+  for (int q = 0; q < 4; ++q) {
+    const float r = wave_tree(t[q]);
+    if (red_lane() == 0) lds[4 * q + (threadIdx.x >> 6)] = r;
+  }
+}
+// chunk q's value from its 4 quarter values (pairwise)
+__device__ __forceinline__ float quarter_chunk(const float* l, int q) {
+  return (l[4 * q] + l[4 * q + 1]) + (l[4 * q + 2] + l[4 * q + 3]);
 }
 // Units of the block's 4 chunk values l[0..3] (kernels.hpp): unit u of U chunks
 // = the pairwise tree over them
@@ -681,12 +685,34 @@ __device__ __forceinline__ T unit_value(const T* l, uint32_t U, uint32_t u) {
   if (U == 2) return l[2 * u] + l[2 * u + 1];
   return l[u];
 }
+// ... from the 16 quarter values ql[4 q + w] of the block's chunks
+__device__ __forceinline__ float unit_value_q(const float* ql, uint32_t U, uint32_t u) {
+  float l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) l[q] = quarter_chunk(ql, q);
+  return unit_value(l, U, u);
+}
 // the block's chunks are all inside the mesh
 __device__ __forceinline__ bool block_full(uint32_t N) {
   return (size_t)(blockIdx.x + 1) * 4u * kRedChunkCells <= N;
 }
 
 // unit partials of dot(x, y) over 3-component cells
+__global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
+                                                        const float* __restrict__ y, uint32_t N, uint32_t U,
+                                                        float* partial) {
+  __shared__ float lds[16];
+  float a[4][3], b[4][3], t[4];
+  load_cells3<false>(x, N, a);
+  load_cells3<false>(y, N, b);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t[q] = cell_dot3(a[q], b[q]);
+  quarter_trees(t, lds);
+  __syncthreads();
+  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
+  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(lds, U, threadIdx.x);
+}
+
 // norm outputs of a finished dot: mode 1: out = sqrt(s); mode 2: also inv, g0
 __device__ __forceinline__ void norm_out(float s, int mode, float* out, float* inv, float* g0) {
   const float nrm = sqrtf(s);
@@ -695,21 +721,6 @@ __device__ __forceinline__ void norm_out(float s, int mode, float* out, float* i
     inv[0] = 1.0f / nrm;  // host-side `1.0 / residual_norm` (coupled_solver_fgmres.rs:1872)
     if (g0) g0[0] = nrm;
   }
-}
-
-__global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict__ x,
-                                                        const float* __restrict__ y, uint32_t N, uint32_t U,
-                                                        float* partial) {
-  __shared__ float lds[4];
-  const uint32_t k = red_chunk();
-  float a[12], b[12];
-  load_chunk3<false>(x, k, 3 * N, a);
-  load_chunk3<false>(y, k, 3 * N, b);
-  const float r = chunk_dot3(a, b);
-  if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
-  __syncthreads();
-  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
-  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value(lds, U, threadIdx.x);
 }
 
 __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int mode, float* out, float* inv,
@@ -887,45 +898,47 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
 }
 
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + unit] = <w, V_ii>, ii = 0..j,
-// V_ii = binv[ii] * W_ii.  One wavefront per 256-cell chunk, shuffle trees;
-// the block's 4 chunk values per ii meet in LDS and become units at the end.
+// V_ii = binv[ii] * W_ii, in the cell layout of load_cells3; quarter values
+// ql[16 ii + 4 q + w] in LDS, units at the end.
 template <bool FULL>
-__device__ __forceinline__ void cgs_dots_chunk(const float* __restrict__ w, const float* __restrict__ basis,
+__device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, const float* __restrict__ basis,
                                                const float* __restrict__ binv, size_t stride, int j, uint32_t N,
-                                               float* lds) {
-  const uint32_t k = red_chunk();
-  float wv[12];
-  load_chunk3<FULL>(w, k, 3 * N, wv);
+                                               float* ql) {
+  float wv[4][3];
+  load_cells3<FULL>(w, N, wv);
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
-    float v[12];
-    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
+    float v[4][3], t[4];
+    load_cells3<FULL, true, true>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
-    for (int e = 0; e < 12; ++e) v[e] = sc * v[e];
-    const float r = chunk_dot3(wv, v);
-    if (red_lane() == 0) lds[4 * ii + (threadIdx.x >> 6)] = r;
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) v[q][e] = sc * v[q][e];
+      t[q] = cell_dot3(wv[q], v[q]);
+    }
+    quarter_trees(t, ql + 16 * ii);
   }
 }
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
                                                      const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
-  __shared__ float lds[4 * 64];
+  __shared__ float ql[16 * 64];
   if (block_full(N))
-    cgs_dots_chunk<true>(w, basis, binv, stride, j, N, lds);
+    cgs_dots_cells<true>(w, basis, binv, stride, j, N, ql);
   else
-    cgs_dots_chunk<false>(w, basis, binv, stride, j, N, lds);
+    cgs_dots_cells<false>(w, basis, binv, stride, j, N, ql);
   __syncthreads();
   const uint32_t UB = 4 / U;
   for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
     const uint32_t ii = idx / UB, u = idx % UB, unit = blockIdx.x * UB + u;
-    if ((size_t)unit * U * kRedChunkCells < N) partial[(size_t)ii * np + unit] = unit_value(lds + 4 * ii, U, u);
+    if ((size_t)unit * U * kRedChunkCells < N) partial[(size_t)ii * np + unit] = unit_value_q(ql + 16 * ii, U, u);
   }
 }
 
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
 __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
-  __shared__ float la[kRedMaxSegments], lb[kRedMaxSegments];
+  __shared__ float la[kRedMaxSegments], lb[65];
   const int ii = blockIdx.x;
   const float s = red_total<float, kRedFinalThreads>(r, (uint32_t)ii, la, lb);
   if (threadIdx.x == 0) H[(size_t)j * m1 + ii] = s;
@@ -934,25 +947,27 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 // update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
 // updated w is written straight into basis slot j+1 (unnormalised, see binv).
 template <bool FULL>
-__device__ __forceinline__ float cgs_update_chunk(const float* __restrict__ w, float* basis, size_t stride, int j,
-                                                  const float* hcol, const float* scol, uint32_t N) {
-  const uint32_t k = red_chunk();
-  float corr[12];
-#pragma unroll
-  for (int e = 0; e < 12; ++e) corr[e] = 0.0f;
+__device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
+                                                 const float* hcol, const float* scol, uint32_t N, float t[4]) {
+  float corr[4][3] = {};
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
-    float v[12];
-    load_chunk3<FULL, true>(basis + (size_t)ii * stride, k, 3 * N, v);
+    float v[4][3];
+    load_cells3<FULL, true, true>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
-    for (int e = 0; e < 12; ++e) corr[e] += h * (sc * v[e]);
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) corr[q][e] += h * (sc * v[q][e]);
   }
-  float wn[12];
-  load_chunk3<FULL>(w, k, 3 * N, wn);
+  float wn[4][3];
+  load_cells3<FULL>(w, N, wn);
 #pragma unroll
-  for (int e = 0; e < 12; ++e) wn[e] = wn[e] - corr[e];
-  store_chunk3_stream<FULL>(basis + (size_t)(j + 1) * stride, k, 3 * N, wn);
-  return chunk_dot3(wn, wn);
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) wn[q][e] = wn[q][e] - corr[q][e];
+    t[q] = cell_dot3(wn[q], wn[q]);
+  }
+  store_cells3_stream<FULL>(basis + (size_t)(j + 1) * stride, N, wn);
 }
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
@@ -960,18 +975,21 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
                                                             uint32_t N, uint32_t U, float* partial) {
-  __shared__ float hcol[64], scol[64], lds[4];
+  __shared__ float hcol[64], scol[64], ql[16];
   if (threadIdx.x <= (unsigned)j) {
     hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
     scol[threadIdx.x] = binv[threadIdx.x];
   }
   __syncthreads();
-  const float r = block_full(N) ? cgs_update_chunk<true>(w, basis, stride, j, hcol, scol, N)
-                                : cgs_update_chunk<false>(w, basis, stride, j, hcol, scol, N);
-  if (red_lane() == 0) lds[threadIdx.x >> 6] = r;
+  float t[4];
+  if (block_full(N))
+    cgs_update_cells<true>(w, basis, stride, j, hcol, scol, N, t);
+  else
+    cgs_update_cells<false>(w, basis, stride, j, hcol, scol, N, t);
+  quarter_trees(t, ql);
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
-  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value(lds, U, threadIdx.x);
+  if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, threadIdx.x);
 }
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens

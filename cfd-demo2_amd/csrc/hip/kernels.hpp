@@ -33,13 +33,11 @@ constexpr uint32_t kMetaRankShift = 8;         // scalar-row rank of the neighbo
 
 // Canonical reduction order (rank-invariant; mirrors oracle/oracle.cpp).  A
 // sum over cells is ONE fixed binary tree over global cell indices:
-//   chunk    256 consecutive cells [256k, 256k + 256) (one wavefront):
-//            1-value cells: pairwise tree over the 256 cell terms; 3-component
-//            vectors (3 floats per cell): the chunk's 768 floats in three parts
-//            of 256, each a pairwise tree over its element terms, combined as
-//            (part0 + part1) + part2.  Missing cells / elements: +0.  GPU: lane l
-//            holds elements 4l..4l+3 of a part as ((e0 + e1) + (e2 + e3)) (one
-//            coalesced dwordx4), then lanes are paired at strides 1, 2, ..., 32
+//   chunk    256 consecutive cells [256k, 256k + 256): pairwise tree over the
+//            256 cell terms (missing cells: +0).  The cell term of a dot of
+//            3-component vectors (3 floats per cell) is (x_u y_u + x_v y_v) +
+//            x_p y_p.  GPU: a wavefront's 64 consecutive cells by a shuffle tree
+//            (strides 1, 2, ..., 32), then the chunk's 4 quarters pairwise
 //   segment  G = 2^g consecutive chunks: pairwise tree over G chunk slots
 //            (chunks past the end: +0).  g depends on the GLOBAL cell count
 //            only: g = clamp(floor(log2(N / 16384)), 0, 8)

@@ -917,7 +917,19 @@ void Solver::ensure_amg() {
   d_tail = arena.upload(tl, stream);
   check_launch("AMG setup");
   const char* tb_env = std::getenv("CFD_AMG_TAIL_BLOB");
-  if (tail_lds && !(tb_env && tb_env[0] == '0')) build_tail_blob(std::max({tail_first, 1, dist() ? amg_g : 0}));
+  if (tail_lds && !(tb_env && tb_env[0] == '0')) {
+    // The LDS image of the tail (matrices included) is the fast tail; when it
+    // does not fit in one CU's LDS, up to CFD_AMG_BLOB_SHIFT (default 2) more
+    // levels run with the row kernels so that it does (C1: the 3.9 k-row level).
+    const char* sh_env = std::getenv("CFD_AMG_BLOB_SHIFT");
+    const int shift = sh_env ? std::max(0, (int)std::strtol(sh_env, nullptr, 10)) : 2;
+    const int t0 = std::max({tail_first, 1, dist() ? amg_g : 0});
+    for (int t = t0; t < std::min(L, t0 + 1 + shift) && tail_blob_first < 0; ++t) {
+      if (t > t0 && levels[t - 1].wide) break;  // wide levels run only in the tail kernels
+      build_tail_blob(t);
+      if (tail_blob_first >= 0) tail_first = t;
+    }
+  }
   sync();
   amg_built = true;
   if (!from_checkpoint) amg_age = 0;

@@ -45,10 +45,9 @@ int fail(const std::string& m) {
 // any fixed order is a valid restatement, and this one is a single binary
 // tree over GLOBAL cell indices, so a distributed solver reproduces it
 // exactly on any rank count:
-//   chunk    256 cells: 1-value cells: pairwise tree over the 256 cell terms;
-//            3-component vectors: the chunk's 768 floats in three parts of 256,
-//            each a pairwise tree over its element terms, (part0 + part1) + part2
-//            (missing cells / elements: +0)
+//   chunk    256 cells: pairwise tree over the 256 cell terms (missing cells:
+//            +0); a dot of 3-component vectors has the cell term
+//            (x_u y_u + x_v y_v) + x_p y_p
 //   segment  G = 2^g chunks: pairwise tree over G chunk slots (missing: +0),
 //            g = clamp(floor(log2(N / 16384)), 0, 8) for the global N
 //   total    pairwise tree over the segment values padded to a power of two
@@ -110,23 +109,10 @@ T canon_sum(size_t ncells, Leaf leaf) {
 
 // canonical dot over 3-component cells
 float canon_dot(const float* x, const float* y, size_t ncells) {
-  const RedGeom g = red_geom(ncells);
-  const size_t n3 = 3 * ncells;
-  std::vector<float> chunk(g.nchunks);
-#pragma omp parallel for schedule(static)
-  for (long k = 0; k < (long)g.nchunks; ++k) {
-    float part[3];
-    for (int i = 0; i < 3; ++i) {
-      float lv[kChunkCells];
-      for (size_t e = 0; e < kChunkCells; ++e) {
-        const size_t d = (size_t)k * 3 * kChunkCells + (size_t)i * kChunkCells + e;
-        lv[e] = d < n3 ? x[d] * y[d] : 0.0f;
-      }
-      part[i] = pairwise(lv, kChunkCells);
-    }
-    chunk[k] = (part[0] + part[1]) + part[2];
-  }
-  return canon_total(chunk, g);
+  return canon_sum<float>(ncells, [&](size_t c) {
+    const size_t d = 3 * c;
+    return (x[d] * y[d] + x[d + 1] * y[d + 1]) + x[d + 2] * y[d + 2];
+  });
 }
 
 // ---------------------------------------------------------------------------

@@ -72,15 +72,10 @@ def canon_sum(terms):
 
 
 def canon_dot3(x, y):
-    """canonical dot of two 3-component cell vectors (3N float32 each)"""
-    n3 = len(x)
-    n = n3 // 3
-    G, nch, nseg = _geom(n)
-    p = np.zeros(nch * 768, F)
-    p[:n3] = x * y
-    parts = _pairwise_last(p.reshape(nch, 3, 256))
-    chunks = (parts[:, 0] + parts[:, 1]) + parts[:, 2]
-    return _total(chunks, n)
+    """canonical dot of two 3-component cell vectors (3N float32 each): cell
+    terms (x_u y_u + x_v y_v) + x_p y_p, summed like canon_sum"""
+    p = (x * y).reshape(-1, 3)
+    return canon_sum((p[:, 0] + p[:, 1]) + p[:, 2])
 
 
 # ---------------------------------------------------------------------- mesh
