@@ -27,6 +27,18 @@ namespace {
 #ifndef CFD_CGS_NT_ST
 #define CFD_CGS_NT_ST CFD_CGS_NT  // nontemporal stores of the new basis vector
 #endif
+#ifndef CFD_CGS_DOT_SER
+#define CFD_CGS_DOT_SER 1  // one basis load in flight per wavefront (load_cells3)
+#endif
+#ifndef CFD_CGS_UPD_SER
+#define CFD_CGS_UPD_SER 1
+#endif
+#ifndef CFD_UPDX_SER
+#define CFD_UPDX_SER 1  // one Z load in flight per thread in k_update_x (A/B C2: 614 -> 583 us)
+#endif
+#ifndef CFD_DPP_TREE
+#define CFD_DPP_TREE 1  // wavefront trees of the chunk kernels by DPP (wave_tree64)
+#endif
 #ifndef CFD_RED_SEGS
 #define CFD_RED_SEGS 4  // independent partial loads per lane in the finishing kernels
 #endif
@@ -664,12 +676,35 @@ __device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const 
 __device__ __forceinline__ float cell_dot3(const float a[3], const float b[3]) {
   return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
 }
+// wave_tree(v, 64) without LDS traffic: strides 1..8 by DPP row shifts (lane
+// l adds lane l + s of its row of 16; only lanes whose chain stays inside the
+// row are read), strides 16 and 32 from the row roots by lane reads -- the
+// same additions in the same order.  Valid in every lane.
+template <int S>
+__device__ __forceinline__ float row_down(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + S, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float wave_tree64(float v) {
+#if CFD_DPP_TREE
+  v = v + row_down<1>(v);
+  v = v + row_down<2>(v);
+  v = v + row_down<4>(v);
+  v = v + row_down<8>(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+#else
+  return wave_tree(v);
+#endif
+}
 // quarters of the block's chunks: lds[4 q + w] = wave_tree of wavefront w's
 // cell terms t[q] (written by lane 0)
 __device__ __forceinline__ void quarter_trees(const float t[4], float* lds) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float r = wave_tree(t[q]);
+    const float r = wave_tree64(t[q]);
     if (red_lane() == 0) lds[4 * q + (threadIdx.x >> 6)] = r;
   }
 }
@@ -909,7 +944,7 @@ __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, cons
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[4][3], t[4];
-    load_cells3<FULL, true, true>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, true, CFD_CGS_DOT_SER>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -953,7 +988,7 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
-    load_cells3<FULL, true, true>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, true, CFD_CGS_UPD_SER>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1270,6 +1305,11 @@ __device__ __forceinline__ float4 ld4_upd(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 #endif
 }
+__device__ __forceinline__ void upd_wait() {
+#if CFD_UPDX_SER
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
 
 // basis_size x axpy_from_y (gmres_ops.wgsl:96-105) fused: x = y_i * z_i + x, i ascending
 __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __restrict__ z,
@@ -1282,7 +1322,9 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
     int ii = 0;
     for (; ii + 1 < k; ii += 2) {
       const float4 z0 = ld4_upd(z + (size_t)ii * stride + e);
+      upd_wait();
       const float4 z1 = ld4_upd(z + (size_t)(ii + 1) * stride + e);
+      upd_wait();
       const float y0 = y[ii], y1 = y[ii + 1];
       xv.x = y0 * z0.x + xv.x;
       xv.y = y0 * z0.y + xv.y;
