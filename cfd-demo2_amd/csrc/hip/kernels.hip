@@ -59,6 +59,15 @@ __device__ __forceinline__ float f4(const float4& v, int k) {
 __device__ __forceinline__ uint32_t u4(const uchar4& v, int k) {
   return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
 }
+// aligned-slot rows (CoupledMatrix::lg): slots in use, and whether slot r
+// holds an entry of row k of the thread's 4
+__device__ __forceinline__ uint32_t lg_used(const ushort4& v, int k) {
+  return (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) & 0xFFu;
+}
+__device__ __forceinline__ bool lg_on(const ushort4& v, int k, uint32_t r) {
+  const uint32_t w = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+  return r < (w & 0xFFu) && !((w >> 8 >> r) & 1u);
+}
 
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
@@ -496,10 +505,10 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
       sdpp += lapl;
       const float scoeff = c.density * dp_f * area / dist;
       sdiag += scoeff;
-      const size_t slot = (size_t)rank * a.ld + i;
-      a.cval_a[slot] = make_float2(coeff, -lapl);
-      a.cval_g[slot] = make_float2(oml * pgx, oml * pgy);
-      a.sval[slot] = -scoeff;
+      const size_t cslot = (size_t)((meta >> kMetaTSlotShift) & 0xFFu) * a.ld + i;
+      a.cval_a[cslot] = make_float2(coeff, -lapl);
+      a.cval_g[cslot] = make_float2(oml * pgx, oml * pgy);
+      a.sval[(size_t)rank * a.ld + i] = -scoeff;
     } else if (bt == 1u) {
       const float ramp = wsmoothstep(0.0f, c.ramp_time, c.time);
       const float ubx = c.inlet_velocity * ramp, uby = 0.0f;
@@ -530,12 +539,11 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
       sdiag += scoeff;
     }
   }
-  const uint32_t dr = a.srank_diag[i];
-  const size_t dslot = (size_t)dr * a.ld + i;
-  a.cval_a[dslot] = make_float2(diag_uv, 0.0f + sdpp);
-  a.cval_g[dslot] = make_float2(sdup, sdvp);
+  const size_t cdslot = (size_t)a.cslot_diag[i] * a.ld + i;
+  a.cval_a[cdslot] = make_float2(diag_uv, 0.0f + sdpp);
+  a.cval_g[cdslot] = make_float2(sdup, sdvp);
   a.cdiag2[i] = make_float2(sdpu, sdpv);
-  a.sval[dslot] = sdiag;
+  a.sval[(size_t)a.srank_diag[i] * a.ld + i] = sdiag;
   a.rhs[3 * (size_t)i + 0] = rhs_u;
   a.rhs[3 * (size_t)i + 1] = rhs_v;
   a.rhs[3 * (size_t)i + 2] = rhs_p;
@@ -870,7 +878,7 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
 // thread; per-row term order identical to the CSR row (neighbour-major, u,v,p).
 template <bool D16, int U>
 __device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
-                                           uint32_t r0, uint32_t rmax, const uchar4 ln, const uchar4 dr,
+                                           uint32_t r0, uint32_t rmax, const ushort4 ln, const uchar4 dr,
                                            const float2 d2[4], float su[4], float sv[4], float sp[4]) {
   float2 a[U][4], g[U][4];
   int c[U][4];
@@ -886,7 +894,7 @@ __device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* 
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const bool on = r0 + u < u4(ln, k);
+      const bool on = lg_on(ln, k, r0 + u);
       const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
       xg[u][k][0] = gat<true>(on, x + j);
       xg[u][k][1] = gat<true>(on, x + j + 1);
@@ -897,7 +905,7 @@ __device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* 
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t r = r0 + u;
-      if (r >= u4(ln, k)) continue;
+      if (!lg_on(ln, k, r)) continue;
       const bool dg = (r == u4(dr, k));
       const float uu = a[u][k].x, pp = a[u][k].y, up = g[u][k].x, vp = g[u][k].y;
       const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
@@ -920,11 +928,11 @@ __global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* _
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   uint32_t i0;
   if (!row_range<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
+  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
   float2 d2[4];
   load2x4(A.cdiag2 + i0, d2);
-  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
   float su[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   spmv_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, su, sv, sp);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv_group<D16, U>(A, x, i0, r0, maxlen - 1u, ln, dr, d2, su, sv, sp);
@@ -1080,7 +1088,7 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int 
 template <bool D16, int U>
 __device__ __forceinline__ void predict_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
                                               const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
-                                              uint32_t rmax, const uchar4 ln, const uchar4 dr, const float2 d2[4],
+                                              uint32_t rmax, const ushort4 ln, const uchar4 dr, const float2 d2[4],
                                               float rhs[4]) {
   float2 g[U][4];
   int c[U][4];
@@ -1122,7 +1130,7 @@ __device__ __forceinline__ void predict_group(const CoupledMatrix& A, const floa
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const bool on = r0 + u < u4(ln, k);
+        const bool on = lg_on(ln, k, r0 + u);
         const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
         gd[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, dinv_uv + c[u][k]);
         gu[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j);
@@ -1134,7 +1142,7 @@ __device__ __forceinline__ void predict_group(const CoupledMatrix& A, const floa
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint32_t r = r0 + u;
-      if (r >= u4(ln, k)) continue;
+      if (!lg_on(ln, k, r)) continue;
       const bool dg = (r == u4(dr, k));
       const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
       const float ru = sc * gu[u][k], rv = sc * gv[u][k];
@@ -1162,11 +1170,11 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
   float rhs[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) rhs[k] = sc * wo[3 * k + 2];
-  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
+  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
   float2 d2[4];
   load2x4(A.cdiag2 + i0, d2);
-  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
   predict_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, rhs);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
     predict_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, ln, dr, d2, rhs);
@@ -1206,7 +1214,7 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 #endif
 template <bool D16, int U>
 __device__ __forceinline__ void correct_group(const CoupledMatrix& A, const float* __restrict__ p_sol,
-                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln, float cu[4],
+                                              uint32_t i0, uint32_t r0, uint32_t rmax, const ushort4 ln, float cu[4],
                                               float cv[4]) {
   float2 g[U][4];
   int c[U][4];
@@ -1236,13 +1244,13 @@ __device__ __forceinline__ void correct_group(const CoupledMatrix& A, const floa
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(r0 + u < u4(ln, k), p_sol + c[u][k]);
+      for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(lg_on(ln, k, r0 + u), p_sol + c[u][k]);
   }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (r0 + u >= u4(ln, k)) continue;
+      if (!lg_on(ln, k, r0 + u)) continue;
       cu[k] += g[u][k].x * pj[u][k];
       cv[k] += g[u][k].y * pj[u][k];
     }
@@ -1258,8 +1266,8 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
   constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
   uint32_t i0;
   if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const uchar4 ln = *reinterpret_cast<const uchar4*>(A.len + i0);
-  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
+  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
   float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   correct_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, ln, cu, cv);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, ln, cu, cv);

@@ -30,6 +30,7 @@ constexpr uint32_t kMetaOwner = 1u << 2;       // face_owner == this cell
 constexpr uint32_t kMetaDegen = 1u << 3;       // d_c + d_o <= 1e-6 (lambda fallback 0.5)
 constexpr uint32_t kMetaFluxFlip = 1u << 4;    // normal_flux = -stored normal
 constexpr uint32_t kMetaRankShift = 8;         // scalar-row rank of the neighbour (0xFF boundary)
+constexpr uint32_t kMetaTSlotShift = 16;       // its slot in the coupled-matrix ELL (Topology::tslot)
 
 // Canonical reduction order (rank-invariant; mirrors oracle/oracle.cpp).  A
 // sum over cells is ONE fixed binary tree over global cell indices:
@@ -153,6 +154,7 @@ struct AssembleArgs {
   const float2* grad_u;
   const float2* grad_v;
   const uint32_t* srank_diag;  // [N] diagonal rank in the scalar row
+  const uint8_t* cslot_diag;   // [N] slot of the diagonal in the coupled-matrix ELL
   float2* cval_a; // [r*ld + i] {A_uu (=A_vv), A_pp}
   float2* cval_g; // [r*ld + i] {A_up (=A_pu), A_vp (=A_pv)}
   float2* cdiag2; // [ld] {s_pu, s_pv} of the diagonal block
@@ -172,10 +174,12 @@ struct CoupledMatrix {
   uint32_t ld;            // slot stride (N rounded up to 64)
   int ws;
   int use16;
-  const int32_t* col;     // [r*ld + i] signed local column
+  // aligned-slot ELL (Topology::tslot): entries of a row sit in increasing
+  // slots (CSR order), gaps where a neighbour is missing
+  const int32_t* col;     // [r*ld + i] signed local column (gaps: a virtual column)
   const int16_t* col16;   // [r*ld + i] col - i (use16)
-  const uint8_t* len;     // [ld]
-  const uint8_t* drank;   // [ld]
+  const uint16_t* lg;     // [ld] slots in use (low byte) | gap mask << 8
+  const uint8_t* drank;   // [ld] slot of the diagonal
   const float2* cval_a;
   const float2* cval_g;
   const float2* cdiag2;   // [ld]

@@ -144,6 +144,12 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (topo.use16) d_scol16 = arena.upload(topo.ell_col16, stream);
   d_slen8 = arena.upload(topo.ell_len8, stream);
   d_sdrank8 = arena.upload(topo.ell_drank8, stream);
+  if (topo.use16)
+    d_tcol16 = arena.upload(topo.tcol16, stream);
+  else
+    d_tcol = arena.upload(topo.tcol, stream);
+  d_tlg = arena.upload(topo.tlg, stream);
+  d_tdrank8 = arena.upload(topo.tdrank8, stream);
   // fields (init/fields.rs:62-139): zero-initialised, with ghost space
   auto zeros_state = [&](StateView& v) {
     v.u = valloc<float2>(1);
@@ -222,10 +228,10 @@ CoupledMatrix Solver::cmat() const {
   A.ld = topo.ld;
   A.ws = topo.ws;
   A.use16 = topo.use16 ? 1 : 0;
-  A.col = d_scol;
-  A.col16 = d_scol16;
-  A.len = d_slen8;
-  A.drank = d_sdrank8;
+  A.col = d_tcol;
+  A.col16 = d_tcol16;
+  A.lg = d_tlg;
+  A.drank = d_tdrank8;
   A.cval_a = cval_a;
   A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
@@ -449,6 +455,7 @@ void Solver::assemble() {
   a.grad_u = grad_u;
   a.grad_v = grad_v;
   a.srank_diag = d_sdrank;
+  a.cslot_diag = d_tdrank8;
   a.cval_a = cval_a;
   a.cval_g = cval_g;
   a.cdiag2 = cdiag2;
@@ -1700,7 +1707,8 @@ void Solver::debug_buffer(int id, float* out) {
         const uint32_t so = topo.srow[i], nb = topo.srow[i + 1] - so;
         const uint32_t r0 = 9 * so, r1 = r0 + 3 * nb, r2 = r0 + 6 * nb;
         for (uint32_t r = 0; r < nb; ++r) {
-          const float2 a = ca[(size_t)r * ld + i], gg = cg[(size_t)r * ld + i];
+          const size_t e = (size_t)topo.tslot[so + r] * ld + i;  // aligned slot of CSR entry r
+          const float2 a = ca[e], gg = cg[e];
           const bool diag = (r == topo.ell_drank[i]);
           out[r0 + 3 * r + 0] = a.x;
           out[r0 + 3 * r + 1] = 0.0f;

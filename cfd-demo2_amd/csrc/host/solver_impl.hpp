@@ -117,6 +117,21 @@ struct Topology {
   bool use16 = false;            // every |col - row| < 2^15: ell_col16 valid
   std::vector<int16_t> ell_col16;
   std::vector<uint8_t> ell_len8, ell_drank8;
+  // Coupled-matrix ELL (CoupledMatrix, kernels.hpp): the same rows with their
+  // entries moved to aligned slots.  tmode[r] = the most frequent column - row
+  // of slot r over the full rows; a row with fewer entries places each entry,
+  // in CSR order, at the first slot still free whose mode is its delta, so
+  // missing neighbours (walls) leave gaps instead of shifting the rest of the
+  // row, and 4 consecutive rows keep 4 consecutive columns per slot.  Gaps and
+  // trailing slots hold the virtual column row + tmode[r] (clamped into the
+  // vectors' range; never accumulated).  Position layout when ws > 8 or
+  // CFD_TYPED_ELL=0.
+  std::vector<int32_t> tmode;
+  std::vector<uint8_t> tslot;    // [nnz] slot of CSR entry k
+  std::vector<int32_t> tcol;     // [r*ld + i]
+  std::vector<int16_t> tcol16;   // (use16)
+  std::vector<uint16_t> tlg;     // [ld] slots in use | gap mask << 8
+  std::vector<uint8_t> tdrank8;  // [ld] slot of the diagonal
 };
 
 // Throws std::invalid_argument on inconsistent meshes.
@@ -209,6 +224,10 @@ struct Solver {
   int16_t* d_scol16 = nullptr;
   uint8_t* d_slen8 = nullptr;
   uint8_t* d_sdrank8 = nullptr;
+  int32_t* d_tcol = nullptr;      // coupled-matrix ELL (Topology::tslot)
+  int16_t* d_tcol16 = nullptr;
+  uint16_t* d_tlg = nullptr;
+  uint8_t* d_tdrank8 = nullptr;
   uint32_t* d_slen = nullptr;
   uint32_t* d_sdrank = nullptr;
   // ring of 3 FluidState slots (SoA) + prepare's d_p / grad_p scratch

@@ -7,6 +7,8 @@
 // same order, as the WGSL expression it replaces (compiled -ffp-contract=off),
 // so the kernels reading it produce identical bits.
 #include <algorithm>
+#include <cstdlib>
+#include <unordered_map>
 #include <cmath>
 #include <stdexcept>
 
@@ -129,12 +131,74 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
     t.ell_len8[li] = (uint8_t)t.ell_len[li];
     t.ell_drank8[li] = (uint8_t)t.ell_drank[li];
   }
+  // coupled-matrix ELL with aligned slots (Topology::tslot)
+  {
+    const char* te = std::getenv("CFD_TYPED_ELL");
+    const bool typed = ws <= 8 && !(te && te[0] == '0');
+    t.tmode.assign(ws, 0);
+    if (typed) {
+      const uint32_t step = N > (1u << 20) ? 7u : 1u;  // a sample is enough for a mode
+      for (int r = 0; r < ws; ++r) {
+        std::unordered_map<int32_t, uint32_t> cnt;
+        for (uint32_t li = 0; li < N; li += step)
+          if (t.ell_len[li] == (uint32_t)ws) ++cnt[t.ell_col[(size_t)r * ld + li] - (int32_t)li];
+        uint32_t best = 0;
+        for (const auto& kv : cnt)
+          if (kv.second > best || (kv.second == best && kv.first < t.tmode[r])) {
+            best = kv.second;
+            t.tmode[r] = kv.first;
+          }
+      }
+    }
+    const int32_t vlo = -(int32_t)t.glo, vhi = (int32_t)(t.npad + t.ghi) - 1;
+    t.tslot.assign(t.scol.size(), 0);
+    t.tcol.assign((size_t)ws * ld, 0);
+    t.tlg.assign(ld, 0);
+    t.tdrank8.assign(ld, 0);
+    for (uint32_t li = 0; li < ld; ++li) {
+      const uint32_t a = li < N ? t.srow[li] : 0, len = li < N ? t.srow[li + 1] - a : 0;
+      std::vector<int> slot(len);
+      int prev = -1;
+      for (uint32_t q = 0; q < len; ++q) {
+        const int32_t d = t.ell_col[(size_t)q * ld + li] - (int32_t)li;
+        const int lo = prev + 1, hi = ws - (int)(len - q);
+        int s = lo;
+        if (typed && len < (uint32_t)ws)
+          for (int c = lo; c <= hi; ++c)
+            if (t.tmode[c] == d) {
+              s = c;
+              break;
+            }
+        slot[q] = prev = s;
+      }
+      uint32_t used = 0, on = 0;
+      for (uint32_t q = 0; q < len; ++q) {
+        t.tslot[a + q] = (uint8_t)slot[q];
+        on |= 1u << slot[q];
+        used = (uint32_t)slot[q] + 1;
+        t.tcol[(size_t)slot[q] * ld + li] = t.ell_col[(size_t)q * ld + li];
+      }
+      const uint32_t gap = ((1u << used) - 1u) & ~on;
+      for (int r = 0; r < ws; ++r) {
+        if (on >> r & 1u) continue;
+        const int32_t v = li < N ? (int32_t)li + t.tmode[r] : (int32_t)li;
+        t.tcol[(size_t)r * ld + li] = std::min(std::max(v, vlo), vhi);
+        const int64_t dd = (int64_t)t.tcol[(size_t)r * ld + li] - (int64_t)li;
+        if (dd < -32768 || dd > 32767) small = false;
+      }
+      t.tlg[li] = (uint16_t)(used | gap << 8);
+      if (li < N) t.tdrank8[li] = (uint8_t)slot[t.ell_drank[li]];
+    }
+  }
   t.use16 = small;
   t.ell_col16.clear();
+  t.tcol16.clear();
   if (small) {
     t.ell_col16.resize(t.ell_col.size());
     for (size_t e = 0; e < t.ell_col.size(); ++e)
       t.ell_col16[e] = (int16_t)(t.ell_col[e] - (int32_t)(e % ld));
+    t.tcol16.resize(t.tcol.size());
+    for (size_t e = 0; e < t.tcol.size(); ++e) t.tcol16[e] = (int16_t)(t.tcol[e] - (int32_t)(e % ld));
   }
 
   // face slots
@@ -204,6 +268,7 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
         rank = (uint32_t)(it - b);
       }
       meta |= rank << kMetaRankShift;
+      if (internal) meta |= (uint32_t)t.tslot[t.srow[li] + rank] << kMetaTSlotShift;
       const size_t e = (size_t)k * N + li;
       t.fs_other[e] = internal ? t.rel(other) : kNoCell;
       t.fs_meta[e] = meta;
