@@ -49,6 +49,27 @@ void run(const char* name, const cfd2::Mesh& m) {
           cfd2::build_halo_plan(starts, r, t.srow.data(), t.N, t.scol.data(), t.ghost, t.glo, t.npad);
       rows += t.N;
       nnz += t.scol.size();
+      // aligned-slot coupled ELL: every CSR entry in its own, increasing slot,
+      // with its column there; slots in use and gaps as the mask says
+      for (uint32_t i = 0; i < t.N; ++i) {
+        const uint32_t a = t.srow[i], len = t.srow[i + 1] - a;
+        uint32_t on = 0;
+        int prev = -1;
+        for (uint32_t q = 0; q < len; ++q) {
+          const int s = t.tslot[a + q];
+          check(s > prev && s < t.ws, "aligned slots must increase inside the ELL width");
+          check(t.tcol[(size_t)s * t.ld + i] == t.rel(t.scol[a + q]), "aligned slot holds its column");
+          on |= 1u << s;
+          prev = s;
+        }
+        const uint32_t used = t.tlg[i] & 0xFFu, gap = t.tlg[i] >> 8;
+        check(used == (uint32_t)prev + 1 && (gap | on) == (1u << used) - 1u && !(gap & on), "slot mask");
+        check(t.tslot[a + t.ell_drank[i]] == t.tdrank8[i], "diagonal slot");
+        for (int r = 0; r < t.ws; ++r) {
+          const int32_t c = t.tcol[(size_t)r * t.ld + i];
+          check(c >= -(int32_t)t.glo && c < (int32_t)(t.npad + t.ghi), "virtual columns inside the vectors");
+        }
+      }
       for (const auto& h : p.peers) {
         sends += h.send_cnt;
         recvs += h.recv_cnt;

@@ -79,3 +79,24 @@ def test_wide_amg_rows_take_the_16bit_path_bitexact(monkeypatch, tail_lds):
     _setup_amg_test(g2, mesh, 1)
     g2.step()
     assert g2.amg_setup_info()[0] == 2, "without wide rows the device setup runs"
+
+
+@pytest.mark.parametrize("typed", ["1", "0"])
+def test_aligned_slot_ell_bitexact(monkeypatch, typed):
+    """Coupled-matrix ELL with aligned slots (gaps where a wall removes a
+    neighbour; Topology::tslot) and the plain positional layout
+    (CFD_TYPED_ELL=0): both give the oracle's bits (amg_test setup, Jacobi and
+    AMG preconditioners)."""
+    mesh = backwards_step()
+    monkeypatch.setenv("CFD_TYPED_ELL", typed)
+    for precond in (0, 1):
+        g = GpuSolver(mesh, config=default_config())
+        o = OracleSolver(mesh, config=default_config())
+        for s in (g, o):
+            _setup_amg_test(s, mesh, precond)
+        for k in range(3):
+            g.step()
+            o.step()
+            _assert_same_fields(g, o, f"typed={typed} precond={precond} step {k}")
+            _assert_same_info(g, o, f"typed={typed} precond={precond} step {k}")
+        g.close()
