@@ -1556,9 +1556,10 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
                                                          float* __restrict__ cx, uint32_t stride_c,
                                                          uint32_t glo, uint32_t ghi,
                                                          float* __restrict__ sm_out,
-                                                         const float* __restrict__ sm_de) {
-  const uint32_t I = row_id();
-  if (I < L.nc) {
+                                                         const float* __restrict__ sm_de, uint32_t I0,
+                                                         uint32_t I1) {
+  const uint32_t I = I0 + row_id();
+  if (I < I1) {
     float sum = 0.0f;
     if (CFD_RESTRICT_M4 && L.r_m4) {
       // the first 4 members in one 16-byte load, then their values
@@ -1598,7 +1599,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
     return;
   }
   if (sm_out) return;
-  const uint32_t g = I - L.nc;
+  const uint32_t g = I - I1;
   if (g < glo)
     cx[-1 - (int)g] = 0.0f;
   else if (g < glo + ghi)
@@ -1609,9 +1610,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
 // agg is a signed local index on a distributed level (aggregates seeded on a
 // lower rank are ghosts of xc below 0).
 __global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* __restrict__ x,
-                                                        const float* __restrict__ xc) {
-  const uint32_t i0 = 4 * row_id();
-  if (i0 >= L.n) return;
+                                                        const float* __restrict__ xc, uint32_t f0, uint32_t f1) {
+  const uint32_t i0 = f0 + 4 * row_id();
+  if (i0 >= f1) return;
   float4 xx = *reinterpret_cast<const float4*>(x + i0);
   const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;  // padding rows (>= n) get 0
@@ -2142,14 +2143,18 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
-                         uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de) {
-  const size_t n = (size_t)L.nc + (sm_out ? 0 : (size_t)glo + ghi);
+                         uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de, uint32_t I0,
+                         uint32_t I1, bool ghosts) {
+  if (I1 == 0) I1 = L.nc;
+  const size_t n = (size_t)(I1 - I0) + (sm_out || !ghosts ? 0 : (size_t)glo + ghi);
   if (n)
     hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
-                       sm_out, sm_de);
+                       sm_out, sm_de, I0, I1);
 }
-void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s) {
-  if (L.n) hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, x, xc);
+void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1) {
+  if (f1 == 0) f1 = L.n;
+  if (f1 > f0)
+    hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((f1 - f0 + 3) / 4)), dim3(kBlock), 0, s, L, x, xc, f0, f1);
 }
 void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s) {
   if (lds_bytes == 0) {

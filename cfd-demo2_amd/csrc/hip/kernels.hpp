@@ -51,7 +51,6 @@ constexpr uint32_t kMetaTSlotShift = 16;       // its slot in the coupled-matrix
 // U = min(G, 4) chunks (the first log2(U) levels of the segment tree), so a
 // segment is G / U units.
 constexpr uint32_t kRedChunkCells = 256;
-constexpr uint32_t kRedCellsPerLane = 4;
 constexpr uint32_t kRedMaxSegLog2 = 8;
 constexpr uint32_t kRedMaxSegments = 4096;  // the total's tree runs in LDS (N <= 268 M cells)
 
@@ -308,9 +307,12 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 // distributed coarse level also clears its ghosts: [-glo, 0) and [stride_c, stride_c + ghi)
 // sm_out != null: instead of clearing coarse_x, write the coarse level's
 // zero-x pre-smoother result (mix(0, (b - 0)/de, 0.8), de = sm_de) to sm_out.
+// Coarse rows [I0, I1) only (I1 = 0: all L.nc); `ghosts` false: no ghost
+// clearing (a distributed launch split around the residual halo).
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
                          uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s,
-                         float* sm_out = nullptr, const float* sm_de = nullptr);
+                         float* sm_out = nullptr, const float* sm_de = nullptr, uint32_t I0 = 0,
+                         uint32_t I1 = 0, bool ghosts = true);
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).
@@ -322,7 +324,9 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 // desc[l] describes level l (l in [first, nlev)).  lds_bytes = 4 * (vec_floats + blob_words).
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s);
-void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s);
+// fine rows [f0, f1) (multiples of 4 but f1 = L.n; f1 = 0: all)
+void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,
+                        uint32_t f1 = 0);
 // Sets the tail kernels' dynamic-LDS attribute on `device` (once per device,
 // thread-safe; throws on failure) and returns their LDS budget there:
 // min(kTailLdsMax, the device's opt-in per-block LDS).  Call with `device` current.

@@ -801,6 +801,31 @@ void Solver::build_amg_host() {
           f = (uint32_t)lf;
         }
         G.dev.nc = (uint32_t)(I1 - I0);
+        // members live on this or higher ranks, seeds on this or lower ones: the
+        // aggregates with ghost members come last, the fine rows of lower-rank
+        // aggregates first
+        const uint32_t nown = (uint32_t)(G.C1 - G.C0);
+        G.rc_hi = G.dev.nc;
+        for (uint32_t I = 0; I < G.dev.nc; ++I) {
+          bool ghost = false;
+          for (uint32_t k = r_row[I]; k < r_row[I + 1]; ++k) ghost |= r_col[k] >= nown;
+          if (ghost) {
+            G.rc_hi = I;
+            break;
+          }
+        }
+        G.pf_lo = 0;
+        if (next_dist) {
+          const uint32_t ncl = G.dev.nc;
+          for (uint32_t i = 0; i < nown; ++i)
+            if ((int32_t)agg[i] < 0 || agg[i] >= ncl) G.pf_lo = i + 1;
+          G.pf_lo = std::min((G.pf_lo + 3) & ~3u, nown);
+        }
+        const char* ov = std::getenv("CFD_AMG_HALO_OVERLAP");
+        if (ov && ov[0] == '0') {  // everything after the exchange (A/B)
+          G.rc_hi = 0;
+          G.pf_lo = nown;
+        }
       } else {
         std::copy(HL.agg.begin(), HL.agg.end(), agg.begin());
         r_row = HL.r_row;
@@ -1172,19 +1197,29 @@ void Solver::v_cycle() {
     else
       sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
     res(i);
-    // the restriction sums members owned by the next ranks too (their residuals are ghosts)
-    if (Lv.dist) halo(Lv.plan, {{Lv.r, 1}});
     AmgGpuLevel& C = levels[i + 1];
     // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
     presmoothed = fuse_presmooth && (i + 1 < down) && (!Lv.dist || C.dist);
     float* smo = presmoothed ? C.xt : nullptr;
     if (!Lv.dist) {
       launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream, smo, C.dev.de);
-    } else if (C.dist) {
-      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, C.npad, C.glo, C.ghi, stream, smo, C.dev.de);
-    } else {  // into the first replicated level: own slice, clear all, all-gather
-      launch_amg_restrict(Lv.dev, Lv.r, C.b + C.C0, C.x + C.C0, Lv.dev.nc, (uint32_t)C.C0,
-                          (uint32_t)(C.nglob - C.C1), stream);
+    } else {
+      // the restriction sums members owned by the next ranks too (their residuals
+      // are ghosts): the aggregates without such members overlap the exchange
+      const bool into_dist = C.dist;
+      float* cb = into_dist ? C.b : C.b + C.C0;
+      float* cx = into_dist ? C.x : C.x + C.C0;
+      const uint32_t sc = into_dist ? C.npad : Lv.dev.nc;
+      const uint32_t cg_lo = into_dist ? C.glo : (uint32_t)C.C0;
+      const uint32_t cg_hi = into_dist ? C.ghi : (uint32_t)(C.nglob - C.C1);
+      float* so = into_dist ? smo : nullptr;
+      const uint32_t split = Lv.dev.n >= overlap_min_rows ? Lv.rc_hi : 0u;  // as overlapped()
+      halo_begin(Lv.plan, {{Lv.r, 1}});
+      if (split > 0) launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false);
+      halo_end();
+      launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, split, Lv.dev.nc, true);
+    }
+    if (Lv.dist && !C.dist) {  // into the first replicated level: own slice, all-gather
       std::vector<size_t> off(R + 1);
       for (int q = 0; q <= R; ++q) off[q] = C.part[q] * sizeof(float);
       comm->allgatherv_inplace(C.b, off, stream);
@@ -1202,8 +1237,16 @@ void Solver::v_cycle() {
   }
   for (int ii = down - 1; ii >= 0; --ii) {
     // the prolongation reads aggregates seeded on lower ranks (ghosts of the coarse x)
-    if (levels[ii + 1].dist) halo(levels[ii + 1].plan, {{levels[ii + 1].x, 1}});
-    launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
+    if (levels[ii + 1].dist) {  // the rows of owned aggregates overlap the coarse-x exchange
+      AmgGpuLevel& F = levels[ii];
+      const uint32_t split = F.dev.n >= overlap_min_rows ? F.pf_lo : F.dev.n;  // as overlapped()
+      halo_begin(levels[ii + 1].plan, {{levels[ii + 1].x, 1}});
+      if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n);
+      halo_end();
+      if (split > 0) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, split);
+    } else {
+      launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
+    }
     sm(ii, false);
   }
   // every level performs an even number of sweeps, so level 0 ends in p_sol

@@ -175,6 +175,10 @@ struct AmgGpuLevel {
   uint32_t glo = 0, ghi = 0, npad = 0;
   // this rank's rows of the level (replicated level: restriction target range)
   uint64_t C0 = 0, C1 = 0;
+  // distributed level: its aggregates [0, rc_hi) have only owned members (their
+  // restriction overlaps the residual halo); fine rows [pf_lo, n) belong to
+  // owned aggregates (their prolongation overlaps the coarse-x halo)
+  uint32_t rc_hi = 0, pf_lo = 0;
   std::vector<uint64_t> part;  // row partition of the level over the ranks
 };
 

@@ -163,8 +163,10 @@ def test_group_amg_rebuild_interval(refresh, replicate_rows, monkeypatch):
 @pytest.mark.parametrize("nranks,which", [(2, "amg_test"), (3, "channel"), (4, "c1")])
 def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
     """The interior/boundary split that hides every halo exchange behind the
-    interior rows (Solver::overlapped; production: >= 1M rows per rank, so no
-    other test reaches it) forced on for every level with >= 64 rows."""
+    interior rows (Solver::overlapped, and the AMG restriction / prolongation
+    split around the residual / coarse-x exchanges of straddling aggregates;
+    production: >= 1M rows per rank, so no other test reaches it) forced on
+    for every level with >= 64 rows."""
     monkeypatch.setenv("CFD_OVERLAP_MIN_ROWS", "64")
     replicate_rows(50 if which != "c1" else 4096)
     if which == "c1":
