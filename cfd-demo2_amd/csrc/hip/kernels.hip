@@ -1383,6 +1383,172 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
   store12(z + 3 * (size_t)i0, o);
 }
 
+// ---- Schur predict / correct with 2 cells per thread (CFD_SCHUR_ROWS = 2) ----
+#ifndef CFD_SCHUR_ROWS
+#define CFD_SCHUR_ROWS 2
+#endif
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ f2u ld2u(const float* p) { return *reinterpret_cast<const f2u*>(p); }
+template <bool D16>
+__device__ __forceinline__ void ccols2(const CoupledMatrix& A, size_t off, uint32_t i0, int c[2]) {
+  if constexpr (D16) {
+    const short2 d = *reinterpret_cast<const short2*>(A.col16 + off);
+    c[0] = (int)i0 + (int)d.x;
+    c[1] = (int)i0 + 1 + (int)d.y;
+  } else {
+    const int2 q = *reinterpret_cast<const int2*>(A.col + off);
+    c[0] = q.x;
+    c[1] = q.y;
+  }
+}
+template <bool D16, int U>
+__device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
+                                               const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
+                                               uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
+                                               const float2 d2[2], float rhs[2]) {
+  float4 g[U];
+  int c[U][2];
+  float gd[U][2], gu[U][2], gv[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
+    g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    ccols2<D16>(A, off, i0, c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // 2 consecutive cells: 8 + 24 bytes
+    const f2u d = ld2u(dinv_uv + c[u][0]);
+    const float* b = w_in + 3 * (ptrdiff_t)c[u][0];
+    const f4u q0 = ld4u(b);
+    const f2u q1 = ld2u(b + 4);
+    gd[u][0] = d.x;
+    gd[u][1] = d.y;
+    gu[u][0] = q0.x;
+    gv[u][0] = q0.y;
+    gu[u][1] = q0.w;
+    gv[u][1] = q1.x;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (c[u][1] != c[u][0] + 1) {
+      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][1];
+      gd[u][1] = dinv_uv[c[u][1]];
+      gu[u][1] = w_in[j];
+      gv[u][1] = w_in[j + 1];
+    }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t r = r0 + u;
+      if (!lg2_on(lw[k], r)) continue;
+      const bool dg = (r == dr[k]);
+      const float gx = k ? g[u].z : g[u].x, gy = k ? g[u].w : g[u].y;
+      const float pu = dg ? d2[k].x : gx, pv = dg ? d2[k].y : gy;
+      const float ru = sc * gu[u][k], rv = sc * gv[u][k];
+      const float zu = ru * gd[u][k];
+      const float zv = rv * gd[u][k];
+      rhs[k] -= pu * zu;
+      rhs[k] -= pv * zv;
+    }
+}
+template <bool D16>
+__global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, const float* __restrict__ w_in,
+                                                             const float* __restrict__ binv, int jv,
+                                                             const float* __restrict__ dinv_uv,
+                                                             const float* __restrict__ dinv_p, float* temp_p,
+                                                             float* p_sol, float* p_prev) {
+  constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
+  uint32_t i0;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  const float sc = binv[jv];
+  const float* wb = w_in + 3 * (size_t)i0;
+  const f4u wa = ld4u(wb);
+  const f2u wc = ld2u(wb + 4);
+  float rhs[2] = {sc * wa.z, sc * wc.y};
+  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
+  const uchar2 drr = *reinterpret_cast<const uchar2*>(A.drank + i0);
+  const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
+  const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
+  const uint32_t lw[2] = {lg.x, lg.y}, dr[2] = {drr.x, drr.y};
+  const uint32_t maxlen = max(lw[0] & 0xFFu, lw[1] & 0xFFu);
+  predict2_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
+    predict2_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, lw, dr, d2, rhs);
+  const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
+  *reinterpret_cast<float2*>(temp_p + i0) = make_float2(rhs[0], rhs[1]);
+  *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
+  if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
+}
+template <bool D16, int U>
+__device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const float* __restrict__ p_sol, uint32_t i0,
+                                               uint32_t r0, uint32_t rmax, const uint32_t lw[2], float cu[2],
+                                               float cv[2]) {
+  float4 g[U];
+  int c[U][2];
+  float pj[U][2];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
+    g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    ccols2<D16>(A, off, i0, c[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const f2u q = ld2u(p_sol + c[u][0]);
+    pj[u][0] = q.x;
+    pj[u][1] = q.y;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (c[u][1] != c[u][0] + 1) pj[u][1] = p_sol[c[u][1]];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (!lg2_on(lw[k], r0 + u)) continue;
+      cu[k] += (k ? g[u].z : g[u].x) * pj[u][k];
+      cv[k] += (k ? g[u].w : g[u].y) * pj[u][k];
+    }
+}
+template <bool D16>
+__global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, const float* __restrict__ w_in,
+                                                             const float* __restrict__ binv, int jv,
+                                                             const float* __restrict__ p_sol,
+                                                             const float* __restrict__ dinv_uv,
+                                                             float* __restrict__ z) {
+  constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
+  uint32_t i0;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
+  const uint32_t lw[2] = {lg.x, lg.y};
+  const uint32_t maxlen = max(lw[0] & 0xFFu, lw[1] & 0xFFu);
+  float cu[2] = {0.0f, 0.0f}, cv[2] = {0.0f, 0.0f};
+  correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
+  const float sc = binv[jv];
+  const float* wb = w_in + 3 * (size_t)i0;
+  const f4u wa = ld4u(wb);
+  const f2u wc = ld2u(wb + 4);
+  const float wo[6] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y};
+  const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
+  const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
+  const float dk[2] = {du.x, du.y}, pk[2] = {ps.x, ps.y};
+  float o[6];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float ru = sc * wo[3 * k], rv = sc * wo[3 * k + 1];
+    const float zu = dk[k] * ru, zv = dk[k] * rv;
+    o[3 * k] = zu - dk[k] * cu[k];
+    o[3 * k + 1] = zv - dk[k] * cv[k];
+    o[3 * k + 2] = pk[k];
+  }
+  float* zo = z + 3 * (size_t)i0;
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<f4u*>(zo) = f4u{o[0], o[1], o[2], o[3]};
+  *reinterpret_cast<f2v*>(zo + 4) = f2v{o[4], o[5]};
+}
+
 // solve_triangular (gmres_logic.wgsl:78-104), single lane
 __global__ void k_solve_triangular(const float* H, const float* g, float* y, int k, int m1) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -2191,6 +2357,16 @@ void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const flo
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
+  if (CFD_SCHUR_ROWS == 2) {
+    const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
+    if (A.use16)
+      hipLaunchKernelGGL(k_precond_predict2<true>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
+                         temp_p, p_sol, p_prev);
+    else
+      hipLaunchKernelGGL(k_precond_predict2<false>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv,
+                         dinv_p, temp_p, p_sol, p_prev);
+    return;
+  }
   const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_predict<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
@@ -2209,6 +2385,15 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
+  if (CFD_SCHUR_ROWS == 2) {
+    const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
+    if (A.use16)
+      hipLaunchKernelGGL(k_precond_correct2<true>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+    else
+      hipLaunchKernelGGL(k_precond_correct2<false>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv,
+                         z);
+    return;
+  }
   const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_precond_correct<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
