@@ -128,7 +128,7 @@ def load_step_traffic(round_tag, config, world):
         return None
 
 
-def reference_workloads(max_seconds=60.0):
+def reference_workloads(max_seconds=60.0, only=None):
     """The reference's own criterion benchmarks, run under THEIR schedule
     (natural convergence: lagged FGMRES/outer tests, up to 20 Picard x 20
     restarts x 50), as extra keys beside the headline (not the headline:
@@ -179,32 +179,34 @@ def reference_workloads(max_seconds=60.0):
                 "fgmres_iterations_per_step": iters}
 
     out = {}
-    m = mesh_for(0.02)
-    s = GpuSolver(m, config=default_config())
-    s.set_dt(0.01)
-    s.set_viscosity(0.001)
-    s.set_density(1000.0)
-    s.set_alpha_p(1.0)
-    s.set_u(inlet(m))
-    r = run(s, m.num_cells(), 0, 10)
-    r["source"] = "benches/gpu_solver_benchmark.rs:6-46 (criterion sample_size 10)"
-    out["solver_step"] = r
-    s.close()
-    m = mesh_for(0.00175)
-    s = GpuSolver(m, config=default_config())
-    s.set_dt(0.001)
-    s.set_viscosity(0.001)
-    s.set_density(1.0)
-    s.set_alpha_p(0.3)
-    s.set_alpha_u(0.7)
-    s.set_scheme(0)
-    s.set_u(inlet(m))
-    s.initialize_history()
-    s.set_precond_type(1)
-    r = run(s, m.num_cells(), 1, 10)
-    r["source"] = "benches/gpu_dispatch_benchmark.rs:198-227 (criterion sample_size 10, one untimed step)"
-    out["fine_mesh"] = r
-    s.close()
+    if only in (None, "solver_step"):
+        m = mesh_for(0.02)
+        s = GpuSolver(m, config=default_config())
+        s.set_dt(0.01)
+        s.set_viscosity(0.001)
+        s.set_density(1000.0)
+        s.set_alpha_p(1.0)
+        s.set_u(inlet(m))
+        r = run(s, m.num_cells(), 0, 10)
+        r["source"] = "benches/gpu_solver_benchmark.rs:6-46 (criterion sample_size 10)"
+        out["solver_step"] = r
+        s.close()
+    if only in (None, "fine_mesh"):
+        m = mesh_for(0.00175)
+        s = GpuSolver(m, config=default_config())
+        s.set_dt(0.001)
+        s.set_viscosity(0.001)
+        s.set_density(1.0)
+        s.set_alpha_p(0.3)
+        s.set_alpha_u(0.7)
+        s.set_scheme(0)
+        s.set_u(inlet(m))
+        s.initialize_history()
+        s.set_precond_type(1)
+        r = run(s, m.num_cells(), 1, 10)
+        r["source"] = "benches/gpu_dispatch_benchmark.rs:198-227 (criterion sample_size 10, one untimed step)"
+        out["fine_mesh"] = r
+        s.close()
     return out
 
 

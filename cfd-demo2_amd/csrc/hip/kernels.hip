@@ -1301,6 +1301,86 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
   p_prev[i] = wmix(p_prev[i], hat_x, 1.2f);
 }
 
+// Every relax_pressure sweep of one preconditioner application in ONE
+// workgroup (small meshes, N <= 8192): the p_iters launches of k_relax_pressure
+// (64 at the reference's 8 k-cell benchmark mesh, each a ~4.6 us launch for a
+// few microseconds of work) become one kernel.  Thread t owns rows t + 1024 k;
+// its rows' off-diagonal ELL entries (slot order kept, diagonal and padding
+// masked out), temp_p and dinv_p live in registers for all sweeps, the two
+// ping-pong iterates in LDS.  Sweep s reads the iterate written by sweep s-1
+// (P for even s, T for odd) and writes the other buffer, exactly the launch
+// sequence's src/dst alternation, so one barrier per sweep orders it.  Same
+// f32 operations in the same order as k_relax_pressure: bit-identical.
+constexpr int kRelaxThreads = 1024;
+constexpr uint32_t kRelaxNoCol = 0xFFFFu;  // masked slot (diagonal or padding); N <= 8192 < 0xFFFF
+template <int RPT, int WS>
+__global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t N, uint32_t ld,
+                                                                      const int32_t* __restrict__ col,
+                                                                      const uint32_t* __restrict__ len,
+                                                                      const float* __restrict__ sval,
+                                                                      const float* __restrict__ dinv_p,
+                                                                      const float* __restrict__ temp_p,
+                                                                      float* p_sol, float* temp, uint32_t iters) {
+  extern __shared__ float relax_lds[];
+  float* P = relax_lds;      // p_sol iterate
+  float* T = relax_lds + N;  // temp iterate
+  const uint32_t t = threadIdx.x;
+  float dv[RPT], tp[RPT], v[RPT][WS];
+  uint32_t cp[RPT][(WS + 1) / 2];  // two 16-bit columns per register, kRelaxNoCol = masked
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const uint32_t i = t + (uint32_t)k * kRelaxThreads;
+    dv[k] = tp[k] = 0.0f;
+#pragma unroll
+    for (int r = 0; r < WS; ++r) v[k][r] = 0.0f;
+#pragma unroll
+    for (int q = 0; q < (WS + 1) / 2; ++q) cp[k][q] = 0xFFFFFFFFu;
+    if (i < N) {
+      P[i] = p_sol[i];
+      T[i] = temp[i];
+      dv[k] = dinv_p[i];
+      tp[k] = temp_p[i];
+      const uint32_t l = len[i];
+#pragma unroll
+      for (int r = 0; r < WS; ++r) {
+        if ((uint32_t)r < l) {
+          const size_t slot = (size_t)r * ld + i;
+          const int32_t cc = col[slot];
+          v[k][r] = sval[slot];
+          if (cc != (int32_t)i) cp[k][r / 2] &= ~(0xFFFFu << (16 * (r & 1))) | ((uint32_t)cc << (16 * (r & 1)));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t s = 0; s < iters; ++s) {
+    const float* src = (s & 1u) ? T : P;
+    float* dst = (s & 1u) ? P : T;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint32_t i = t + (uint32_t)k * kRelaxThreads;
+      if (i >= N) continue;
+      float sigma = 0.0f;
+#pragma unroll
+      for (int r = 0; r < WS; ++r) {
+        const uint32_t c = (cp[k][r / 2] >> (16 * (r & 1))) & 0xFFFFu;
+        if (c != kRelaxNoCol) sigma += v[k][r] * src[c];
+      }
+      const float hat_x = dv[k] * (tp[k] - sigma);
+      dst[i] = wmix(dst[i], hat_x, 1.2f);  // own row: only this thread touches dst[i] in this sweep
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const uint32_t i = t + (uint32_t)k * kRelaxThreads;
+    if (i < N) {
+      p_sol[i] = P[i];
+      temp[i] = T[i];
+    }
+  }
+}
+
 // correct_velocity (schur_precond.wgsl:93-139) fused with the velocity
 // prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol);
 // 4 cells per thread.
@@ -2381,6 +2461,25 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
   if (N)
     hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, ld, col, len, sval, dinv_p,
                        temp_p, p_sol, p_prev);
+}
+bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int32_t* col, const uint32_t* len,
+                                 const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
+                                 float* temp, uint32_t iters, hipStream_t s) {
+  if (N == 0 || N > kRelaxFusedMaxRows || iters == 0) return false;
+  const size_t lds = 2 * (size_t)N * sizeof(float);
+  const dim3 g(1), b(kRelaxThreads);
+#define CFD_RELAX_FUSED_CASE(RPT, WS)                                                                         \
+  if (N <= (uint32_t)(RPT) * kRelaxThreads && ws <= (uint32_t)(WS)) {                                         \
+    hipLaunchKernelGGL((k_relax_pressure_fused<RPT, WS>), g, b, lds, s, N, ld, col, len, sval, dinv_p, temp_p, \
+                       p_sol, temp, iters);                                                                   \
+    return true;                                                                                              \
+  }
+  CFD_RELAX_FUSED_CASE(1, 16)
+  CFD_RELAX_FUSED_CASE(2, 16)
+  CFD_RELAX_FUSED_CASE(4, 12)
+  CFD_RELAX_FUSED_CASE(8, 6)
+#undef CFD_RELAX_FUSED_CASE
+  return false;
 }
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {

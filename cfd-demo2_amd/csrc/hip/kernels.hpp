@@ -290,6 +290,13 @@ void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const flo
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
+// all `iters` relax_pressure sweeps in one single-workgroup launch (p_sol / temp
+// ping-pong as the per-sweep launches, the final iterates back in both); false
+// when N > kRelaxFusedMaxRows or the ELL width is too wide for the register image
+constexpr uint32_t kRelaxFusedMaxRows = 8192;
+bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int32_t* col, const uint32_t* len,
+                                 const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
+                                 float* temp, uint32_t iters, hipStream_t s);
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s);
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,

@@ -84,6 +84,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
     const char* cs = std::getenv("CFD_CHECK_SYNC");
     check_sync = cs && cs[0] == '1';
   }
+  if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -1282,12 +1283,19 @@ void Solver::precondition(int j, float* z) {
     // p_iters of coupled_solver_fgmres.rs:1949-1976 (global cell count)
     const size_t raw = 20u + (size_t)std::sqrt((float)NG) / 2u;
     const size_t p_iters = std::min<size_t>(raw, 200) == 0 ? 0 : std::min<size_t>(raw, 200) - 1;
-    for (size_t it = 0; it < p_iters; ++it) {
-      float* src = in_sol ? p_sol : temp;
-      float* dst = in_sol ? temp : p_sol;
-      if (dist()) halo(cell_plan, {{src, 1}});
-      launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
-      in_sol = !in_sol;
+    // small meshes: every sweep in one single-workgroup launch (same bits)
+    if (!dist() && relax_fused &&
+        launch_relax_pressure_fused(N, topo.ld, (uint32_t)topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, p_sol, temp,
+                                    (uint32_t)p_iters, stream)) {
+      if (p_iters & 1) in_sol = false;
+    } else {
+      for (size_t it = 0; it < p_iters; ++it) {
+        float* src = in_sol ? p_sol : temp;
+        float* dst = in_sol ? temp : p_sol;
+        if (dist()) halo(cell_plan, {{src, 1}});
+        launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
+        in_sol = !in_sol;
+      }
     }
   }
   float* ps = in_sol ? p_sol : temp;

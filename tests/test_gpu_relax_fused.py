@@ -1,0 +1,95 @@
+"""Jacobi-path Schur preconditioner on small meshes: all p_iters relax_pressure
+sweeps (schur_precond.wgsl:52-90, coupled_solver_fgmres.rs:1949-1976) run in
+one single-workgroup launch (k_relax_pressure_fused) instead of one launch per
+sweep.  Each case below selects one (rows per thread, ELL width) instantiation
+and an odd or even sweep count; fused GPU == per-sweep GPU == oracle, bit-exact."""
+import numpy as np
+import pytest
+
+from cfd2_amd import GpuSolver, default_config
+from cfd2_amd.mesh import ChannelWithObstacle, generate_voronoi_mesh
+from tests.meshes import backwards_step
+from tests.oracle_py import OracleSolver
+from tests.test_gpu_parity import _assert_same_fields, _assert_same_info, _setup_amg_test
+
+pytestmark = pytest.mark.gpu
+
+NONE = 0xFFFFFFFF
+CHANNEL = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.5), obstacle_radius=0.2)
+
+
+def _mesh(name):
+    if name.startswith("voronoi"):
+        h = float(name.split("_")[1])
+        return generate_voronoi_mesh(CHANNEL, h, 2 * h, 1.2, (3.0, 1.0), seed=1)
+    return backwards_step(float(name.split("_")[1]))
+
+
+def _shape(mesh):
+    """(cells, ELL width incl. the diagonal, sweeps per preconditioner application)."""
+    a = mesh.arrays()
+    n = mesh.num_cells()
+    nb = np.asarray(a["face_neighbor"]).astype(np.int64)
+    ow = np.asarray(a["face_owner"]).astype(np.int64)
+    inner = nb != NONE
+    cnt = np.bincount(ow[inner], minlength=n) + np.bincount(nb[inner], minlength=n)
+    raw = 20 + int(np.sqrt(np.float32(n))) // 2
+    return n, int(cnt.max()) + 1, min(raw, 200) - 1
+
+
+# (mesh, rows per thread, ELL width bound of the instantiation it must select)
+CASES = [
+    ("voronoi_0.03", 1, 16),   # 908 cells, width 10, 34 sweeps
+    ("step_0.05", 2, 16),      # 1,300 cells (amg_test.rs mesh), width 5, 37 sweeps
+    ("voronoi_0.015", 4, 12),  # 2,813 cells, width 10, 45 sweeps
+    ("step_0.03", 4, 12),      # 3,722 cells, width 5, 49 sweeps
+    ("step_0.02", 8, 6),       # 8,125 cells: gpu_solver_benchmark.rs's mesh, 64 sweeps
+]
+
+
+@pytest.mark.parametrize("name,rpt,wmax", CASES, ids=[c[0] for c in CASES])
+def test_relax_fused_parity(name, rpt, wmax, monkeypatch):
+    mesh = _mesh(name)
+    n, ws, sweeps = _shape(mesh)
+    # the case must exercise the instantiation it names (launch_relax_pressure_fused)
+    assert n <= rpt * 1024 and (rpt == 1 or n > rpt // 2 * 1024) and ws <= wmax, (n, ws)
+    cfg = dict(fixed_outer=3, fixed_inner=12)
+    fused = GpuSolver(mesh, config=default_config(**cfg))
+    monkeypatch.setenv("CFD_RELAX_FUSED", "0")
+    per_sweep = GpuSolver(mesh, config=default_config(**cfg))
+    monkeypatch.delenv("CFD_RELAX_FUSED")
+    o = OracleSolver(mesh, config=default_config(**cfg))
+    for s in (fused, per_sweep, o):
+        _setup_amg_test(s, mesh, 0)
+    for k in range(2):
+        for s in (fused, per_sweep, o):
+            s.step()
+        ctx = f"{name} ({n} cells, width {ws}, {sweeps} sweeps) step {k}"
+        _assert_same_fields(fused, o, "fused " + ctx)
+        _assert_same_info(fused, o, "fused " + ctx)
+        _assert_same_fields(per_sweep, o, "per-sweep " + ctx)
+    for s in (fused, per_sweep):
+        s.close()
+
+
+def test_relax_fused_reference_benchmark_natural():
+    """benches/gpu_solver_benchmark.rs:6-46 (water, BackwardsStep h = 0.02,
+    Jacobi, natural convergence): three steps, fused GPU == oracle bit-exact."""
+    mesh = backwards_step(0.02)
+    a = mesh.arrays()
+    u = np.zeros((mesh.num_cells(), 2))
+    u[(np.asarray(a["cell_cx"]) < 0.05) & (np.asarray(a["cell_cy"]) > 0.5), 0] = 1.0
+    g = GpuSolver(mesh, config=default_config())
+    o = OracleSolver(mesh, config=default_config())
+    for s in (g, o):
+        s.set_dt(0.01)
+        s.set_viscosity(0.001)
+        s.set_density(1000.0)
+        s.set_alpha_p(1.0)
+        s.set_u(u)
+    for k in range(3):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"solver benchmark step {k}")
+        _assert_same_info(g, o, f"solver benchmark step {k}")
+    g.close()
