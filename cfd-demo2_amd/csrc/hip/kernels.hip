@@ -1302,17 +1302,22 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 }
 
 // Every relax_pressure sweep of one preconditioner application in ONE
-// workgroup (small meshes, N <= 8192): the p_iters launches of k_relax_pressure
+// workgroup (small meshes, N < 8192): the p_iters launches of k_relax_pressure
 // (64 at the reference's 8 k-cell benchmark mesh, each a ~4.6 us launch for a
 // few microseconds of work) become one kernel.  Thread t owns rows t + 1024 k;
-// its rows' off-diagonal ELL entries (slot order kept, diagonal and padding
-// masked out), temp_p and dinv_p live in registers for all sweeps, the two
-// ping-pong iterates in LDS.  Sweep s reads the iterate written by sweep s-1
-// (P for even s, T for odd) and writes the other buffer, exactly the launch
-// sequence's src/dst alternation, so one barrier per sweep orders it.  Same
-// f32 operations in the same order as k_relax_pressure: bit-identical.
+// its rows' ELL entries (values + 16-bit LDS byte addresses of their columns,
+// two per register, slot order kept), temp_p and dinv_p live in registers for all sweeps; the two
+// ping-pong iterates live in LDS (P = p_sol at byte 0, T = temp at byte
+// 32768: a sweep's source buffer is an immediate offset; unit-stride rows keep
+// the neighbour reads free of bank conflicts).  Sweep s
+// reads the iterate written by sweep s-1 (P for even s, T for odd) and writes
+// the other buffer, exactly the launch sequence's src/dst alternation; one
+// barrier per sweep orders it.  The diagonal and the ELL padding point at a
+// zero row with value +0: they add +0 * +0 = +0 to sigma, which starts at +0
+// and so is never -0 (a round-to-nearest sum is -0 only if both operands are),
+// hence sigma + +0 == sigma bit for bit -- the same f32 result as skipping them
+// in k_relax_pressure, without a compare and select per slot.
 constexpr int kRelaxThreads = 1024;
-constexpr uint32_t kRelaxNoCol = 0xFFFFu;  // masked slot (diagonal or padding); N <= 8192 < 0xFFFF
 template <int RPT, int WS>
 __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t N, uint32_t ld,
                                                                       const int32_t* __restrict__ col,
@@ -1321,12 +1326,14 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
                                                                       const float* __restrict__ dinv_p,
                                                                       const float* __restrict__ temp_p,
                                                                       float* p_sol, float* temp, uint32_t iters) {
-  extern __shared__ float relax_lds[];
-  float* P = relax_lds;      // p_sol iterate
-  float* T = relax_lds + N;  // temp iterate
+  extern __shared__ float relax_lds[];  // P [0, 8192), T [8192, 16384); row N of each = +0
+  char* base = reinterpret_cast<char*>(relax_lds);
+  constexpr uint32_t kT = 4u * kRelaxFusedMaxRows + 4u;  // byte offset of T (32768)
   const uint32_t t = threadIdx.x;
   float dv[RPT], tp[RPT], v[RPT][WS];
-  uint32_t cp[RPT][(WS + 1) / 2];  // two 16-bit columns per register, kRelaxNoCol = masked
+  uint32_t ad[RPT][(WS + 1) / 2];  // 16-bit byte addresses, slot r in half r & 1
+  const uint32_t zero_row = 4u * N;  // <= 32764
+  const uint32_t zero_pair = zero_row | (zero_row << 16);
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
@@ -1334,10 +1341,10 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
 #pragma unroll
     for (int r = 0; r < WS; ++r) v[k][r] = 0.0f;
 #pragma unroll
-    for (int q = 0; q < (WS + 1) / 2; ++q) cp[k][q] = 0xFFFFFFFFu;
+    for (int q = 0; q < (WS + 1) / 2; ++q) ad[k][q] = zero_pair;
     if (i < N) {
-      P[i] = p_sol[i];
-      T[i] = temp[i];
+      relax_lds[i] = p_sol[i];
+      relax_lds[kT / 4 + i] = temp[i];
       dv[k] = dinv_p[i];
       tp[k] = temp_p[i];
       const uint32_t l = len[i];
@@ -1346,37 +1353,55 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
         if ((uint32_t)r < l) {
           const size_t slot = (size_t)r * ld + i;
           const int32_t cc = col[slot];
-          v[k][r] = sval[slot];
-          if (cc != (int32_t)i) cp[k][r / 2] &= ~(0xFFFFu << (16 * (r & 1))) | ((uint32_t)cc << (16 * (r & 1)));
+          if (cc != (int32_t)i) {
+            v[k][r] = sval[slot];
+            const uint32_t sh = 16u * (r & 1);
+            ad[k][r / 2] = (ad[k][r / 2] & ~(0xFFFFu << sh)) | ((4u * (uint32_t)cc) << sh);
+          }
         }
       }
     }
   }
+  if (t == 0) relax_lds[N] = relax_lds[kT / 4 + N] = 0.0f;
   __syncthreads();
-  for (uint32_t s = 0; s < iters; ++s) {
-    const float* src = (s & 1u) ? T : P;
-    float* dst = (s & 1u) ? P : T;
+  // SRC = byte offset of the source iterate (0: P, kT: T)
+  auto sweep = [&](auto src_off) {
+    constexpr uint32_t SRC = decltype(src_off)::value, DST = kT - SRC;
+    // keep the packed addresses packed: without this the compiler hoists the
+    // loop-invariant 16-bit extractions out of the sweep loop and spills
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+      for (int q = 0; q < (WS + 1) / 2; ++q) asm volatile("" : "+v"(ad[k][q]));
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const uint32_t i = t + (uint32_t)k * kRelaxThreads;
-      if (i >= N) continue;
+      // rows past N compute on the zero row: +0 slots, dv = tp = +0, so they
+      // write mix(+0, +0, 1.2) = +0 back into it (branch-free sweep)
+      const uint32_t i = min(t + (uint32_t)k * kRelaxThreads, N);
       float sigma = 0.0f;
 #pragma unroll
       for (int r = 0; r < WS; ++r) {
-        const uint32_t c = (cp[k][r / 2] >> (16 * (r & 1))) & 0xFFFFu;
-        if (c != kRelaxNoCol) sigma += v[k][r] * src[c];
+        const uint32_t a = (r & 1) ? (ad[k][r / 2] >> 16) : (ad[k][r / 2] & 0xFFFFu);
+        sigma += v[k][r] * *reinterpret_cast<const float*>(base + a + SRC);
       }
       const float hat_x = dv[k] * (tp[k] - sigma);
-      dst[i] = wmix(dst[i], hat_x, 1.2f);  // own row: only this thread touches dst[i] in this sweep
+      float* d = reinterpret_cast<float*>(base + 4u * i + DST);
+      *d = wmix(*d, hat_x, 1.2f);  // own row: only this thread touches it in this sweep
     }
     __syncthreads();
+  };
+  uint32_t s = 0;
+  for (; s + 1 < iters; s += 2) {
+    sweep(std::integral_constant<uint32_t, 0u>{});
+    sweep(std::integral_constant<uint32_t, kT>{});
   }
+  if (s < iters) sweep(std::integral_constant<uint32_t, 0u>{});
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
     if (i < N) {
-      p_sol[i] = P[i];
-      temp[i] = T[i];
+      p_sol[i] = relax_lds[i];
+      temp[i] = relax_lds[kT / 4 + i];
     }
   }
 }
@@ -2466,7 +2491,7 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
                                  const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
                                  float* temp, uint32_t iters, hipStream_t s) {
   if (N == 0 || N > kRelaxFusedMaxRows || iters == 0) return false;
-  const size_t lds = 2 * (size_t)N * sizeof(float);
+  const size_t lds = 2 * ((size_t)kRelaxFusedMaxRows + 1) * sizeof(float);  // 64 KiB
   const dim3 g(1), b(kRelaxThreads);
 #define CFD_RELAX_FUSED_CASE(RPT, WS)                                                                         \
   if (N <= (uint32_t)(RPT) * kRelaxThreads && ws <= (uint32_t)(WS)) {                                         \
@@ -2477,6 +2502,7 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
   CFD_RELAX_FUSED_CASE(1, 16)
   CFD_RELAX_FUSED_CASE(2, 16)
   CFD_RELAX_FUSED_CASE(4, 12)
+  CFD_RELAX_FUSED_CASE(8, 5)
   CFD_RELAX_FUSED_CASE(8, 6)
 #undef CFD_RELAX_FUSED_CASE
   return false;

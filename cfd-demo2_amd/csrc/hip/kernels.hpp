@@ -293,7 +293,7 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
 // all `iters` relax_pressure sweeps in one single-workgroup launch (p_sol / temp
 // ping-pong as the per-sweep launches, the final iterates back in both); false
 // when N > kRelaxFusedMaxRows or the ELL width is too wide for the register image
-constexpr uint32_t kRelaxFusedMaxRows = 8192;
+constexpr uint32_t kRelaxFusedMaxRows = 8191;  // two (N + 1)-float iterates in 64 KiB of LDS
 bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int32_t* col, const uint32_t* len,
                                  const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
                                  float* temp, uint32_t iters, hipStream_t s);
