@@ -1305,20 +1305,21 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 // workgroup (small meshes, N < 8192): the p_iters launches of k_relax_pressure
 // (64 at the reference's 8 k-cell benchmark mesh, each a ~4.6 us launch for a
 // few microseconds of work) become one kernel.  Thread t owns rows t + 1024 k;
-// its rows' ELL entries (values + 16-bit LDS byte addresses of their columns,
-// two per register, slot order kept), temp_p and dinv_p live in registers for all sweeps; the two
-// ping-pong iterates live in LDS (P = p_sol at byte 0, T = temp at byte
+// its rows' off-diagonal entries (values + LDS byte addresses of their
+// columns, compacted in slot order: the diagonal is skipped as in
+// k_relax_pressure), temp_p and dinv_p live in registers for all sweeps; the
+// two ping-pong iterates live in LDS (P = p_sol at byte 0, T = temp at byte
 // 32768: a sweep's source buffer is an immediate offset; unit-stride rows keep
-// the neighbour reads free of bank conflicts).  Sweep s
-// reads the iterate written by sweep s-1 (P for even s, T for odd) and writes
-// the other buffer, exactly the launch sequence's src/dst alternation; one
-// barrier per sweep orders it.  The diagonal and the ELL padding point at a
-// zero row with value +0: they add +0 * +0 = +0 to sigma, which starts at +0
-// and so is never -0 (a round-to-nearest sum is -0 only if both operands are),
-// hence sigma + +0 == sigma bit for bit -- the same f32 result as skipping them
-// in k_relax_pressure, without a compare and select per slot.
+// the neighbour reads free of bank conflicts).  Sweep s reads the iterate
+// written by sweep s-1 (P for even s, T for odd) and writes the other buffer,
+// exactly the launch sequence's src/dst alternation; one barrier per sweep
+// orders it.  Unused entries point at a zero row with value +0: they add
+// +0 * +0 = +0 to sigma, which starts at +0 and so is never -0 (a
+// round-to-nearest sum is -0 only if both operands are), hence sigma + +0 ==
+// sigma bit for bit -- the f32 result of k_relax_pressure, without a compare
+// and select per entry.
 constexpr int kRelaxThreads = 1024;
-template <int RPT, int WS>
+template <int RPT, int OD>
 __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t N, uint32_t ld,
                                                                       const int32_t* __restrict__ col,
                                                                       const uint32_t* __restrict__ len,
@@ -1330,33 +1331,38 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   char* base = reinterpret_cast<char*>(relax_lds);
   constexpr uint32_t kT = 4u * kRelaxFusedMaxRows + 4u;  // byte offset of T (32768)
   const uint32_t t = threadIdx.x;
-  float dv[RPT], tp[RPT], v[RPT][WS];
-  uint32_t ad[RPT][(WS + 1) / 2];  // 16-bit byte addresses, slot r in half r & 1
-  const uint32_t zero_row = 4u * N;  // <= 32764
-  const uint32_t zero_pair = zero_row | (zero_row << 16);
+  float dv[RPT], tp[RPT], v[RPT][OD];
+  uint32_t ad[RPT][OD];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
     dv[k] = tp[k] = 0.0f;
 #pragma unroll
-    for (int r = 0; r < WS; ++r) v[k][r] = 0.0f;
-#pragma unroll
-    for (int q = 0; q < (WS + 1) / 2; ++q) ad[k][q] = zero_pair;
+    for (int e = 0; e < OD; ++e) {
+      v[k][e] = 0.0f;
+      ad[k][e] = 4u * N;  // the zero row
+    }
     if (i < N) {
       relax_lds[i] = p_sol[i];
       relax_lds[kT / 4 + i] = temp[i];
       dv[k] = dinv_p[i];
       tp[k] = temp_p[i];
       const uint32_t l = len[i];
+      int e = 0;
 #pragma unroll
-      for (int r = 0; r < WS; ++r) {
+      for (int r = 0; r <= OD; ++r) {  // <= OD off-diagonals + the diagonal
         if ((uint32_t)r < l) {
           const size_t slot = (size_t)r * ld + i;
           const int32_t cc = col[slot];
           if (cc != (int32_t)i) {
-            v[k][r] = sval[slot];
-            const uint32_t sh = 16u * (r & 1);
-            ad[k][r / 2] = (ad[k][r / 2] & ~(0xFFFFu << sh)) | ((4u * (uint32_t)cc) << sh);
+            // e only ever increases by one: a static select chain keeps v / ad in registers
+#pragma unroll
+            for (int q = 0; q < OD; ++q)
+              if (q == e) {
+                v[k][q] = sval[slot];
+                ad[k][q] = 4u * (uint32_t)cc;
+              }
+            ++e;
           }
         }
       }
@@ -1367,23 +1373,14 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   // SRC = byte offset of the source iterate (0: P, kT: T)
   auto sweep = [&](auto src_off) {
     constexpr uint32_t SRC = decltype(src_off)::value, DST = kT - SRC;
-    // keep the packed addresses packed: without this the compiler hoists the
-    // loop-invariant 16-bit extractions out of the sweep loop and spills
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-#pragma unroll
-      for (int q = 0; q < (WS + 1) / 2; ++q) asm volatile("" : "+v"(ad[k][q]));
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      // rows past N compute on the zero row: +0 slots, dv = tp = +0, so they
+      // rows past N compute on the zero row: +0 entries, dv = tp = +0, so they
       // write mix(+0, +0, 1.2) = +0 back into it (branch-free sweep)
       const uint32_t i = min(t + (uint32_t)k * kRelaxThreads, N);
       float sigma = 0.0f;
 #pragma unroll
-      for (int r = 0; r < WS; ++r) {
-        const uint32_t a = (r & 1) ? (ad[k][r / 2] >> 16) : (ad[k][r / 2] & 0xFFFFu);
-        sigma += v[k][r] * *reinterpret_cast<const float*>(base + a + SRC);
-      }
+      for (int e = 0; e < OD; ++e) sigma += v[k][e] * *reinterpret_cast<const float*>(base + ad[k][e] + SRC);
       const float hat_x = dv[k] * (tp[k] - sigma);
       float* d = reinterpret_cast<float*>(base + 4u * i + DST);
       *d = wmix(*d, hat_x, 1.2f);  // own row: only this thread touches it in this sweep
@@ -2493,17 +2490,17 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
   if (N == 0 || N > kRelaxFusedMaxRows || iters == 0) return false;
   const size_t lds = 2 * ((size_t)kRelaxFusedMaxRows + 1) * sizeof(float);  // 64 KiB
   const dim3 g(1), b(kRelaxThreads);
-#define CFD_RELAX_FUSED_CASE(RPT, WS)                                                                         \
-  if (N <= (uint32_t)(RPT) * kRelaxThreads && ws <= (uint32_t)(WS)) {                                         \
-    hipLaunchKernelGGL((k_relax_pressure_fused<RPT, WS>), g, b, lds, s, N, ld, col, len, sval, dinv_p, temp_p, \
+  // ws = widest row incl. the diagonal: at most ws - 1 off-diagonal entries per row
+#define CFD_RELAX_FUSED_CASE(RPT, OD)                                                                         \
+  if (N <= (uint32_t)(RPT) * kRelaxThreads && ws <= (uint32_t)(OD) + 1u) {                                    \
+    hipLaunchKernelGGL((k_relax_pressure_fused<RPT, OD>), g, b, lds, s, N, ld, col, len, sval, dinv_p, temp_p, \
                        p_sol, temp, iters);                                                                   \
     return true;                                                                                              \
   }
-  CFD_RELAX_FUSED_CASE(1, 16)
-  CFD_RELAX_FUSED_CASE(2, 16)
-  CFD_RELAX_FUSED_CASE(4, 12)
-  CFD_RELAX_FUSED_CASE(8, 5)
-  CFD_RELAX_FUSED_CASE(8, 6)
+  CFD_RELAX_FUSED_CASE(1, 15)  // register budget at 1024 threads: 128 VGPRs, no spills
+  CFD_RELAX_FUSED_CASE(2, 15)
+  CFD_RELAX_FUSED_CASE(4, 9)
+  CFD_RELAX_FUSED_CASE(8, 4)
 #undef CFD_RELAX_FUSED_CASE
   return false;
 }

@@ -37,13 +37,13 @@ def _shape(mesh):
     return n, int(cnt.max()) + 1, min(raw, 200) - 1
 
 
-# (mesh, rows per thread, ELL width bound of the instantiation it must select)
+# (mesh, rows per thread, ELL width bound (off-diagonals + 1) of the instantiation it must select)
 CASES = [
     ("voronoi_0.03", 1, 16),   # 908 cells, width 10, 34 sweeps
     ("step_0.05", 2, 16),      # 1,300 cells (amg_test.rs mesh), width 5, 37 sweeps
-    ("voronoi_0.015", 4, 12),  # 2,813 cells, width 10, 45 sweeps
-    ("step_0.03", 4, 12),      # 3,722 cells, width 5, 49 sweeps
-    ("step_0.02", 8, 6),       # 8,125 cells: gpu_solver_benchmark.rs's mesh, 64 sweeps
+    ("voronoi_0.015", 4, 10),  # 2,813 cells, width 10, 45 sweeps
+    ("step_0.03", 4, 10),      # 3,722 cells, width 5, 49 sweeps
+    ("step_0.02", 8, 5),       # 8,125 cells: gpu_solver_benchmark.rs's mesh, 64 sweeps
 ]
 
 
