@@ -285,6 +285,15 @@ def main():
         shared = os.path.join(base, f"cfd2_bench_mesh_{os.environ.get('MASTER_PORT', '0')}_{args.config}_{world}.bin")
         ok = [True]
         if rank == 0:
+            import atexit
+
+            def _drop_shared(path=shared):  # a failed run must not leave GBs in /dev/shm
+                for junk in (path, path + ".tmp"):
+                    try:
+                        os.unlink(junk)
+                    except OSError:
+                        pass
+            atexit.register(_drop_shared)
             m0 = make_mesh()
             try:
                 save_view_file(m0, shared)
@@ -330,7 +339,7 @@ def main():
     setup_solver(solver)
     if shared is not None:
         dist.barrier()  # every rank has built its slab: the shared file can go
-        if rank == 0:
+        if rank == 0 and os.path.exists(shared):
             os.unlink(shared)
     if world > 1 or args.inproc_ranks > 1:
         del mesh  # the solver keeps what it needs; free the global mesh
