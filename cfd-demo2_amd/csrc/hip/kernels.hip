@@ -1908,6 +1908,47 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
   *reinterpret_cast<float4*>(rr + i0) = o;
 }
 
+// relax_pressure (schur_precond.wgsl:52-90) on large meshes, 4 rows per thread
+// over the scalar ELL image (16-bit column deltas, u8 lengths / diagonal ranks,
+// the AMG row kernels' slot groups and vector gathers): the diagonal sits in
+// the slots and is skipped by its rank, every other entry is summed in slot
+// order -- k_relax_pressure's f32 operations, row for row.
+template <bool D16>
+__global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const uint8_t* __restrict__ drank,
+                                                            const float* __restrict__ dinv_p,
+                                                            const float* __restrict__ temp_p,
+                                                            const float* __restrict__ src, float* dst) {
+  uint32_t i0;
+  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
+  const uchar4 dr = *reinterpret_cast<const uchar4*>(drank + i0);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto step = [&](uint32_t r0, uint32_t rmax) {
+    float4 v[kU];
+    float xg[kU][4];
+    gather_group<D16, 1, true>(L, src, i0, r0, rmax, ln, v, xg);
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t r = r0 + u;
+        if (r < u4(ln, k) && r != u4(dr, k)) sg[k] += f4(v[u], k) * xg[u][k];
+      }
+  };
+  step(0, (uint32_t)max(L.w, 1) - 1u);  // peeled first group: its loads do not wait for the lengths
+  for (uint32_t r0 = kU; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
+  const float4 dp = *reinterpret_cast<const float4*>(dinv_p + i0);
+  const float4 tp = *reinterpret_cast<const float4*>(temp_p + i0);
+  const float4 old = *reinterpret_cast<const float4*>(dst + i0);
+  const float d[4] = {dp.x, dp.y, dp.z, dp.w}, b[4] = {tp.x, tp.y, tp.z, tp.w}, o[4] = {old.x, old.y, old.z, old.w};
+  float y[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)  // padding rows (i >= n) keep their value
+    y[k] = (i0 + k < L.n) ? wmix(o[k], d[k] * (b[k] - sg[k]), 1.2f) : o[k];
+  *reinterpret_cast<float4*>(dst + i0) = make_float4(y[0], y[1], y[2], y[3]);
+}
+
 #ifndef CFD_RESTRICT_M4
 #define CFD_RESTRICT_M4 1
 #endif
@@ -2483,6 +2524,15 @@ void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const ui
   if (N)
     hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, ld, col, len, sval, dinv_p,
                        temp_p, p_sol, p_prev);
+}
+void launch_relax_pressure4(const AmgLevelDev& L, const uint8_t* drank, const float* dinv_p, const float* temp_p,
+                            const float* src, float* dst, hipStream_t s) {
+  if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
+  const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
+  if (L.use16)
+    hipLaunchKernelGGL(k_relax_pressure4<true>, dim3(nb), dim3(kBlock), 0, s, L, drank, dinv_p, temp_p, src, dst);
+  else
+    hipLaunchKernelGGL(k_relax_pressure4<false>, dim3(nb), dim3(kBlock), 0, s, L, drank, dinv_p, temp_p, src, dst);
 }
 bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int32_t* col, const uint32_t* len,
                                  const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,

@@ -290,6 +290,11 @@ void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const flo
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
+// one relax_pressure sweep, 4 rows per thread over the scalar ELL image viewed as
+// an AmgLevelDev (val = the live scalar matrix, len / col16 / col32 incl. the
+// diagonal, skipped by `drank`); rows [L.r0, L.r1) + [L.r2, L.r3)
+void launch_relax_pressure4(const AmgLevelDev& L, const uint8_t* drank, const float* dinv_p, const float* temp_p,
+                            const float* src, float* dst, hipStream_t s);
 // all `iters` relax_pressure sweeps in one single-workgroup launch (p_sol / temp
 // ping-pong as the per-sweep launches, the final iterates back in both); false
 // when N > kRelaxFusedMaxRows or the ELL width is too wide for the register image

@@ -85,6 +85,8 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
     check_sync = cs && cs[0] == '1';
   }
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
+  if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
+  if (topo.ws > 255) relax4 = false;  // u8 row lengths
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -1293,7 +1295,22 @@ void Solver::precondition(int j, float* z) {
         float* src = in_sol ? p_sol : temp;
         float* dst = in_sol ? temp : p_sol;
         if (dist()) halo(cell_plan, {{src, 1}});
-        launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
+        if (relax4) {
+          AmgLevelDev rv{};  // the scalar ELL image (diagonal in the slots) as a row-kernel level
+          rv.n = N;
+          rv.r1 = N;
+          rv.stride = topo.ld;
+          rv.w = topo.ws;
+          rv.use16 = topo.use16 ? 1 : 0;
+          rv.full = 1;
+          rv.val = sval;
+          rv.col16 = d_scol16;
+          rv.col32 = d_scol;
+          rv.len = d_slen8;
+          launch_relax_pressure4(rv, d_sdrank8, dinv_p, temp_p, src, dst, stream);
+        } else {
+          launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
+        }
         in_sol = !in_sol;
       }
     }

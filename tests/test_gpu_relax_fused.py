@@ -1,8 +1,11 @@
 """Jacobi-path Schur preconditioner on small meshes: all p_iters relax_pressure
 sweeps (schur_precond.wgsl:52-90, coupled_solver_fgmres.rs:1949-1976) run in
 one single-workgroup launch (k_relax_pressure_fused) instead of one launch per
-sweep.  Each case below selects one (rows per thread, ELL width) instantiation
-and an odd or even sweep count; fused GPU == per-sweep GPU == oracle, bit-exact."""
+sweep; larger meshes run one launch per sweep with 4 rows per thread over the
+16-bit scalar ELL image (k_relax_pressure4).  Each case below selects one
+(rows per thread, ELL width) instantiation and an odd or even sweep count (or
+is too large for the fused kernel); fused == 4-row per-sweep == 1-row
+per-sweep (k_relax_pressure) == oracle, bit-exact."""
 import numpy as np
 import pytest
 
@@ -44,6 +47,7 @@ CASES = [
     ("voronoi_0.015", 4, 10),  # 2,813 cells, width 10, 45 sweeps
     ("step_0.03", 4, 10),      # 3,722 cells, width 5, 49 sweeps
     ("step_0.02", 8, 5),       # 8,125 cells: gpu_solver_benchmark.rs's mesh, 64 sweeps
+    ("step_0.015", 0, 0),      # 14,589 cells: per-sweep launches only, 79 sweeps
 ]
 
 
@@ -52,24 +56,31 @@ def test_relax_fused_parity(name, rpt, wmax, monkeypatch):
     mesh = _mesh(name)
     n, ws, sweeps = _shape(mesh)
     # the case must exercise the instantiation it names (launch_relax_pressure_fused)
-    assert n <= rpt * 1024 and (rpt == 1 or n > rpt // 2 * 1024) and ws <= wmax, (n, ws)
+    if rpt:
+        assert n <= rpt * 1024 and (rpt == 1 or n > rpt // 2 * 1024) and ws <= wmax, (n, ws)
+    else:
+        assert n > 8191, n
     cfg = dict(fixed_outer=3, fixed_inner=12)
     fused = GpuSolver(mesh, config=default_config(**cfg))
     monkeypatch.setenv("CFD_RELAX_FUSED", "0")
-    per_sweep = GpuSolver(mesh, config=default_config(**cfg))
+    per_sweep4 = GpuSolver(mesh, config=default_config(**cfg))
+    monkeypatch.setenv("CFD_RELAX4", "0")
+    per_sweep1 = GpuSolver(mesh, config=default_config(**cfg))
     monkeypatch.delenv("CFD_RELAX_FUSED")
+    monkeypatch.delenv("CFD_RELAX4")
     o = OracleSolver(mesh, config=default_config(**cfg))
-    for s in (fused, per_sweep, o):
+    gpus = {"fused": fused, "per-sweep 4-row": per_sweep4, "per-sweep 1-row": per_sweep1}
+    for s in (*gpus.values(), o):
         _setup_amg_test(s, mesh, 0)
     for k in range(2):
-        for s in (fused, per_sweep, o):
+        for s in (*gpus.values(), o):
             s.step()
         ctx = f"{name} ({n} cells, width {ws}, {sweeps} sweeps) step {k}"
-        _assert_same_fields(fused, o, "fused " + ctx)
-        _assert_same_info(fused, o, "fused " + ctx)
-        _assert_same_fields(per_sweep, o, "per-sweep " + ctx)
-    for s in (fused, per_sweep):
-        s.close()
+        for label, g in gpus.items():
+            _assert_same_fields(g, o, f"{label} {ctx}")
+            _assert_same_info(g, o, f"{label} {ctx}")
+    for g in gpus.values():
+        g.close()
 
 
 def test_relax_fused_reference_benchmark_natural():
