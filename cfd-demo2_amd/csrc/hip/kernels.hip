@@ -62,11 +62,11 @@ __device__ __forceinline__ uint32_t u4(const uchar4& v, int k) {
 // aligned-slot rows (CoupledMatrix::lg): slots in use, and whether slot r
 // holds an entry of row k of the thread's 4
 __device__ __forceinline__ uint32_t lg_used(const ushort4& v, int k) {
-  return (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) & 0xFFu;
+  return (k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w) & kLgUsedMask;
 }
 __device__ __forceinline__ bool lg_on(const ushort4& v, int k, uint32_t r) {
   const uint32_t w = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-  return r < (w & 0xFFu) && !((w >> 8 >> r) & 1u);
+  return r < (w & kLgUsedMask) && !((w >> 8 >> r) & 1u);
 }
 
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -844,6 +844,8 @@ __device__ __forceinline__ float gat(bool on, const float* p) {
 // gained (level-0 smoother 84 -> 78 us, Schur predict 198 -> 185, correct
 // 166 -> 159)
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ f2u ld2u(const float* p) { return *reinterpret_cast<const f2u*>(p); }
 __device__ __forceinline__ f4u ld4u(const float* p) { return *reinterpret_cast<const f4u*>(p); }
 __device__ __forceinline__ bool consec4(const int c[4]) {
   return c[1] == c[0] + 1 && c[2] == c[0] + 2 && c[3] == c[0] + 3;
@@ -960,8 +962,11 @@ inline unsigned rows2x_grid(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) 
   const size_t t = (size_t)(r1 - r0 + 1) / 2 + (r3 > r2 ? (size_t)(r3 - r2 + 1) / 2 : 0);
   return (unsigned)((t + 255) / 256);
 }
-__device__ __forceinline__ bool lg2_on(uint32_t w, uint32_t r) { return r < (w & 0xFFu) && !((w >> 8 >> r) & 1u); }
-template <bool D16, int U>
+__device__ __forceinline__ bool lg2_on(uint32_t w, uint32_t r) { return r < (w & kLgUsedMask) && !((w >> 8 >> r) & 1u); }
+// REG (first slot group of a wave of regular rows, r0 = 0): columns
+// row + tmode[slot] (no column loads), and the two rows' x entries are six
+// consecutive floats (one 16-byte + one 8-byte gather)
+template <bool D16, int U, bool REG = false>
 __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
                                             uint32_t r0, uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
                                             const float2 d2[2], float su[2], float sv[2], float sp[2]) {
@@ -973,7 +978,10 @@ __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float*
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
     a[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
     g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
-    if constexpr (D16) {
+    if constexpr (REG) {
+      c[u][0] = (int)i0 + A.tmode[u];
+      c[u][1] = c[u][0] + 1;
+    } else if constexpr (D16) {
       const short2 d = *reinterpret_cast<const short2*>(A.col16 + off);
       c[u][0] = (int)i0 + (int)d.x;
       c[u][1] = (int)i0 + 1 + (int)d.y;
@@ -983,15 +991,30 @@ __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float*
       c[u][1] = q.y;
     }
   }
+  if constexpr (REG) {
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-      xg[u][k][0] = x[j];
-      xg[u][k][1] = x[j + 1];
-      xg[u][k][2] = x[j + 2];
+    for (int u = 0; u < U; ++u) {
+      const float* b = x + 3 * (ptrdiff_t)c[u][0];
+      const f4u q0 = ld4u(b);
+      const f2u q1 = ld2u(b + 4);
+      xg[u][0][0] = q0.x;
+      xg[u][0][1] = q0.y;
+      xg[u][0][2] = q0.z;
+      xg[u][1][0] = q0.w;
+      xg[u][1][1] = q1.x;
+      xg[u][1][2] = q1.y;
     }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
+        xg[u][k][0] = x[j];
+        xg[u][k][1] = x[j + 1];
+        xg[u][k][2] = x[j + 2];
+      }
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -1025,9 +1048,12 @@ __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* 
   const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
   const uint32_t lw[2] = {lg.x, lg.y}, dr[2] = {drr.x, drr.y};
-  const uint32_t maxlen = max(lw[0] & 0xFFu, lw[1] & 0xFFu);
+  const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float su[2] = {0.0f, 0.0f}, sv[2] = {0.0f, 0.0f}, sp[2] = {0.0f, 0.0f};
-  spmv2_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
+  if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
+    spmv2_group<D16, U1, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
+  else
+    spmv2_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv2_group<D16, U>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
   float* yo = y + 3 * (size_t)i0;  // 8-byte aligned (i0 even)
   typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1489,8 +1515,6 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
 #ifndef CFD_SCHUR_ROWS
 #define CFD_SCHUR_ROWS 2
 #endif
-typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
-__device__ __forceinline__ f2u ld2u(const float* p) { return *reinterpret_cast<const f2u*>(p); }
 template <bool D16>
 __device__ __forceinline__ void ccols2(const CoupledMatrix& A, size_t off, uint32_t i0, int c[2]) {
   if constexpr (D16) {
@@ -1503,7 +1527,7 @@ __device__ __forceinline__ void ccols2(const CoupledMatrix& A, size_t off, uint3
     c[1] = q.y;
   }
 }
-template <bool D16, int U>
+template <bool D16, int U, bool REG = false>  // REG: see spmv2_group
 __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
                                                const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
                                                uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
@@ -1515,7 +1539,12 @@ __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const flo
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
     g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
-    ccols2<D16>(A, off, i0, c[u]);
+    if constexpr (REG) {
+      c[u][0] = (int)i0 + A.tmode[u];
+      c[u][1] = c[u][0] + 1;
+    } else {
+      ccols2<D16>(A, off, i0, c[u]);
+    }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {  // 2 consecutive cells: 8 + 24 bytes
@@ -1573,8 +1602,11 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
   const uint32_t lw[2] = {lg.x, lg.y}, dr[2] = {drr.x, drr.y};
-  const uint32_t maxlen = max(lw[0] & 0xFFu, lw[1] & 0xFFu);
-  predict2_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
+  const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
+  if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
+    predict2_group<D16, U1, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
+  else
+    predict2_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
     predict2_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, lw, dr, d2, rhs);
   const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
@@ -1582,7 +1614,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
   if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
 }
-template <bool D16, int U>
+template <bool D16, int U, bool REG = false>  // REG: see spmv2_group
 __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const float* __restrict__ p_sol, uint32_t i0,
                                                uint32_t r0, uint32_t rmax, const uint32_t lw[2], float cu[2],
                                                float cv[2]) {
@@ -1593,7 +1625,12 @@ __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const flo
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
     g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
-    ccols2<D16>(A, off, i0, c[u]);
+    if constexpr (REG) {
+      c[u][0] = (int)i0 + A.tmode[u];
+      c[u][1] = c[u][0] + 1;
+    } else {
+      ccols2<D16>(A, off, i0, c[u]);
+    }
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -1624,9 +1661,12 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
   const uint32_t lw[2] = {lg.x, lg.y};
-  const uint32_t maxlen = max(lw[0] & 0xFFu, lw[1] & 0xFFu);
+  const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float cu[2] = {0.0f, 0.0f}, cv[2] = {0.0f, 0.0f};
-  correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
+  if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
+    correct2_group<D16, U1, true>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
+  else
+    correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;

@@ -177,12 +177,19 @@ struct CoupledMatrix {
   // slots (CSR order), gaps where a neighbour is missing
   const int32_t* col;     // [r*ld + i] signed local column (gaps: a virtual column)
   const int16_t* col16;   // [r*ld + i] col - i (use16)
-  const uint16_t* lg;     // [ld] slots in use (low byte) | gap mask << 8
+  const uint16_t* lg;     // [ld] slots in use (bits 0-6) | regular row (bit 7) | gap mask << 8
   const uint8_t* drank;   // [ld] slot of the diagonal
   const float2* cval_a;
   const float2* cval_g;
   const float2* cdiag2;   // [ld]
+  // regular rows (lg bit 7): every slot's column is row + tmode[slot] (the
+  // per-slot modal delta), so the kernels derive the columns instead of
+  // loading them; set when ws <= kCoupledRegMaxWs (one peeled slot group)
+  int reg;
+  int tmode[8];
 };
+constexpr uint32_t kLgUsedMask = 0x7Fu, kLgRegular = 0x80u;
+constexpr int kCoupledRegMaxWs = 5;
 
 // One AMG level (linear_solver/amg.rs AmgLevel) in the layout the gfx950
 // kernels stream: off-diagonal entries only, ELL slot-major with row stride

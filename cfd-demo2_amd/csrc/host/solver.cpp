@@ -86,6 +86,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   }
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
+  if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
   if (topo.ws > 255) relax4 = false;  // u8 row lengths
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
@@ -238,6 +239,8 @@ CoupledMatrix Solver::cmat() const {
   A.cval_a = cval_a;
   A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
+  A.reg = coupled_reg && !topo.tmode.empty() && topo.ws <= kCoupledRegMaxWs ? 1 : 0;
+  for (int r = 0; r < 8; ++r) A.tmode[r] = r < (int)topo.tmode.size() ? topo.tmode[r] : 0;
   return A;
 }
 

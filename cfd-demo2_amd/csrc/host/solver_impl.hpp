@@ -290,6 +290,7 @@ struct Solver {
   // CFD_AMG_WIDE_LIMIT lowers it so that tests exercise the wide path)
   int amg_wide_limit = 255;
   size_t lds_budget = 0;           // dynamic LDS of the tail kernels on this device (init_kernel_attributes)
+  bool coupled_reg = true;         // regular coupled rows: derived columns (CFD_COUPLED_REG=0: always load)
   bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
   bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction

@@ -186,7 +186,11 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
         const int64_t dd = (int64_t)t.tcol[(size_t)r * ld + li] - (int64_t)li;
         if (dd < -32768 || dd > 32767) small = false;
       }
-      t.tlg[li] = (uint16_t)(used | gap << 8);
+      // regular row: every slot's column is row + tmode[slot] (the kernels
+      // then derive the columns instead of loading them)
+      bool regular = typed && li < N;
+      for (int r = 0; r < ws && regular; ++r) regular = t.tcol[(size_t)r * ld + li] == (int32_t)li + t.tmode[r];
+      t.tlg[li] = (uint16_t)(used | (regular ? 0x80u : 0u) | gap << 8);
       if (li < N) t.tdrank8[li] = (uint8_t)slot[t.ell_drank[li]];
     }
   }

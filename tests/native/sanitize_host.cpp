@@ -62,7 +62,7 @@ void run(const char* name, const cfd2::Mesh& m) {
           on |= 1u << s;
           prev = s;
         }
-        const uint32_t used = t.tlg[i] & 0xFFu, gap = t.tlg[i] >> 8;
+        const uint32_t used = t.tlg[i] & 0x7Fu, gap = t.tlg[i] >> 8;
         check(used == (uint32_t)prev + 1 && (gap | on) == (1u << used) - 1u && !(gap & on), "slot mask");
         check(t.tslot[a + t.ell_drank[i]] == t.tdrank8[i], "diagonal slot");
         for (int r = 0; r < t.ws; ++r) {
