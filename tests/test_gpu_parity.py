@@ -487,6 +487,7 @@ VARIANTS = [
     {"CFD_AMG_TAIL_LDS": "0"},        # global-memory single-workgroup tail
     {"CFD_AMG_TAIL_ROWS": "0"},       # no tail kernel: every level launched
     {"CFD_AMG_FUSE_PRESMOOTH": "0"},  # coarse pre-smoother as its own sweep
+    {"CFD_COUPLED_REG": "0"},         # coupled-matrix kernels always load their columns
 ]
 
 
