@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: (h, target cells per GPU, BASELINE.json configs[] index)
+    "c0": (0.0172, 1.0e4, 0),  # the reference-test scale (CPU-runnable); launch-bound on a GPU
     "c1": (0.001723, 1.0e6, 1),
     "c2": (5.449e-4, 1.0e7, 2),
 }
