@@ -41,7 +41,7 @@ void run(const char* name, const cfd2::Mesh& m) {
   const uint32_t n = m.num_cells();
   for (int R = 1; R <= 4 && (uint32_t)R <= cfd2::red_geom(n).nseg; ++R) {
     const auto starts = cfd2::partition_starts(n, R);
-    uint64_t rows = 0, nnz = 0, sends = 0, recvs = 0;
+    uint64_t rows = 0, nnz = 0, sends = 0, recvs = 0, reg_rows = 0;
     for (int r = 0; r < R; ++r) {
       cfd2::Topology t;
       cfd2::build_topology(v, t, (uint32_t)starts[r], (uint32_t)starts[r + 1]);
@@ -65,10 +65,17 @@ void run(const char* name, const cfd2::Mesh& m) {
         const uint32_t used = t.tlg[i] & 0x7Fu, gap = t.tlg[i] >> 8;
         check(used == (uint32_t)prev + 1 && (gap | on) == (1u << used) - 1u && !(gap & on), "slot mask");
         check(t.tslot[a + t.ell_drank[i]] == t.tdrank8[i], "diagonal slot");
+        bool all_modal = true;
         for (int r = 0; r < t.ws; ++r) {
           const int32_t c = t.tcol[(size_t)r * t.ld + i];
           check(c >= -(int32_t)t.glo && c < (int32_t)(t.npad + t.ghi), "virtual columns inside the vectors");
+          if (r >= (int)t.tmode.size() || c != (int32_t)i + t.tmode[r]) all_modal = false;
         }
+        // regular row (the kernels derive its columns): flagged iff every slot
+        // holds row + tmode[slot] (aligned-slot layout only)
+        const bool typed = t.ws <= 8;
+        check(((t.tlg[i] & 0x80u) != 0) == (typed && all_modal), "regular-row flag");
+        if (t.tlg[i] & 0x80u) reg_rows++;
       }
       for (const auto& h : p.peers) {
         sends += h.send_cnt;
@@ -96,8 +103,9 @@ void run(const char* name, const cfd2::Mesh& m) {
       check(H[l].part.size() == (size_t)R + 1 && H[l].part[0] == 0 && H[l].part[R] == H[l].A.rows, "level partition");
       for (int q = 0; q < R; ++q) check(H[l].part[q] <= H[l].part[q + 1], "level partition order");
     }
-    std::printf("%s: %u cells, %d rank(s): nnz %llu, halo %llu, %zu AMG levels: ok\n", name, n, R,
-                (unsigned long long)nnz, (unsigned long long)sends, H.size());
+    std::printf("%s: %u cells, %d rank(s): nnz %llu, halo %llu, regular coupled rows %llu, %zu AMG levels: ok\n",
+                name, n, R, (unsigned long long)nnz, (unsigned long long)sends, (unsigned long long)reg_rows,
+                H.size());
   }
 }
 
