@@ -1330,9 +1330,13 @@ void Solver::precondition(int j, float* z) {
   });
 }
 
-float Solver::norm_blocking(const float* v, int mode, int slot) {
+void Solver::norm_launch(const float* v, int mode, int slot) {
   launch_dot_partial(v, v, N, red.U, partial_n, stream);
   launch_reduce_final(combine(partial_n, 1), mode, dsc + slot, binv, mode == 2 ? g : nullptr, stream);
+}
+
+float Solver::norm_blocking(const float* v, int mode, int slot) {
+  norm_launch(v, mode, slot);
   CFD_HIP(hipMemcpyAsync(h_pin, dsc + slot, sizeof(float), hipMemcpyDeviceToHost, stream));
   sync();
   return h_pin[0];
@@ -1342,6 +1346,13 @@ float Solver::norm_blocking(const float* v, int mode, int slot) {
 // V0 is stored unnormalised: binv[0] = 1/||r|| (the reference's scale_in_place),
 // g = [||r||, 0, ...] (coupled_solver_fgmres.rs:1880-1890, 2380-2392).
 float Solver::residual_into_v0_blocking() {
+  residual_into_v0_launch();
+  CFD_HIP(hipMemcpyAsync(h_pin, dsc + 1, sizeof(float), hipMemcpyDeviceToHost, stream));
+  sync();
+  return h_pin[0];
+}
+
+void Solver::residual_into_v0_launch() {
   CFD_HIP(hipMemsetAsync(g, 0, m1 * sizeof(float), stream));
   overlapped(cell_plan, {{x, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix A = cmat();
@@ -1352,7 +1363,7 @@ float Solver::residual_into_v0_blocking() {
     launch_spmv(A, x, w, stream);
   });
   launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
-  return norm_blocking(basis, 2, 1);
+  norm_launch(basis, 2, 1);
 }
 
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
@@ -1364,14 +1375,22 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   const int lag = cfg.convergence_lag;
   ensure_fgmres();
   if (constants.precond_type == 1) ensure_amg();
-  const float rhs_norm = norm_blocking(rhs, 1, 0);
+  // ||b|| and the initial residual V0 = b - A x, ||V0|| in one submission and
+  // one readback: the reference reads ||b|| first and skips the residual on
+  // its early exit; computing it anyway only writes solver scratch (V0,
+  // binv[0], g) that the next solve rewrites, so the results are unchanged
+  norm_launch(rhs, 1, 0);
+  residual_into_v0_launch();
+  CFD_HIP(hipMemcpyAsync(h_pin, dsc, 2 * sizeof(float), hipMemcpyDeviceToHost, stream));
+  sync();
+  const float rhs_norm = h_pin[0];
   if (rhs_norm < abstol || !std::isfinite(rhs_norm)) {
     st.residual = rhs_norm;
     st.converged = rhs_norm < abstol;
     st.diverged = !std::isfinite(rhs_norm);
     return st;
   }
-  float residual_norm = residual_into_v0_blocking();
+  float residual_norm = h_pin[1];
   const float target = std::fmax(tol * rhs_norm, abstol);
   if (residual_norm < target) {
     log("FGMRES: Initial guess already converged (||r|| = %s < %s)\n", e2(residual_norm).c_str(), e2(target).c_str());

@@ -389,7 +389,9 @@ struct Solver {
   static constexpr size_t kProfPoolMax = 1u << 15;
   void prof_grow(size_t n);  // event pool of at least n events
  private:
+  void norm_launch(const float* v, int mode, int slot);
   float norm_blocking(const float* v, int mode, int slot);
+  void residual_into_v0_launch();
   float residual_into_v0_blocking();
   void check_evolution();
   void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
