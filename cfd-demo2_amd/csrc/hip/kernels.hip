@@ -1358,19 +1358,23 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   constexpr uint32_t kT = 4u * kRelaxFusedMaxRows + 4u;  // byte offset of T (32768)
   const uint32_t t = threadIdx.x;
   float dv[RPT], tp[RPT], v[RPT][OD];
+  // own rows of both iterates (P: own[0], T: own[1]) also live in registers:
+  // a sweep's mix operand (the destination's previous value, written by this
+  // thread two sweeps earlier) is read from them, not from LDS
+  float own[2][RPT];
   uint32_t ad[RPT][OD];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
-    dv[k] = tp[k] = 0.0f;
+    dv[k] = tp[k] = own[0][k] = own[1][k] = 0.0f;
 #pragma unroll
     for (int e = 0; e < OD; ++e) {
       v[k][e] = 0.0f;
       ad[k][e] = 4u * N;  // the zero row
     }
     if (i < N) {
-      relax_lds[i] = p_sol[i];
-      relax_lds[kT / 4 + i] = temp[i];
+      own[0][k] = relax_lds[i] = p_sol[i];
+      own[1][k] = relax_lds[kT / 4 + i] = temp[i];
       dv[k] = dinv_p[i];
       tp[k] = temp_p[i];
       const uint32_t l = len[i];
@@ -1399,17 +1403,19 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   // SRC = byte offset of the source iterate (0: P, kT: T)
   auto sweep = [&](auto src_off) {
     constexpr uint32_t SRC = decltype(src_off)::value, DST = kT - SRC;
+    constexpr int DI = DST == 0 ? 0 : 1;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      // rows past N compute on the zero row: +0 entries, dv = tp = +0, so they
-      // write mix(+0, +0, 1.2) = +0 back into it (branch-free sweep)
+      // rows past N compute on the zero row: +0 entries, dv = tp = own = +0, so
+      // they write mix(+0, +0, 1.2) = +0 back into it (branch-free sweep)
       const uint32_t i = min(t + (uint32_t)k * kRelaxThreads, N);
       float sigma = 0.0f;
 #pragma unroll
       for (int e = 0; e < OD; ++e) sigma += v[k][e] * *reinterpret_cast<const float*>(base + ad[k][e] + SRC);
       const float hat_x = dv[k] * (tp[k] - sigma);
-      float* d = reinterpret_cast<float*>(base + 4u * i + DST);
-      *d = wmix(*d, hat_x, 1.2f);  // own row: only this thread touches it in this sweep
+      // own row: only this thread touches it in this sweep
+      own[DI][k] = wmix(own[DI][k], hat_x, 1.2f);
+      *reinterpret_cast<float*>(base + 4u * i + DST) = own[DI][k];
     }
     __syncthreads();
   };
@@ -1423,8 +1429,8 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
     if (i < N) {
-      p_sol[i] = relax_lds[i];
-      temp[i] = relax_lds[kT / 4 + i];
+      p_sol[i] = own[0][k];
+      temp[i] = own[1][k];
     }
   }
 }
