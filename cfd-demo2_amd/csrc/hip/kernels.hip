@@ -1159,7 +1159,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
 // (gmres_logic.wgsl:24-76).
 __device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens, float* g, float* binv,
-                                float* resid_hist) {
+                                float* resid_hist, float* host_resid = nullptr) {
   const float norm = sqrtf(s);
   H[(size_t)j * m1 + j + 1] = norm;
   binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
@@ -1185,13 +1185,16 @@ __device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens,
   g[j] = cc * gj + ss * gj1;
   g[j + 1] = -ss * gj + cc * gj1;
   resid_hist[j] = fabsf(g[j + 1]);
+  // the host's lag-model read (coupled_solver.rs:326-435): written straight into
+  // pinned host memory, so no copy is enqueued per iteration
+  if (host_resid) host_resid[j] = resid_hist[j];
 }
 __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
                                                                   float* givens, float* g, float* binv,
-                                                                  float* resid_hist) {
+                                                                  float* resid_hist, float* host_resid) {
   __shared__ float la[kRedMaxSegments], lb[65];
   const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
-  if (threadIdx.x == 0) norm_givens_out(s, j, H, m1, givens, g, binv, resid_hist);
+  if (threadIdx.x == 0) norm_givens_out(s, j, H, m1, givens, g, binv, resid_hist, host_resid);
 }
 
 // predict_and_form_schur (schur_precond.wgsl:142-188), 4 cells per thread.
@@ -2538,9 +2541,9 @@ void launch_cgs_update_norm(const float* w, float* basis, const float* binv, siz
                        N, U, partial);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
-                        float* resid_hist, hipStream_t s) {
+                        float* resid_hist, float* host_resid, hipStream_t s) {
   hipLaunchKernelGGL(k_norm_givens, dim3(1), dim3(kRedFinalThreads), 0, s, r, j, H, m1, givens, g, binv,
-                     resid_hist);
+                     resid_hist, host_resid);
 }
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,

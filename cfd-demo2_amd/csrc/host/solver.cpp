@@ -185,7 +185,10 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   partial_d = arena.alloc<double>(5 * (size_t)pstride + 5);
   maxbits = arena.alloc<uint32_t>(4);
   blockmax = arena.alloc<uint32_t>(2 * (((size_t)N + 255) / 256) + 2);
-  CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float), hipHostMallocDefault));
+  // pinned, mapped and coherent: kernels may store the per-iteration residual into
+  // it directly (d_pin, the device view), visible to the host after the event
+  CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
+  CFD_HIP(hipHostGetDevicePointer((void**)&d_pin, h_pin, 0));
   for (auto& e : ev_outer) CFD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // constants (init/fields.rs:100-115)
   constants.dt = 0.0001f;
@@ -1425,7 +1428,8 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream);
-      launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, stream);
+      launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist,
+                         fixed ? nullptr : d_pin + 64, stream);
       check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
@@ -1435,7 +1439,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         inner.has_last = true;
         inner.pending = -1;
       }
-      CFD_HIP(hipMemcpyAsync(h_pin + 64 + j, resid_hist + j, sizeof(float), hipMemcpyDeviceToHost, stream));
+      // k_norm_givens wrote resid_hist[j] into h_pin[64 + j]; the event orders the read
       CFD_HIP(hipEventRecord(ev_iter[j], stream));
       bool have = false;
       float check = 0.0f;

@@ -278,6 +278,7 @@ struct Solver {
   uint32_t* maxbits = nullptr;
   uint32_t* blockmax = nullptr;  // [2 * ceil(N/256)]
   float* h_pin = nullptr;        // pinned host scalars
+  float* d_pin = nullptr;        // device view of h_pin (mapped)
   std::vector<hipEvent_t> ev_iter;
   hipEvent_t ev_outer[2]{};
   LagReader inner;
