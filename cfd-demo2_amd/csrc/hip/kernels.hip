@@ -757,20 +757,25 @@ __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict_
 }
 
 // norm outputs of a finished dot: mode 1: out = sqrt(s); mode 2: also inv, g0
-__device__ __forceinline__ void norm_out(float s, int mode, float* out, float* inv, float* g0) {
+__device__ __forceinline__ void norm_out(float s, int mode, float* out, float* inv, float* g0, float* host_out) {
   const float nrm = sqrtf(s);
   out[0] = nrm;
+  if (host_out) host_out[0] = nrm;  // mapped pinned host memory: the host's read needs no copy
   if (mode == 2) {
     inv[0] = 1.0f / nrm;  // host-side `1.0 / residual_norm` (coupled_solver_fgmres.rs:1872)
     if (g0) g0[0] = nrm;
   }
 }
 
+// g_len > 0 (mode 2): g = [||r||, 0, ..., 0] of length g_len (the zero fill of
+// coupled_solver_fgmres.rs:1880-1890 done here instead of a separate fill)
 __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int mode, float* out, float* inv,
-                                                                   float* g0) {
+                                                                   float* g0, int g_len, float* host_out) {
   __shared__ float la[kRedMaxSegments], lb[65];
   const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
-  if (threadIdx.x == 0) norm_out(s, mode, out, inv, g0);
+  if (g0)
+    for (int k = 1 + (int)threadIdx.x; k < g_len; k += kRedFinalThreads) g0[k] = 0.0f;
+  if (threadIdx.x == 0) norm_out(s, mode, out, inv, g0, host_out);
 }
 
 // axpby (gmres_ops.wgsl:108-117) with alpha = 1, beta = -1: V0 = b - A x
@@ -2503,8 +2508,10 @@ inline unsigned red_blocks(uint32_t N) {  // 4 chunks of 256 cells per 256-threa
 void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
   if (N) hipLaunchKernelGGL(k_dot_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, x, y, N, U, partial);
 }
-void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0);
+void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, int g_len, float* host_out,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0, g_len,
+                     host_out);
 }
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);

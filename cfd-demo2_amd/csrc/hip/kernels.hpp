@@ -275,7 +275,9 @@ void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float*
 void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s);
 // total of the reduction r (one vector): mode 1: out[0] = sqrt(total); mode 2:
 // also *inv = 1.0f / sqrt (host-style) and g0 (if non-null) = sqrt
-void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, hipStream_t s);
+// g0 (mode 2): g0[0] = norm, g0[1..g_len) = 0; host_out (device view of pinned host memory, or null) = norm
+void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, int g_len, float* host_out,
+                         hipStream_t s);
 void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
 void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
 // basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
