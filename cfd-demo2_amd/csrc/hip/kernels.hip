@@ -593,7 +593,7 @@ __global__ void __launch_bounds__(kBlock) k_update_fields(uint32_t N, float alph
 }
 
 __global__ void __launch_bounds__(kBlock) k_maxdiff_final(const uint32_t* __restrict__ blockmax,
-                                                          uint32_t nb, uint32_t* maxbits) {
+                                                          uint32_t nb, uint32_t* maxbits, uint32_t* host_out) {
   __shared__ uint32_t su[4], sp[4];
   uint32_t bu = 0, bp = 0;
   for (uint32_t q = threadIdx.x; q < nb; q += kBlock) {
@@ -614,6 +614,10 @@ __global__ void __launch_bounds__(kBlock) k_maxdiff_final(const uint32_t* __rest
   if (threadIdx.x == 0) {
     maxbits[0] = max(max(su[0], su[1]), max(su[2], su[3]));
     maxbits[1] = max(max(sp[0], sp[1]), max(sp[2], sp[3]));
+    if (host_out) {  // mapped pinned host memory: the host's lagged read needs no copy
+      host_out[0] = maxbits[0];
+      host_out[1] = maxbits[1];
+    }
   }
 }
 
@@ -2474,7 +2478,7 @@ __global__ void __launch_bounds__(kBlock) k_seg_reduce(const T* __restrict__ par
 }
 
 // max over ranks of the (u, p) max-diff bit patterns
-__global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint32_t* out) {
+__global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint32_t* out, uint32_t* host_out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint32_t bu = 0, bp = 0;
   for (int r = 0; r < R; ++r) {
@@ -2483,6 +2487,10 @@ __global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint
   }
   out[0] = bu;
   out[1] = bp;
+  if (host_out) {
+    host_out[0] = bu;
+    host_out[1] = bp;
+  }
 }
 
 }  // namespace
@@ -2495,11 +2503,11 @@ void launch_assemble(const AssembleArgs& a, hipStream_t s) {
   if (a.N) hipLaunchKernelGGL(k_assemble, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
 }
 void launch_update_fields(uint32_t N, float au, float ap, const float* x, float2* u, float* p,
-                          uint32_t* blockmax, uint32_t* maxbits, hipStream_t s) {
+                          uint32_t* blockmax, uint32_t* maxbits, uint32_t* host_out, hipStream_t s) {
   if (!N) return;
   const unsigned nb = grid_for(N);
   hipLaunchKernelGGL(k_update_fields, dim3(nb), dim3(kBlock), 0, s, N, au, ap, x, u, p, blockmax);
-  hipLaunchKernelGGL(k_maxdiff_final, dim3(1), dim3(kBlock), 0, s, blockmax, nb, maxbits);
+  hipLaunchKernelGGL(k_maxdiff_final, dim3(1), dim3(kBlock), 0, s, blockmax, nb, maxbits, host_out);
 }
 inline unsigned red_blocks(uint32_t N) {  // 4 chunks of 256 cells per 256-thread block
   const unsigned nch = (N + kRedChunkCells - 1) / kRedChunkCells;
@@ -2742,8 +2750,8 @@ void launch_seg_reduce_d(const double* part, uint32_t np, uint32_t nchunks, uint
                          uint32_t maxseg, hipStream_t s) {
   seg_reduce(part, np, nchunks, G, nvec, out, maxseg, s);
 }
-void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_max_combine, dim3(1), dim3(64), 0, s, gathered, R, out);
+void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, uint32_t* host_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_max_combine, dim3(1), dim3(64), 0, s, gathered, R, out, host_out);
 }
 void launch_evolution_final(const RedSrcD& r, double* out5, hipStream_t s) {
   hipLaunchKernelGGL(k_evolution_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, out5);

@@ -269,8 +269,9 @@ struct TailBlobLevel {
 void launch_prepare(const PrepareArgs& a, hipStream_t s);
 void launch_assemble(const AssembleArgs& a, hipStream_t s);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
+// (and to host_out[0..1], a device view of pinned host memory, when non-null)
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
-                          float* p, uint32_t* blockmax, uint32_t* maxbits, hipStream_t s);
+                          float* p, uint32_t* blockmax, uint32_t* maxbits, uint32_t* host_out, hipStream_t s);
 // unit partials (U chunks of 256 cells each) of dot(x, y) over 3-component cells
 void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s);
 // total of the reduction r (one vector): mode 1: out[0] = sqrt(total); mode 2:
@@ -367,7 +368,7 @@ void launch_seg_reduce(const float* part, uint32_t np, uint32_t nchunks, uint32_
                        uint32_t maxseg, hipStream_t s);
 void launch_seg_reduce_d(const double* part, uint32_t np, uint32_t nchunks, uint32_t G, int nvec, double* out,
                          uint32_t maxseg, hipStream_t s);
-void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, hipStream_t s);
+void launch_max_combine(const uint32_t* gathered, int R, uint32_t* out, uint32_t* host_out, hipStream_t s);
 // out5[f] = total of the 5 check_evolution sums (r.nvec = 5)
 void launch_evolution_final(const RedSrcD& r, double* out5, hipStream_t s);
 

@@ -1638,12 +1638,16 @@ void Solver::step() {  // coupled_solver.rs:33-499
     info.stats_p = ls;
     info.total_linear_iterations += ls.iterations;
     if (std::isnan(ls.residual)) throw std::domain_error("Coupled Linear Solver Diverged: NaN detected in linear residual");
-    launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, blockmax, maxbits, stream);
+    // the final max-diff pair also lands in this iteration's pinned host slot
+    // (h_pin + 32 + 2 (iter & 1)): the lagged read below needs no copy launch
+    uint32_t* host_slot = reinterpret_cast<uint32_t*>(d_pin + 32 + 2 * (iter & 1));
+    launch_update_fields(N, constants.alpha_u, constants.alpha_p, x, S().u, S().p, blockmax, maxbits,
+                         dist() ? nullptr : host_slot, stream);
     check_launch("update_fields");
     if (dist()) {
       halo_state(false);  // the next prepare reads neighbours' u, p
       comm->allgather(maxbits, mx_gather, 2 * sizeof(uint32_t), stream);
-      launch_max_combine(mx_gather, R, maxbits, stream);
+      launch_max_combine(mx_gather, R, maxbits, host_slot, stream);
     }
     if (iter == 0) {
       info.outer_residual_u = std::numeric_limits<float>::max();
@@ -1660,8 +1664,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
       outer.has_last = true;
       pend = -1;
     }
-    CFD_HIP(hipMemcpyAsync(slot, maxbits, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    CFD_HIP(hipEventRecord(ev_outer[iter & 1], stream));
+    CFD_HIP(hipEventRecord(ev_outer[iter & 1], stream));  // orders the read of slot
     bool have = false;
     float cu = 0.0f, cp = 0.0f;
     if (cfg.convergence_lag == 0) {
