@@ -185,9 +185,11 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   partial_d = arena.alloc<double>(5 * (size_t)pstride + 5);
   maxbits = arena.alloc<uint32_t>(4);
   blockmax = arena.alloc<uint32_t>(2 * (((size_t)N + 255) / 256) + 2);
-  // pinned, mapped and coherent: kernels may store the per-iteration residual into
-  // it directly (d_pin, the device view), visible to the host after the event
-  CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
+  // pinned, mapped (for every device: portable) and coherent: kernels may store
+  // the per-iteration residual into it directly (d_pin, the device view),
+  // visible to the host after the event
+  CFD_HIP(hipHostMalloc((void**)&h_pin, 4096 * sizeof(float),
+                        hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
   CFD_HIP(hipHostGetDevicePointer((void**)&d_pin, h_pin, 0));
   for (auto& e : ev_outer) CFD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // constants (init/fields.rs:100-115)
