@@ -99,6 +99,22 @@ class StepInfo(C.Structure):
     ]
 
 
+class CommStats(C.Structure):  # cfd_comm_stats
+    _fields_ = [
+        ("transport", C.c_int32),
+        ("comm_count", C.c_int32),
+        ("comm_rank", C.c_int32),
+        ("device", C.c_int32),
+        ("exchanges", C.c_uint64),
+        ("allgathers", C.c_uint64),
+        ("bytes_sent", C.c_uint64),
+        ("bytes_gathered", C.c_uint64),
+    ]
+
+
+TRANSPORTS = {0: "none", 1: "rccl", 2: "in-process", 3: "host-staged"}
+
+
 class StateFileHeader(C.Structure):  # cfd_state_file_header (512 bytes)
     _fields_ = [
         ("magic", C.c_char * 8),
@@ -155,7 +171,8 @@ EXPORTED = [
     "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_amg_info",
     "cfd_dist_unique_id", "cfd_solver_create_dist", "cfd_solver_create_dist_host", "cfd_group_create",
     "cfd_group_step",
-    "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest",
+    "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest", "cfd_dist_comm_stats",
+    "cfd_debug_group_fault",
 ]
 
 _lib = None

@@ -80,6 +80,8 @@ def _bind():
     L.cfd_state_save.argtypes = [_vp, C.c_char_p]
     L.cfd_state_load.argtypes = [_vp, C.c_char_p]
     L.cfd_group_state_save.argtypes = [C.POINTER(_vp), C.c_int32, C.c_char_p]
+    L.cfd_dist_comm_stats.argtypes = [_vp, C.POINTER(_ffi.CommStats), C.c_int32]
+    L.cfd_debug_group_fault.argtypes = [C.POINTER(_vp), C.c_int32, C.c_int32]
     _bound = True
     return L
 
@@ -314,6 +316,15 @@ class GpuSolver:
     def debug_prepare_assemble(self, assemble=True):
         self._call("cfd_debug_prepare_assemble", 1 if assemble else 0)
 
+    def comm_stats(self, reset=False) -> dict:
+        """Transport of this handle (RCCL: ncclCommCount / ncclCommUserRank),
+        its HIP device, and the collective traffic since the last reset."""
+        c = _ffi.CommStats()
+        self._call("cfd_dist_comm_stats", C.byref(c), 1 if reset else 0)
+        d = {k: getattr(c, k) for k, _ in _ffi.CommStats._fields_}
+        d["transport"] = _ffi.TRANSPORTS.get(c.transport, str(c.transport))
+        return d
+
 
 def dist_unique_id() -> bytes:
     """RCCL unique id (rank 0 creates it, every rank passes it to create_dist)."""
@@ -378,6 +389,11 @@ class GpuGroup:
             c0, c1 = r.owned
             out[c0:c1] = getattr(r, getter)()
         return out
+
+    def debug_fault(self, fail_rank: int) -> None:
+        """cfd_debug_group_fault: raises (the injected failure of ``fail_rank``)."""
+        _ffi.check(_bind().cfd_debug_group_fault(self._harr, self.nranks, int(fail_rank)),
+                   "cfd_debug_group_fault")
 
     def save_state(self, path):
         _ffi.check(_bind().cfd_group_state_save(self._harr, self.nranks, os.fsencode(path)),

@@ -1196,7 +1196,7 @@ __device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens,
   resid_hist[j] = fabsf(g[j + 1]);
   // the host's lag-model read (coupled_solver.rs:326-435): written straight into
   // pinned host memory, so no copy is enqueued per iteration
-  if (host_resid) host_resid[j] = resid_hist[j];
+  if (host_resid) host_resid[0] = resid_hist[j];
 }
 __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
                                                                   float* givens, float* g, float* binv,

@@ -314,6 +314,23 @@ cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, in
   auto group = std::make_shared<cfd2::LocalGroup>(nranks);
   std::vector<cfd2::Solver*> made;
   const cfd_status st = guard([&] {
+    // ranks on distinct devices copy from each other's memory (LocalComm):
+    // enable peer access both ways once per device pair
+    for (int a = 0; a < nranks; ++a)
+      for (int b = 0; b < nranks; ++b) {
+        if (devices[a] == devices[b]) continue;
+        int can = 0;
+        CFD_HIP(hipDeviceCanAccessPeer(&can, devices[a], devices[b]));
+        if (!can)
+          throw std::invalid_argument("device " + std::to_string(devices[a]) + " cannot access device " +
+                                      std::to_string(devices[b]) + " (peer access)");
+        CFD_HIP(hipSetDevice(devices[a]));
+        const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled)
+          (void)hipGetLastError();
+        else
+          CFD_HIP(e);
+      }
     for (int r = 0; r < nranks; ++r) {
       auto comm = cfd2::make_local_comm(group, r, devices[r]);
       made.push_back(new cfd2::Solver(*mesh, c, devices[r], nranks > 1 ? std::move(comm) : nullptr));
@@ -343,11 +360,14 @@ cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
       st[r] = guard([&] { f(*h[r]->s); });
       if (st[r] != CFD_OK) {
         msg[r] = cfd_last_error();
-        // wake the ranks waiting for this one in a collective (they fail too)
-        if (h[r]->s->comm) h[r]->s->comm->abort();
+        // wake the ranks waiting for this one in a collective (they fail too);
+        // a rank that was itself woken by an abort has nothing to add
+        if (h[r]->s->comm && msg[r].find("group aborted") == std::string::npos) h[r]->s->comm->abort();
       }
     });
   for (auto& t : th) t.join();
+  // every rank has returned: the group is usable again (LocalGroup::reset)
+  if (h[0]->s->comm) h[0]->s->comm->reset();
   // report the first rank that failed on its own (the others fail with "aborted")
   int first = -1;
   for (int r = 0; r < n; ++r)
@@ -399,6 +419,33 @@ cfd_status cfd_debug_rccl_selftest(int32_t device) {
     (void)hipStreamDestroy(s);
     for (size_t i = 0; i < n; ++i)
       if (back[i] != h[i] || back[n + i] != h[i]) throw std::runtime_error("RCCL self-test: wrong data");
+  });
+}
+
+cfd_status cfd_dist_comm_stats(cfd_solver* s, cfd_comm_stats* out, int32_t reset) {
+  CHECK_S(s);
+  if (!out) return set_error(CFD_ERR_INVALID, "null out");
+  std::memset(out, 0, sizeof(*out));
+  out->device = s->s->device;
+  out->comm_count = 1;
+  auto& c = s->s->comm;
+  if (c) {
+    out->transport = c->kind;
+    out->comm_count = c->comm_count();
+    out->comm_rank = c->comm_rank();
+    out->exchanges = c->stats.exchanges;
+    out->allgathers = c->stats.allgathers;
+    out->bytes_sent = c->stats.bytes_sent;
+    out->bytes_gathered = c->stats.bytes_gathered;
+    if (reset) c->stats = cfd2::CommStats{};
+  }
+  return CFD_OK;
+}
+
+cfd_status cfd_debug_group_fault(cfd_solver* const* h, int32_t n, int32_t fail_rank) {
+  return group_run(h, n, [fail_rank](cfd2::Solver& s) {
+    if (s.rk == fail_rank) throw std::runtime_error("injected fault");
+    (void)s.allgather_u64(1);  // waits for the failed rank until the abort wakes it
   });
 }
 

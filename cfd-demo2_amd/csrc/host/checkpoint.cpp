@@ -77,6 +77,9 @@ void Solver::save_state(const char* path) {
   const Range range("state save");
   CFD_HIP(hipSetDevice(device));
   sync();
+  // a lagged residual read still pending is part of the state: complete it
+  // now (the value is the one the next read would take)
+  flush_inner();
   // collective: every rank learns the AMG source size and its value offset
   // a pending refresh stands for a dropped hierarchy (the next AMG solve re-makes it)
   const bool have_amg = (amg_built && !amg_refresh_pending) || amg_src_loaded;

@@ -46,12 +46,22 @@ class RcclComm final : public Comm {
     CFD_NCCL(ncclCommInitRank(&comm_, nranks, id, r));
     rank = r;
     size = nranks;
+    kind = 1;
+  }
+  int comm_count() const override {
+    int n = -1;
+    return ncclCommCount(comm_, &n) == ncclSuccess ? n : -1;
+  }
+  int comm_rank() const override {
+    int r = -1;
+    return ncclCommUserRank(comm_, &r) == ncclSuccess ? r : -1;
   }
   ~RcclComm() override {
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
     if (msgs.empty()) return;
+    count_exchange(msgs);
     CFD_NCCL(ncclGroupStart());
     for (const Msg& m : msgs) {
       if (m.sbytes) CFD_NCCL(ncclSend(m.sbuf, m.sbytes, ncclChar, m.peer, comm_, s));
@@ -60,6 +70,7 @@ class RcclComm final : public Comm {
     CFD_NCCL(ncclGroupEnd());
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    count_allgather(bytes);
     CFD_NCCL(ncclAllGather(send, recv, bytes, ncclChar, comm_, s));
   }
 
@@ -84,9 +95,11 @@ class HostComm final : public Comm {
       : ex_(ex), ag_(ag), user_(user) {
     rank = r;
     size = nranks;
+    kind = 3;
   }
   void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
     if (msgs.empty()) return;
+    count_exchange(msgs);
     CFD_HIP(hipStreamSynchronize(s));
     const size_t n = msgs.size();
     std::vector<std::vector<char>> sb(n), rb(n);
@@ -110,6 +123,7 @@ class HostComm final : public Comm {
       if (msgs[i].rbytes) CFD_HIP(hipMemcpy(msgs[i].rbuf, rb[i].data(), msgs[i].rbytes, hipMemcpyHostToDevice));
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    count_allgather(bytes);
     CFD_HIP(hipStreamSynchronize(s));
     std::vector<char> sb(bytes + 1), rb((size_t)size * bytes + 1);
     if (bytes) CFD_HIP(hipMemcpy(sb.data(), send, bytes, hipMemcpyDeviceToHost));
@@ -159,6 +173,17 @@ void LocalGroup::abort() {
   cv_.notify_all();
 }
 
+void LocalGroup::reset() {
+  std::lock_guard<std::mutex> lk(mu_);
+  aborted_ = false;
+  arrived_ = 0;
+  ++gen_;
+  for (auto& sl : slots) {
+    sl.posted.clear();
+    sl.gather_src = nullptr;
+  }
+}
+
 namespace {
 
 // Pull model: after barrier 1 every rank copies what it receives out of the
@@ -170,6 +195,7 @@ class LocalComm final : public Comm {
   LocalComm(std::shared_ptr<LocalGroup> g, int r, int device) : g_(std::move(g)) {
     rank = r;
     size = g_->size();
+    kind = 2;
     auto& sl = g_->slots[r];
     sl.device = device;
     CFD_HIP(hipSetDevice(device));
@@ -178,6 +204,7 @@ class LocalComm final : public Comm {
   }
 
   void exchange(const std::vector<Msg>& msgs, hipStream_t s) override {
+    count_exchange(msgs);
     auto& me = g_->slots[rank];
     me.posted = msgs;
     CFD_HIP(hipEventRecord(me.ready, s));
@@ -220,8 +247,10 @@ class LocalComm final : public Comm {
   }
 
   void abort() override { g_->abort(); }
+  void reset() override { g_->reset(); }
 
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    count_allgather(bytes);
     auto& me = g_->slots[rank];
     me.gather_src = send;
     CFD_HIP(hipEventRecord(me.ready, s));

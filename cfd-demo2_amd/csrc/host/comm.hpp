@@ -37,10 +37,29 @@ struct Msg {
   size_t rbytes;
 };
 
+// Traffic counters of one rank's transport (cfd_comm_stats).
+struct CommStats {
+  uint64_t exchanges = 0, allgathers = 0, bytes_sent = 0, bytes_gathered = 0;
+};
+
 class Comm {
  public:
   virtual ~Comm() = default;
   int rank = 0, size = 1;
+  int kind = 0;  // cfd_comm_stats.transport
+  CommStats stats;
+  // the transport's own view of the communicator (RCCL: ncclCommCount /
+  // ncclCommUserRank; the others: size / rank)
+  virtual int comm_count() const { return size; }
+  virtual int comm_rank() const { return rank; }
+  void count_exchange(const std::vector<Msg>& msgs) {
+    ++stats.exchanges;
+    for (const Msg& m : msgs) stats.bytes_sent += m.sbytes;
+  }
+  void count_allgather(size_t bytes) {
+    ++stats.allgathers;
+    stats.bytes_gathered += bytes;
+  }
   virtual void exchange(const std::vector<Msg>& msgs, hipStream_t s) = 0;
   // recv[r * bytes ...] = rank r's send (bytes each), all ranks
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
@@ -51,6 +70,11 @@ class Comm {
   // group) so they fail too instead of waiting forever.  RCCL / host
   // transports: no-op (the launcher tears the processes down).
   virtual void abort() {}
+  // After every rank has returned from a failed collective call: clear the
+  // abort so the group can be used again (the caller restores a consistent
+  // state, e.g. by cfd_state_load; a symmetric failure such as divergence
+  // leaves every rank at the same point anyway).
+  virtual void reset() {}
 };
 
 // ---- RCCL ----
@@ -73,6 +97,7 @@ class LocalGroup {
   // throws std::runtime_error once the group is aborted (sticky)
   void barrier();
   void abort();
+  void reset();  // only while no rank is inside barrier()
   struct Slot {
     std::vector<Msg> posted;
     const void* gather_src = nullptr;

@@ -87,7 +87,6 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
-  if (topo.ws > 255) relax4 = false;  // u8 row lengths
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -507,7 +506,7 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   y = g + m1;
   resid_hist = y + m;
   binv = resid_hist + m;
-  ev_iter.resize(m);
+  ev_iter.resize(2);  // the two pinned residual slots (Solver::solve)
   for (auto& e : ev_iter) CFD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   fgmres_ready = true;
 }
@@ -1371,6 +1370,15 @@ void Solver::residual_into_v0_launch() {
   norm_launch(basis, 2, 1);
 }
 
+// complete the lagged FGMRES residual read, if one is pending (async_buffer.rs)
+void Solver::flush_inner() {
+  if (inner.pending < 0) return;
+  CFD_HIP(hipEventSynchronize(ev_iter[inner.pending]));
+  inner.last = h_pin[64 + inner.pending];
+  inner.has_last = true;
+  inner.pending = -1;
+}
+
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   const Range range("fgmres solve");
   cfd_linear_stats st{};
@@ -1429,31 +1437,30 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
       launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream);
+      // the residual estimate goes to one of two pinned slots, never the slot
+      // of a lagged read still pending (which may carry over from the previous
+      // iteration, restart or solve: the reader is never reset)
+      const int wslot = inner.pending == 0 ? 1 : 0;
       launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist,
-                         fixed ? nullptr : d_pin + 64, stream);
+                         fixed ? nullptr : d_pin + 64 + wslot, stream);
       check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
-      if (inner.pending >= 0) {
-        CFD_HIP(hipEventSynchronize(ev_iter[inner.pending]));
-        inner.last = h_pin[64 + inner.pending];
-        inner.has_last = true;
-        inner.pending = -1;
-      }
-      // k_norm_givens wrote resid_hist[j] into h_pin[64 + j]; the event orders the read
-      CFD_HIP(hipEventRecord(ev_iter[j], stream));
+      flush_inner();
+      // k_norm_givens wrote resid_hist[j] into h_pin[64 + wslot]; the event orders the read
+      CFD_HIP(hipEventRecord(ev_iter[wslot], stream));
       bool have = false;
       float check = 0.0f;
       if (lag == 0) {
-        CFD_HIP(hipEventSynchronize(ev_iter[j]));
-        inner.last = h_pin[64 + j];
+        CFD_HIP(hipEventSynchronize(ev_iter[wslot]));
+        inner.last = h_pin[64 + wslot];
         inner.has_last = true;
         have = true;
         check = inner.last;
       } else {
         have = inner.has_last;
         check = inner.last;
-        inner.pending = j;
+        inner.pending = wslot;
       }
       if (have && (total % 10 == 0 || check < tol * rhs_norm))
         log("FGMRES iter %u: residual = %s (target %s)\n", total, e2(check).c_str(), e2(tol * rhs_norm).c_str());
@@ -1466,12 +1473,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     launch_update_x(x, zvec, stride, y, basis_size, n, stream);
     check_launch("FGMRES solution update");
     if (converged) {  // async_reader.flush()
-      if (inner.pending >= 0) {
-        CFD_HIP(hipEventSynchronize(ev_iter[inner.pending]));
-        inner.last = h_pin[64 + inner.pending];
-        inner.has_last = true;
-        inner.pending = -1;
-      }
+      flush_inner();
       final_resid = inner.last;
       log("FGMRES restart %d: estimated residual = %s\n", outer + 1, e2(final_resid).c_str());
       break;

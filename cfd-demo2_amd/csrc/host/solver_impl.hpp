@@ -370,18 +370,19 @@ struct Solver {
   void save_state(const char* path);  // collective on a distributed solver
   void load_state(const char* path);
   uint64_t amg_level_digest(int li);  // FNV-1a over every byte of level li's device image
+  std::vector<uint64_t> allgather_u64(uint64_t mine);  // every rank's value (collective)
 
  private:
   void rotate();
   void prepare();
   void assemble();
   cfd_linear_stats solve();
+  void flush_inner();
   void ensure_fgmres();
   void ensure_amg();
   void build_amg_host();
   bool build_amg_device();  // false: a per-thread capacity overflowed on some rank (host path then)
   void set_amg_full_policy(AmgGpuLevel& G, int li);
-  std::vector<uint64_t> allgather_u64(uint64_t mine);  // every rank's value (collective)
   void precondition(int j, float* z);
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);

@@ -89,7 +89,13 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
     t.srow[N] = (uint32_t)t.scol.size();
   }
   t.ws = ws;
-  if (ws > 255) throw std::invalid_argument("cell with more than 255 neighbours");
+  // one validated width limit for every row layout: the coupled-matrix ELL
+  // header keeps a row's slots-in-use in 7 bits (kLgUsedMask), the scalar
+  // image and the Jacobi relaxation u8 lengths
+  if (ws > (int)kLgUsedMask)
+    throw std::invalid_argument("cell with more than " + std::to_string(kLgUsedMask - 1) +
+                                " neighbours (scalar row width " + std::to_string(ws) + " > " +
+                                std::to_string(kLgUsedMask) + ")");
   // ghosts: off-range neighbours, ascending global id
   t.ghost.clear();
   for (uint32_t c : t.scol)
@@ -171,16 +177,18 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
             }
         slot[q] = prev = s;
       }
+      // slots in use; the gap mask exists only for the typed layout (ws <= 8):
+      // untyped rows fill slots 0..len-1 and have no gaps
       uint32_t used = 0, on = 0;
       for (uint32_t q = 0; q < len; ++q) {
         t.tslot[a + q] = (uint8_t)slot[q];
-        on |= 1u << slot[q];
+        if (typed) on |= 1u << slot[q];
         used = (uint32_t)slot[q] + 1;
         t.tcol[(size_t)slot[q] * ld + li] = t.ell_col[(size_t)q * ld + li];
       }
-      const uint32_t gap = ((1u << used) - 1u) & ~on;
+      const uint32_t gap = typed ? ((1u << used) - 1u) & ~on : 0u;
       for (int r = 0; r < ws; ++r) {
-        if (on >> r & 1u) continue;
+        if (typed ? (on >> r & 1u) : (uint32_t)r < len) continue;
         const int32_t v = li < N ? (int32_t)li + t.tmode[r] : (int32_t)li;
         t.tcol[(size_t)r * ld + li] = std::min(std::max(v, vlo), vhi);
         const int64_t dd = (int64_t)t.tcol[(size_t)r * ld + li] - (int64_t)li;

@@ -325,6 +325,23 @@ cfd_status cfd_group_step(cfd_solver* const* handles, int32_t nranks);
  * self and an all-gather through the solver's transport; CFD_OK if the data
  * arrived intact.                                                           */
 cfd_status cfd_debug_rccl_selftest(int32_t hip_device);
+/* Transport of a distributed handle and its traffic since the last reset
+ * (bench.py prints these on a --gpus N line).                               */
+typedef struct {
+  int32_t transport;        /* 0 none (one rank), 1 RCCL, 2 in-process group, 3 host-staged */
+  int32_t comm_count;       /* RCCL: ncclCommCount; otherwise the rank count */
+  int32_t comm_rank;        /* RCCL: ncclCommUserRank; otherwise the rank */
+  int32_t device;           /* HIP device of this rank */
+  uint64_t exchanges;       /* grouped point-to-point calls (halos) */
+  uint64_t allgathers;      /* all-gather calls (reductions, replicated AMG levels) */
+  uint64_t bytes_sent;      /* point-to-point payload bytes this rank sent */
+  uint64_t bytes_gathered;  /* all-gather payload bytes this rank contributed */
+} cfd_comm_stats;
+cfd_status cfd_dist_comm_stats(cfd_solver* s, cfd_comm_stats* out, int32_t reset);
+/* In-process group failure path (test hook): every rank enters a collective
+ * except `fail_rank`, which fails first; the others must return an error
+ * instead of waiting forever, and the group must stay usable afterwards.     */
+cfd_status cfd_debug_group_fault(cfd_solver* const* handles, int32_t nranks, int32_t fail_rank);
 /* rank, rank count, owned global range [c0, c1), global cell count         */
 cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0,
                          uint32_t* c1, uint32_t* num_global_cells);

@@ -70,6 +70,61 @@ def strip(n, h=0.1):
         cell_faces=np.array([f for cf in cell_faces for f in cf], np.uint32))
 
 
+def wheel(k, r1=0.3, r2=1.0):
+    """A hub cell (regular k-gon, k internal faces) inside a ring of k sectors:
+    the hub's scalar row has k + 1 entries (the widest row a mesh can give
+    the layouts: topology rejects width > 127).  Sector outer faces are inlets
+    where the outward normal points left, outlets where it points right,
+    walls elsewhere."""
+    th = 2.0 * np.pi * np.arange(k + 1) / k
+    ci, si = np.cos(th), np.sin(th)
+    owner, nb, bt, area, nx, ny, fx, fy = [], [], [], [], [], [], [], []
+    n = k + 1  # cell 0 = hub, cell 1 + s = sector s
+    cell_faces = [[] for _ in range(n)]
+
+    def face(o, ngh, b, a, nxx, nyy, cx, cy):
+        f = len(owner)
+        owner.append(o), nb.append(ngh), bt.append(b), area.append(a)
+        nx.append(nxx), ny.append(nyy), fx.append(cx), fy.append(cy)
+        cell_faces[o].append(f)
+        if ngh != NONE:
+            cell_faces[ngh].append(f)
+
+    def poly(xs, ys):  # shoelace area and centroid
+        x2, y2 = np.roll(xs, -1), np.roll(ys, -1)
+        c = xs * y2 - x2 * ys
+        a = 0.5 * c.sum()
+        return a, ((xs + x2) * c).sum() / (6 * a), ((ys + y2) * c).sum() / (6 * a)
+
+    cx, cy, vol = [0.0] * n, [0.0] * n, [0.0] * n
+    vol[0], cx[0], cy[0] = poly(r1 * ci[:k], r1 * si[:k])
+    for s in range(k):
+        a, x, y = poly(np.array([r1 * ci[s], r2 * ci[s], r2 * ci[s + 1], r1 * ci[s + 1]]),
+                       np.array([r1 * si[s], r2 * si[s], r2 * si[s + 1], r1 * si[s + 1]]))
+        vol[1 + s], cx[1 + s], cy[1 + s] = a, x, y
+    for s in range(k):  # hub edges: hub -> sector s
+        mx, my = 0.5 * r1 * (ci[s] + ci[s + 1]), 0.5 * r1 * (si[s] + si[s + 1])
+        ln = np.hypot(mx, my)
+        face(0, 1 + s, 0, 2 * r1 * np.sin(np.pi / k), mx / ln, my / ln, mx, my)
+    for s in range(k):  # radial edge at th[s]: sector s-1 -> sector s
+        o = 1 + (s - 1) % k
+        face(o, 1 + s, 0, r2 - r1, -si[s], ci[s], 0.5 * (r1 + r2) * ci[s], 0.5 * (r1 + r2) * si[s])
+    for s in range(k):  # outer boundary
+        mx, my = 0.5 * r2 * (ci[s] + ci[s + 1]), 0.5 * r2 * (si[s] + si[s + 1])
+        ln = np.hypot(mx, my)
+        b = 1 if mx / ln < -0.5 else (2 if mx / ln > 0.5 else 3)
+        face(1 + s, NONE, b, 2 * r2 * np.sin(np.pi / k), mx / ln, my / ln, mx, my)
+    offs = np.zeros(n + 1, dtype=np.uint32)
+    for i in range(n):
+        offs[i + 1] = offs[i] + len(cell_faces[i])
+    return ArrayMesh(
+        face_owner=np.array(owner, np.uint32), face_neighbor=np.array(nb, np.uint32),
+        face_boundary=np.array(bt, np.uint32), face_area=np.array(area), face_nx=np.array(nx),
+        face_ny=np.array(ny), face_cx=np.array(fx), face_cy=np.array(fy),
+        cell_cx=np.array(cx), cell_cy=np.array(cy), cell_vol=np.array(vol), cell_face_offsets=offs,
+        cell_faces=np.array([f for cf in cell_faces for f in cf], np.uint32))
+
+
 def broken(kind):
     m = strip(4)
     a = {k: v.copy() for k, v in m.arrays().items()}

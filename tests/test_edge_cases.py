@@ -9,7 +9,7 @@ import pytest
 from cfd2_amd import _ffi, default_config, dist_plan
 from cfd2_amd.solver import _bind
 from tests.oracle_py import OracleSolver
-from tests.synthetic import broken, strip
+from tests.synthetic import broken, strip, wheel
 
 
 def _create_status(mesh, **cfg):
@@ -27,6 +27,44 @@ def test_broken_meshes_rejected_before_device_use(kind):
     st, msg = _create_status(broken(kind))
     assert st == 1, (st, msg)
     assert msg
+
+
+def test_row_width_limit():
+    """A cell with 127 neighbours (scalar row width 128) exceeds the 7-bit
+    slots-in-use field of the coupled-matrix ELL header: rejected with a
+    status before any device use, never silently truncated.  126 neighbours
+    (width 127) pass the topology check (the GPU parity of wide rows is
+    tests/test_gpu_edge.py)."""
+    st, msg = _create_status(wheel(127))
+    assert st == 1 and "neighbours" in msg, (st, msg)
+    st, msg = _create_status(wheel(126))
+    assert "neighbours" not in msg, msg  # fails later, at device use, on a GPU-less host
+
+
+@pytest.mark.parametrize("k", [5, 40, 100])
+def test_oracle_wheel_mesh(k):
+    """The wheel mesh is a valid FV mesh: closed cells, and the oracle steps it."""
+    m = wheel(k)
+    a = m.arrays()
+    # every cell closed: sum of area * outward normal = 0
+    for c in range(m.num_cells()):
+        fs = a["cell_faces"][a["cell_face_offsets"][c]:a["cell_face_offsets"][c + 1]]
+        sgn = np.where(a["face_owner"][fs] == c, 1.0, -1.0)
+        sx = (sgn * a["face_area"][fs] * a["face_nx"][fs]).sum()
+        sy = (sgn * a["face_area"][fs] * a["face_ny"][fs]).sum()
+        assert abs(sx) < 1e-12 and abs(sy) < 1e-12, c
+    s = OracleSolver(m)
+    s.set_dt(0.01)
+    s.set_viscosity(0.01)
+    s.set_density(1.0)
+    s.set_precond_type(1)
+    s.initialize_history()
+    c = s.constants
+    c.time = 0.1
+    s.constants = c
+    for _ in range(2):
+        s.step()
+    assert np.all(np.isfinite(s.get_u())) and np.abs(s.get_u()).max() > 0
 
 
 def test_bad_config_rejected():

@@ -136,25 +136,42 @@ def test_coupled_schemes_parity(scheme, time_scheme):
 
 
 def test_divergence_channel_obstacle_gpu():
-    """tests/gpu_divergence_test.rs (shortened to 20 steps): adaptive dt, max|u| <= 20."""
+    """tests/gpu_divergence_test.rs:6-92 at its own length: up to 200 adaptive
+    steps (CFL 0.5 on the 0.025 cell size, dt clamped to [1e-5, 0.1]) with the
+    should_stop break, max|u| <= 20 checked every 10 steps as the reference
+    does -- and GPU == oracle bit-exact after every step (same host-side dt
+    sequence: both solvers' dt comes from the GPU's velocities, which equal
+    the oracle's)."""
     mesh = channel_obstacle()
-    g = GpuSolver(mesh)
-    g.set_dt(0.01)
-    g.set_viscosity(0.01)
-    g.set_density(1.0)
-    g.set_scheme(0)
+    g, o = _pair(mesh)
     a = mesh.arrays()
     u = np.zeros((mesh.num_cells(), 2))
     u[a["cell_cx"] < 0.025, 0] = 1.0
-    g.set_u(u)
-    for _ in range(20):
+    for s in (g, o):
+        s.set_dt(0.01)
+        s.set_viscosity(0.01)
+        s.set_density(1.0)
+        s.set_scheme(0)
+        s.set_u(u)
+    steps = 0
+    for step in range(200):
         uu = g.get_u()
         vmax = float(np.sqrt((uu ** 2).sum(1)).max())
         if vmax > 1e-6:
-            g.set_dt(float(np.clip(0.5 * 0.025 / vmax, 1e-5, 0.1)))
+            dt = float(np.clip(0.5 * 0.025 / vmax, 1e-5, 0.1))
+            g.set_dt(dt)
+            o.set_dt(dt)
         g.step()
-        assert not g.should_stop or g.degenerate_count <= 10
-        assert vmax <= 20.0 and np.isfinite(vmax)
+        o.step()
+        steps += 1
+        _assert_same_fields(g, o, f"gpu_divergence_test step {step}")
+        _assert_same_info(g, o, f"gpu_divergence_test step {step}")
+        if g.should_stop:
+            assert g.degenerate_count <= 10, "Solver stopped due to degenerate solution!"
+            break
+        if step % 10 == 0:
+            assert vmax <= 20.0 and np.isfinite(vmax), f"Divergence detected at step {step}"
+    assert steps >= 10
 
 
 @pytest.mark.parametrize("lag", [0, 1])
@@ -297,9 +314,9 @@ def _scalar_csr_fast(mesh):
 
 def test_reproduce_divergence_gpu():
     """tests/reproduce_divergence.rs: BackwardsStep h=0.025, water, alpha 0.7/0.3,
-    adaptive dt (CFL 0.2, growth <= 1.2, dt <= 0.1), 50 steps: outer residuals
-    finite and < 1e10.  The first 10 steps are also checked bit-exact vs the
-    oracle (same host-side dt sequence)."""
+    adaptive dt (CFL 0.2, growth <= 1.2, dt <= 0.1), all 50 steps with the
+    should_stop break: outer residuals finite and < 1e10, and GPU == oracle
+    bit-exact after every step (same host-side dt sequence)."""
     from tests.meshes import STEP
     from cfd2_amd.mesh import generate_cut_cell_mesh
     mesh = generate_cut_cell_mesh(STEP, 0.025, 0.025, 1.2, (3.5, 1.0))
@@ -320,8 +337,7 @@ def test_reproduce_divergence_gpu():
         s.set_dt(0.001)
         dts[id(s)] = np.float32(0.001)
     for step in range(50):
-        active = sols if step < 10 else [g]
-        for s in active:
+        for s in sols:
             s.step()
             assert not (s.should_stop and s.degenerate_count > 10)
             i = s.step_info()
@@ -335,8 +351,10 @@ def test_reproduce_divergence_gpu():
                 new_dt = min(new_dt, dt * 1.2, 0.1)
                 s.set_dt(new_dt)
                 dts[id(s)] = np.float32(new_dt)
-        if step < 10:
-            _assert_same_fields(g, o, f"reproduce_divergence step {step}")
+        _assert_same_fields(g, o, f"reproduce_divergence step {step}")
+        _assert_same_info(g, o, f"reproduce_divergence step {step}")
+        if g.should_stop:
+            break
 
 
 def test_fine_mesh_obstacle_gpu():
