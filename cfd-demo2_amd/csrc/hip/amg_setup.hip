@@ -29,17 +29,17 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 
 // entry k of fine row i: ELL slot-major (level 0: the scalar pressure matrix
 // as assembled) or CSR (coarse levels produced by k_galerkin)
-template <bool ELL>
+template <int MODE>  // SetupMatrix::ell
 struct Rows {
   SetupMatrix m;
   __device__ __forceinline__ uint32_t len(uint32_t i) const {
-    if constexpr (ELL)
+    if constexpr (MODE == 1)
       return m.len[i];
     else
       return m.rowptr[i + 1] - m.rowptr[i];
   }
   __device__ __forceinline__ size_t at(uint32_t i, uint32_t k) const {
-    if constexpr (ELL)
+    if constexpr (MODE == 1)
       return (size_t)k * m.ld + i;
     else
       return (size_t)m.rowptr[i] + k;
@@ -50,9 +50,9 @@ struct Rows {
 
 // FILL = false: cnt[I] = number of distinct coarse columns of row I.
 // FILL = true: the sorted row written at rowptr_c[I].  `agg` is indexed by
-// the (signed local) fine column: on a distributed level it holds the global
-// aggregate ids of the owned rows and of the ghosts (halo-exchanged).
-template <bool ELL, bool FILL>
+// the fine column (modes 0 / 1); member rows (mode 2) carry the aggregate of
+// every entry instead.
+template <int MODE, bool FILL>
 __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32_t* __restrict__ agg,
                                                      const uint32_t* __restrict__ r_row,
                                                      const uint32_t* __restrict__ r_col, uint32_t nc,
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32
                                                      uint32_t* overflow) {
   const uint32_t I = blockIdx.x * kBlock + threadIdx.x;
   if (I >= nc) return;
-  const Rows<ELL> a{A};
+  const Rows<MODE> a{A};
   const uint32_t k0 = r_row[I], m = r_row[I + 1] - k0;
   if (m > (uint32_t)kSetupMaxMembers) {
     atomicOr(overflow, 1u);
@@ -84,12 +84,17 @@ __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32
       if (cur[t] < end[t]) jmin = min(jmin, a.col(mem[t], cur[t]));
     if (jmin == INT32_MAX) break;
     float ra = 0.0f;  // RA[I, jmin], members in ascending order (first touch: 0 + ...)
+    uint32_t J = 0;
+    bool first = true;
     for (uint32_t t = 0; t < m; ++t)
       if (cur[t] < end[t] && a.col(mem[t], cur[t]) == jmin) {
+        if constexpr (MODE == 2)
+          if (first) J = A.eagg[a.at(mem[t], cur[t])];
+        first = false;
         ra += 1.0f * a.val(mem[t], cur[t]);
         ++cur[t];
       }
-    const uint32_t J = agg[jmin];
+    if constexpr (MODE != 2) J = agg[jmin];
     uint32_t q = 0;
     while (q < nl && cj[q] != J) ++q;
     if (q == nl) {
@@ -130,7 +135,7 @@ __global__ void __launch_bounds__(kBlock) k_galerkin(SetupMatrix A, const uint32
 // ELL slot-major order (row order kept), diagonal value and rank, smoother
 // diagonal (amg.wgsl:46: 1.0 when |diag| < 1e-14); padding slots / rows hold
 // value 0 and the row's own column.  Same bytes as the host level_image.
-template <bool ELL>
+template <int MODE>
 __global__ void __launch_bounds__(kBlock) k_amg_pack(SetupMatrix A, uint32_t n, uint32_t st, int w, int use16,
                                                      float* __restrict__ val, int16_t* __restrict__ col16,
                                                      int32_t* __restrict__ col32, uint8_t* __restrict__ len,
@@ -138,7 +143,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_pack(SetupMatrix A, uint32_t n, 
                                                      float* __restrict__ de) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= st) return;
-  const Rows<ELL> a{A};
+  const Rows<MODE> a{A};
   uint32_t off = 0, dr = 0;
   float diag = 1.0f, raw = 0.0f;
   if (i < n) {
@@ -179,38 +184,51 @@ __global__ void __launch_bounds__(kBlock) k_amg_pack(SetupMatrix A, uint32_t n, 
   de[i] = diag;
 }
 
+__global__ void __launch_bounds__(kBlock) k_gather_f32(const float* __restrict__ src, const uint32_t* __restrict__ idx,
+                                                       uint32_t n, float* __restrict__ dst) {
+  const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+  if (k < n) dst[k] = src[idx[k]];
+}
+
+template <bool FILL>
+void galerkin_mode(const SetupMatrix& A, const uint32_t* agg, const uint32_t* r_row, const uint32_t* r_col,
+                   uint32_t nc, uint32_t* cnt, const uint32_t* rowptr_c, uint32_t* col_c, float* val_c,
+                   uint32_t* overflow, hipStream_t s) {
+  if (A.ell == 1)
+    hipLaunchKernelGGL((k_galerkin<1, FILL>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col, nc, cnt,
+                       rowptr_c, col_c, val_c, overflow);
+  else if (A.ell == 2)
+    hipLaunchKernelGGL((k_galerkin<2, FILL>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col, nc, cnt,
+                       rowptr_c, col_c, val_c, overflow);
+  else
+    hipLaunchKernelGGL((k_galerkin<0, FILL>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col, nc, cnt,
+                       rowptr_c, col_c, val_c, overflow);
+}
+
 }  // namespace
+
+void launch_gather_f32(const float* src, const uint32_t* idx, uint32_t n, float* dst, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_gather_f32, dim3(grid_for(n)), dim3(kBlock), 0, s, src, idx, n, dst);
+}
 
 void launch_galerkin(const SetupMatrix& A, const uint32_t* agg, const uint32_t* r_row, const uint32_t* r_col,
                      uint32_t nc, uint32_t* cnt, const uint32_t* rowptr_c, uint32_t* col_c, float* val_c,
                      uint32_t* overflow, hipStream_t s) {
   if (!nc) return;
-  const bool fill = rowptr_c != nullptr;
-  if (A.ell) {
-    if (fill)
-      hipLaunchKernelGGL((k_galerkin<true, true>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col, nc,
-                         cnt, rowptr_c, col_c, val_c, overflow);
-    else
-      hipLaunchKernelGGL((k_galerkin<true, false>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col, nc,
-                         cnt, rowptr_c, col_c, val_c, overflow);
-  } else {
-    if (fill)
-      hipLaunchKernelGGL((k_galerkin<false, true>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col,
-                         nc, cnt, rowptr_c, col_c, val_c, overflow);
-    else
-      hipLaunchKernelGGL((k_galerkin<false, false>), dim3(grid_for(nc)), dim3(kBlock), 0, s, A, agg, r_row, r_col,
-                         nc, cnt, rowptr_c, col_c, val_c, overflow);
-  }
+  if (rowptr_c != nullptr)
+    galerkin_mode<true>(A, agg, r_row, r_col, nc, cnt, rowptr_c, col_c, val_c, overflow, s);
+  else
+    galerkin_mode<false>(A, agg, r_row, r_col, nc, cnt, rowptr_c, col_c, val_c, overflow, s);
 }
 
 void launch_amg_pack(const SetupMatrix& A, uint32_t n, uint32_t st, int w, int use16, float* val, int16_t* col16,
                      int32_t* col32, uint8_t* len, uint8_t* drank, float* dv, float* de, hipStream_t s) {
   if (!st) return;
-  if (A.ell)
-    hipLaunchKernelGGL(k_amg_pack<true>, dim3(grid_for(st)), dim3(kBlock), 0, s, A, n, st, w, use16, val, col16,
+  if (A.ell == 1)
+    hipLaunchKernelGGL(k_amg_pack<1>, dim3(grid_for(st)), dim3(kBlock), 0, s, A, n, st, w, use16, val, col16,
                        col32, len, drank, dv, de);
   else
-    hipLaunchKernelGGL(k_amg_pack<false>, dim3(grid_for(st)), dim3(kBlock), 0, s, A, n, st, w, use16, val, col16,
+    hipLaunchKernelGGL(k_amg_pack<0>, dim3(grid_for(st)), dim3(kBlock), 0, s, A, n, st, w, use16, val, col16,
                        col32, len, drank, dv, de);
 }
 

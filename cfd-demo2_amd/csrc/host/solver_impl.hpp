@@ -188,6 +188,8 @@ struct LagReader {  // async_buffer.rs restated as a deterministic lag model
   int pending = -1;
 };
 
+struct AmgSetupLevel;  // amg_device.cpp
+
 struct Solver {
   cfd_config cfg{};
   int device = 0;
@@ -317,19 +319,37 @@ struct Solver {
   // so a rebuild from new values re-runs just the Galerkin fill and the level
   // packing over the kept structure -- the same bytes as a full rebuild.
   struct AmgRefreshLevel {
-    SetupMatrix fine{};                  // the level as the setup kernels read it
+    SetupMatrix fine{};                  // the level as the setup kernels read it (pack source)
     bool has_coarse = false;
-    const uint32_t* gal_agg = nullptr;   // aggregate id per (owned or ghost) fine column
+    const uint32_t* gal_agg = nullptr;   // aggregate id per fine column (one GPU / replicated)
+    const uint32_t* r_row = nullptr;     // R over the Galerkin input rows
+    const uint32_t* r_col = nullptr;
     uint32_t nagg_own = 0;
     const uint32_t* rowptr_c = nullptr;  // this rank's coarse rows (fill output)
     uint32_t* col_c = nullptr;
     float* val_c = nullptr;
     size_t nnz_own = 0;
+    // distributed level (build_amg_device_dist): the Galerkin input is the
+    // member-row matrix `mem`; its values are gathered from the level's values
+    // (own entries, msrc) and received from the ranks owning the imported rows
+    // (val_msgs, whose send side is gathered through esrc into ebuf)
+    bool dist = false;
+    SetupMatrix mem{};
+    const float* src_val = nullptr;
+    const uint32_t* msrc = nullptr;
+    const uint32_t* esrc = nullptr;
+    uint32_t n_own_e = 0, n_exp_e = 0;
+    float* ebuf = nullptr;
+    std::vector<Msg> val_msgs;
+    // last distributed level: the replicated level's values, all-gathered in place
+    float* rep_val = nullptr;
+    std::vector<size_t> rep_off;
   };
   std::vector<AmgRefreshLevel> amg_refresh;
   uint32_t* amg_setup_flag = nullptr;  // k_galerkin overflow flag (amg_arena)
   bool amg_refresh_pending = false;    // refresh at the next AMG solve
   void refresh_amg();
+  void member_values(const AmgRefreshLevel& F);
   // host-side state
   cfd_constants constants{};
   cfd_step_info info{};
@@ -382,6 +402,9 @@ struct Solver {
   void ensure_amg();
   void build_amg_host();
   bool build_amg_device();  // false: a per-thread capacity overflowed on some rank (host path then)
+  bool build_amg_device_dist();
+  bool device_levels(AmgSetupLevel& cur, int li0, const std::vector<uint64_t>& part0);
+  std::vector<std::vector<uint32_t>> allgatherv_u32(const std::vector<uint32_t>& mine);  // collective
   void set_amg_full_policy(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
   void v_cycle();
@@ -476,7 +499,6 @@ struct Solver {
   RedSrc combine(const float* part, int nvec);
   RedSrcD combine_d(const double* part, int nvec);
   void make_plan_buffers(HaloPlan& p, int max_comps);
-  void build_dist_amg(std::vector<AmgHostLevel>& H);
 };
 
 }  // namespace cfd2

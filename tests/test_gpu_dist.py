@@ -140,7 +140,7 @@ def test_group_hierarchy_is_the_global_one(replicate_rows):
     for r in range(4):
         pr, dr = g.ranks[r].amg_setup_info()
         lv = g.ranks[r].amg_levels()
-        assert pr == 1 and len(lv) == len(levels1)
+        assert pr == 2 and len(lv) == len(levels1)
         nrep = [i for i, (a, b) in enumerate(zip(lv, levels1)) if a == b and a[0] <= 4096]
         assert nrep, "no replicated level"
         for i in nrep:
@@ -193,3 +193,37 @@ def test_group_variants_parity(env, replicate_rows, monkeypatch):
     replicate_rows(50)
     mesh = backwards_step()
     _three_way(mesh, 3, dict(fixed_outer=3, fixed_inner=10), lambda s: _setup_amg_test(s, mesh, 1), 3, str(env))
+
+
+@pytest.mark.parametrize("nranks,rep,which", [(4, 4096, "bench_100k"), (3, 50, "amg_test"), (8, 4096, "c1")])
+def test_group_device_setup_equals_host_setup(nranks, rep, which, replicate_rows, monkeypatch):
+    """The distributed DEVICE setup (aggregation pipeline over the ranks,
+    member rows of straddling aggregates imported from their owners, Galerkin
+    and packing on each rank's GPU) builds every rank's level images byte for
+    byte as the host setup of the all-gathered global matrix does: equal
+    per-rank, per-level digests, then equal fields after two steps."""
+    replicate_rows(rep)
+    mesh = {"bench_100k": lambda: bench_mesh(0.0055, 30), "amg_test": backwards_step,
+            "c1": lambda: bench_mesh(0.001723, 100)}[which]()
+    cfg = default_config(fixed_outer=1, fixed_inner=6)
+    groups = {}
+    for path in ("host", "device"):
+        monkeypatch.setenv("CFD_AMG_SETUP", path)
+        g = GpuGroup(mesh, nranks, config=cfg)
+        _bench_physics(g, 0.05)
+        g.step()
+        groups[path] = g
+    monkeypatch.delenv("CFD_AMG_SETUP")
+    h, d = groups["host"], groups["device"]
+    for r in range(nranks):
+        ph, dh = h.ranks[r].amg_setup_info()
+        pd, dd = d.ranks[r].amg_setup_info()
+        assert (ph, pd) == (1, 2)
+        assert h.ranks[r].amg_levels() == d.ranks[r].amg_levels(), f"rank {r}"
+        assert dh == dd, f"rank {r}: level digests differ at {[i for i, (a, b) in enumerate(zip(dh, dd)) if a != b]}"
+    d.step()
+    h.step()
+    _assert_same_fields(d, h, f"{which} R={nranks} device vs host setup")
+    _assert_same_info(d, h, f"{which} R={nranks} device vs host setup")
+    h.close()
+    d.close()
