@@ -57,6 +57,8 @@ def _bind():
                                  C.POINTER(C.c_uint64)]
     L.cfd_step_algorithmic_bytes.argtypes = [_vp]
     L.cfd_step_algorithmic_bytes.restype = C.c_double
+    L.cfd_smoother_layout_bytes.argtypes = [_vp]
+    L.cfd_smoother_layout_bytes.restype = C.c_double
     L.cfd_debug_buffer_len.argtypes = [_vp, C.c_int32]
     L.cfd_debug_buffer_len.restype = C.c_size_t
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
@@ -297,6 +299,10 @@ class GpuSolver:
 
     def step_algorithmic_bytes(self) -> float:
         return float(_ffi.lib().cfd_step_algorithmic_bytes(self._h))
+
+    def smoother_layout_bytes(self) -> float:
+        """Layout-true bytes of one level-0 smoother sweep (cfd_smoother_layout_bytes)."""
+        return float(_ffi.lib().cfd_smoother_layout_bytes(self._h))
 
     def debug_buffer(self, bid: int) -> np.ndarray:
         n = _ffi.lib().cfd_debug_buffer_len(self._h, bid)

@@ -296,8 +296,7 @@ bool Solver::build_amg_device_dist() {
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
-  const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
-  const uint64_t rep = ev ? std::strtoull(ev, nullptr, 10) : 262144u;
+  const uint64_t rep = amg_replicate_rows();
   levels.clear();
   amg_refresh.clear();
   amg_g = 0;

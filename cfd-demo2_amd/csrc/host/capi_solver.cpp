@@ -241,6 +241,7 @@ cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path,
     if (digest) *digest = s->s->amg_level_digest(level);
   });
 }
+double cfd_smoother_layout_bytes(const cfd_solver* s) { return (s && s->s) ? s->s->smoother_layout_bytes() : 0.0; }
 double cfd_step_algorithmic_bytes(const cfd_solver* s) {
   return (s && s->s) ? s->s->algorithmic_step_bytes() : 0.0;
 }

@@ -605,7 +605,7 @@ void level_image(const HostCsr& A, uint64_t r0, uint32_t n, Rel rel, AmgGpuLevel
 // distributed rank all-gathers the scalar matrix, builds the GLOBAL hierarchy
 // (the one a single GPU builds, so results do not depend on the rank count)
 // and keeps its rows of the levels with more than CFD_AMG_REPLICATE_ROWS rows
-// (default 262144); the small levels are replicated on every rank.
+// (default kAmgReplicateRowsDefault); the small levels are replicated on every rank.
 // Unconditional slot loads (kernels.hip gather_group) on level 0 (the face
 // stencil: rows fill the ELL width) and on latency-bound small levels;
 // predicated loads on the big coarse levels, whose row lengths vary (same-box
@@ -690,8 +690,7 @@ void Solver::build_amg_host() {
   // distributed levels [0, amg_g): the rest are replicated (all of them on one GPU)
   amg_g = 0;
   if (dist()) {
-    const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
-    const uint64_t rep = ev ? std::strtoull(ev, nullptr, 10) : 262144u;
+    const uint64_t rep = amg_replicate_rows();
     amg_g = L;
     for (int li = 1; li < L; ++li)
       if (H[li].A.rows <= rep) {
@@ -1845,6 +1844,19 @@ double Solver::smoother_bytes() const {
   if (levels.empty()) return 0.0;
   const double n = levels[0].dev.n, nnz = (double)levels[0].nnz;
   return 4.0 * (n + 1.0) + 8.0 * nnz + 12.0 * n;
+}
+
+// Layout-true bytes of one level-0 sweep of k_amg_smooth: what the kernel
+// must move in the AmgLevelDev image -- the u8 row lengths, every ELL slot's
+// value and column (16-bit delta or i32) over the padded rows, b, x, the
+// smoother diagonal and x_out (4 B each per row; the x gathers at the
+// neighbours counted once, as SURVEY §8(d) counts them).  At C2 (w = 4,
+// 16-bit deltas) 41 B per row against the reference format's 56.
+double Solver::smoother_layout_bytes() const {
+  if (levels.empty()) return 0.0;
+  const AmgLevelDev& d = levels[0].dev;
+  const double st = d.stride, n = d.n;
+  return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n;
 }
 
 double Solver::algorithmic_step_bytes() const {

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -189,6 +190,17 @@ struct LagReader {  // async_buffer.rs restated as a deterministic lag model
 };
 
 struct AmgSetupLevel;  // amg_device.cpp
+
+// Distributed runs replicate the AMG levels with at most this many GLOBAL rows
+// on every rank (CFD_AMG_REPLICATE_ROWS overrides).  DESIGN §7 "Latency
+// budget": below ~1 M rows a replicated level's redundant kernels plus one
+// all-gather of its rhs cost less than the four un-overlapped halos per
+// V-cycle that keeping it row-partitioned costs (C4: level 4, 650 k rows).
+constexpr uint64_t kAmgReplicateRowsDefault = 1u << 20;
+inline uint64_t amg_replicate_rows() {
+  const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
+  return ev ? std::strtoull(ev, nullptr, 10) : kAmgReplicateRowsDefault;
+}
 
 struct Solver {
   cfd_config cfg{};
@@ -386,6 +398,7 @@ struct Solver {
   void debug_buffer(int id, float* out);
   double algorithmic_step_bytes() const;
   double smoother_bytes() const;
+  double smoother_layout_bytes() const;
   // checkpoint / resume (checkpoint.cpp, cfd_state_file_header)
   void save_state(const char* path);  // collective on a distributed solver
   void load_state(const char* path);

@@ -268,6 +268,12 @@ cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* ro
  * (matrix, diagonal, P, R) -- host and device setups must agree bit-for-bit.
  * Debug/parity only; not part of the reference surface.                     */
 cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path, uint64_t* digest);
+/* Layout-true bytes of one level-0 smoother sweep: the minimum the kernel
+ * moves in this library's level image (u8 lengths, ELL values + 16/32-bit
+ * columns, b, x, diagonal, x_out); the roofline of record divides this by
+ * the measured sweep time (cfd_profile_smoother's bytes are the reference
+ * CSR format's count).                                        */
+double cfd_smoother_layout_bytes(const cfd_solver* s);
 /* Algorithmic bytes of one step under the fixed schedule.    */
 double cfd_step_algorithmic_bytes(const cfd_solver* s);
 
