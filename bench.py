@@ -375,6 +375,7 @@ def main():
         solver.num_cells = solver.ranks[0].num_cells
         solver.profile_smoother = solver.ranks[0].profile_smoother
         solver.smoother_layout_bytes = solver.ranks[0].smoother_layout_bytes
+        solver.step_layout_bytes = solver.ranks[0].step_layout_bytes
         solver.step_algorithmic_bytes = solver.ranks[0].step_algorithmic_bytes
     else:
         solver = GpuSolver(mesh, config=cfg, device=0)
@@ -463,6 +464,7 @@ def main():
     achieved = layout_bytes / sm_avg_s / 1e9 if sm_n else 0.0
     achieved_ref = sm_bytes / sm_avg_s / 1e9 if sm_n else 0.0
     step_bytes = solver.step_algorithmic_bytes()
+    step_layout = solver.step_layout_bytes()
     traffic, traffic_src = load_traffic(args.round, args.config, world if not inproc else args.inproc_ranks)
     counter_gbs = traffic / sm_avg_s / 1e9 if (traffic and sm_n) else None
     if world > 1:
@@ -540,6 +542,14 @@ def main():
         # sum): this layout moves ~45 % less (step_counter_traffic below is the
         # measured traffic), so count / step time is not an HBM rate
         "step_reference_format_bytes": step_bytes,
+        # layout-true bytes of one step (this rank): each kernel's minimum
+        # traffic in this library's layouts x its launches; a lower bound of
+        # the step's HBM traffic, so its rate is a lower bound of the achieved one
+        "step_layout_bytes": {
+            "bytes_per_step": step_layout,
+            "gbs": step_layout / (ms_per_step / 1e3) / 1e9,
+            "frac": step_layout / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS,
+        },
         "linear_iterations_last_step": int(info.total_linear_iterations),
     }
     st = load_step_traffic(args.round, args.config, world if not inproc else args.inproc_ranks)

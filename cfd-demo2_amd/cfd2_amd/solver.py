@@ -59,6 +59,8 @@ def _bind():
     L.cfd_step_algorithmic_bytes.restype = C.c_double
     L.cfd_smoother_layout_bytes.argtypes = [_vp]
     L.cfd_smoother_layout_bytes.restype = C.c_double
+    L.cfd_step_layout_bytes.argtypes = [_vp]
+    L.cfd_step_layout_bytes.restype = C.c_double
     L.cfd_debug_buffer_len.argtypes = [_vp, C.c_int32]
     L.cfd_debug_buffer_len.restype = C.c_size_t
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
@@ -299,6 +301,10 @@ class GpuSolver:
 
     def step_algorithmic_bytes(self) -> float:
         return float(_ffi.lib().cfd_step_algorithmic_bytes(self._h))
+
+    def step_layout_bytes(self) -> float:
+        """Layout-true bytes of one fixed-schedule step (cfd_step_layout_bytes)."""
+        return float(_ffi.lib().cfd_step_layout_bytes(self._h))
 
     def smoother_layout_bytes(self) -> float:
         """Layout-true bytes of one level-0 smoother sweep (cfd_smoother_layout_bytes)."""

@@ -2068,6 +2068,67 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
     cx[stride_c + (g - glo)] = 0.0f;
 }
 
+// Residual (amg.wgsl:80-111) and restriction (:114-120) of a single-GPU or
+// replicated level in one kernel: a block owns aggregates [I0, I1) (L.rr_agg
+// per block); its threads compute the residuals of those aggregates' members,
+// rows r_col[p] for p in [r_row[I0], r_row[I1]), one row per thread, into
+// LDS in member order; then thread t sums aggregate I0 + t's members in
+// ascending order.  Every row's residual accumulates as in k_amg_residual
+// (slots below the diagonal's rank, the diagonal, the rest) and every coarse
+// value as in k_amg_restrict (0 + r_1 + r_2 ...): the same f32 operations.
+// Saves the residual vector's store and the restriction's gathers of it, and
+// one launch per level.  REV: top-down, after the bottom-up pre-smoother.
+template <bool D16>
+__global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const float* __restrict__ x,
+                                                            const float* __restrict__ b, float* __restrict__ cb,
+                                                            float* __restrict__ cx, float* __restrict__ sm_out,
+                                                            const float* __restrict__ sm_de) {
+  __shared__ float rl[kRRCap];
+  const uint32_t I0 = xcd_block<CFD_REV_RESIDUAL>() * L.rr_agg;
+  if (I0 >= L.nc) return;
+  const uint32_t I1 = min(I0 + L.rr_agg, L.nc);
+  const uint32_t p0 = L.r_row[I0], p1 = L.r_row[I1];
+  const uint32_t w = (uint32_t)max(L.w, 1);
+  for (uint32_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
+    const uint32_t f = L.r_col[p];
+    const uint32_t len = L.len[f], dr = L.drank[f];
+    const float xf = x[f], dvf = L.dv[f];
+    float ax = 0.0f;
+    uint32_t r0 = 0;
+    for (; r0 < len; r0 += 4) {
+      float v[4], xg[4];
+      int c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t off = (size_t)min(r0 + u, w - 1u) * L.stride + f;
+        v[u] = L.val[off];
+        c[u] = D16 ? (int)f + (int)L.col16[off] : L.col32[off];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xg[u] = x[c[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t r = r0 + u;
+        if (r == dr) ax += dvf * xf;
+        if (r < len) ax += v[u] * xg[u];
+      }
+    }
+    if (dr >= r0) ax += dvf * xf;  // a diagonal ranked after every visited slot comes last
+    rl[p - p0] = b[f] - ax;
+  }
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  if (I0 + t >= I1) return;
+  const uint32_t I = I0 + t;
+  float sum = 0.0f;
+  for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * rl[k - p0];
+  cb[I] = sum;
+  if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
+    sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
+  else
+    cx[I] = 0.0f;
+}
+
 // prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread.
 // agg is a signed local index on a distributed level (aggregates seeded on a
 // lower rank are ghosts of xc below 0).
@@ -2674,6 +2735,15 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float*
   if (n)
     hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
                        sm_out, sm_de, I0, I1);
+}
+void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* cb, float* cx,
+                            float* sm_out, const float* sm_de, hipStream_t s) {
+  if (!L.nc || !L.rr_agg) return;
+  const unsigned nb = (unsigned)((L.nc + L.rr_agg - 1) / L.rr_agg);
+  if (L.use16)
+    hipLaunchKernelGGL(k_amg_resrestrict<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
+  else
+    hipLaunchKernelGGL(k_amg_resrestrict<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1) {
   if (f1 == 0) f1 = L.n;

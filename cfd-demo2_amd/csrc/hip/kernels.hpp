@@ -228,7 +228,11 @@ struct AmgLevelDev {
   // load instead of r_row -> r_col); -1 pads, r_m4[I].w < -1 flags an
   // aggregate with more than 4 members (the rest read through r_row / r_col)
   const int4* r_m4;
+  // k_amg_resrestrict: aggregates per block (0: the level keeps the separate
+  // residual + restriction kernels); every block's members fit kRRCap
+  uint32_t rr_agg;
 };
+constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
 
 // Halo pack (distributed): up to 8 fields packed per launch.
 struct PackField {
@@ -348,6 +352,11 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s);
 // fine rows [f0, f1) (multiples of 4 but f1 = L.n; f1 = 0: all)
+// residual + restriction fused (k_amg_resrestrict; L.rr_agg > 0, replicated
+// or single-GPU level): coarse_b = R (b - A x), coarse_x cleared or the
+// coarse zero-x pre-smoother written to sm_out (as launch_amg_restrict)
+void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* coarse_b, float* coarse_x,
+                            float* sm_out, const float* sm_de, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,
                         uint32_t f1 = 0);
 // Sets the tail kernels' dynamic-LDS attribute on `device` (once per device,

@@ -242,6 +242,7 @@ cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path,
   });
 }
 double cfd_smoother_layout_bytes(const cfd_solver* s) { return (s && s->s) ? s->s->smoother_layout_bytes() : 0.0; }
+double cfd_step_layout_bytes(const cfd_solver* s) { return (s && s->s) ? s->s->layout_step_bytes() : 0.0; }
 double cfd_step_algorithmic_bytes(const cfd_solver* s) {
   return (s && s->s) ? s->s->algorithmic_step_bytes() : 0.0;
 }

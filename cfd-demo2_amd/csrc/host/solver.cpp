@@ -926,6 +926,7 @@ void Solver::ensure_amg() {
     build_amg_host();
   }
   const int L = (int)levels.size();
+  set_resrestrict_blocks();
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
   fuse_presmooth = !(fz_env && fz_env[0] == '0');
@@ -985,6 +986,37 @@ void Solver::ensure_amg() {
   if (timing)
     std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s\n", how, L,
                  std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+}
+
+// Aggregates per block of k_amg_resrestrict for the single-GPU / replicated
+// levels with a coarse level and at most CFD_AMG_FUSED_RR_ROWS rows (default
+// 2^18; distributed levels restrict ghost residuals and keep the two
+// kernels): about 256 members per block, fewer aggregates while a block's
+// members exceed its LDS capacity.  Its one-row-per-thread residual over
+// permuted rows only pays on the latency-bound levels: same-box A/B
+// (profiles/r03/ab_log.md) C2 level 0 129 vs 68 + 34 us, level 1 104 vs
+// 56 + 13 us; C1 levels of 125 k rows and fewer 6-8 vs 10-11 us.
+// CFD_AMG_FUSED_RR=0 keeps the two kernels everywhere.
+void Solver::set_resrestrict_blocks() {
+  const char* fe = std::getenv("CFD_AMG_FUSED_RR");
+  const bool on = !(fe && fe[0] == '0');
+  const char* fr = std::getenv("CFD_AMG_FUSED_RR_ROWS");
+  const uint64_t max_rows = fr ? std::strtoull(fr, nullptr, 10) : (1u << 18);
+  for (AmgGpuLevel& G : levels) {
+    AmgLevelDev& d = G.dev;
+    d.rr_agg = 0;
+    if (!on || G.dist || d.nc == 0 || d.n == 0 || d.n > max_rows || !d.r_row) continue;
+    std::vector<uint32_t> rr((size_t)d.nc + 1);
+    CFD_HIP(hipMemcpyAsync(rr.data(), d.r_row, rr.size() * 4, hipMemcpyDeviceToHost, stream));
+    sync();
+    uint32_t a = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, (uint64_t)256 * d.nc / d.n));
+    for (; a >= 1; a /= 2) {
+      uint32_t worst = 0;
+      for (uint32_t I = 0; I < d.nc; I += a) worst = std::max(worst, rr[std::min(I + a, d.nc)] - rr[I]);
+      if (worst <= kRRCap) break;
+    }
+    d.rr_agg = a;
+  }
 }
 
 // LDS image of the tail levels [tf, L) for k_amg_tail_blob: every array the
@@ -1213,14 +1245,17 @@ void Solver::v_cycle() {
       std::swap(Lv.x, Lv.xt);
     else
       sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
-    res(i);
     AmgGpuLevel& C = levels[i + 1];
     // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
     presmoothed = fuse_presmooth && (i + 1 < down) && (!Lv.dist || C.dist);
     float* smo = presmoothed ? C.xt : nullptr;
-    if (!Lv.dist) {
+    if (!Lv.dist && Lv.dev.rr_agg) {
+      launch_amg_resrestrict(Lv.dev, Lv.x, Lv.b, C.b, C.x, smo, C.dev.de, stream);
+    } else if (!Lv.dist) {
+      res(i);
       launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream, smo, C.dev.de);
     } else {
+      res(i);
       // the restriction sums members owned by the next ranks too (their residuals
       // are ghosts): the aggregates without such members overlap the exchange
       const bool into_dist = C.dist;
@@ -1857,6 +1892,59 @@ double Solver::smoother_layout_bytes() const {
   const AmgLevelDev& d = levels[0].dev;
   const double st = d.stride, n = d.n;
   return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n;
+}
+
+// Layout-true bytes of one step under the fixed schedule: per kernel, the
+// bytes its arrays in THIS library's layouts must move (each element once:
+// neighbour gathers counted once, as SURVEY §8(d) counts them), times its
+// launches per step.  Unlike the reference-format count this is a lower bound
+// of the HBM traffic the kernels generate, so count / step time <= the
+// achieved rate (compare with the PMC step traffic, step_counter_traffic).
+double Solver::layout_step_bytes() const {
+  const double Nn = N;
+  double S = 0.0, Sint = 0.0;  // used face slots, internal ones
+  for (uint32_t i = 0; i < N; ++i) S += topo.nface[i];
+  for (uint32_t li = 0; li < N; ++li) Sint += (double)(topo.srow[li + 1] - topo.srow[li]) - 1.0;
+  const double ws = topo.ws;
+  const int K = cfg.fixed_outer > 0 ? cfg.fixed_outer : std::max(cfg.n_outer_correctors, 10);
+  const int M = cfg.fixed_inner > 0 ? std::min(cfg.fixed_inner, m) : m;
+  const double prep = 40 * S + 60 * Nn;                    // 9 slot arrays + flux out; cell state in, gradients out
+  const double asmb = 32 * S + 20 * Sint + 78 * Nn;        // 8 slot arrays; 3x3 block + Poisson entry out
+  const double spmv = (35 + 16 * ws) * Nn;                 // headers, cval_a + cval_g slots, x, y
+  const double predict = (39 + 8 * ws) * Nn;               // headers, cval_g slots, V_j, dinv, temp_p / p_sol out
+  const double correct = (34 + 8 * ws) * Nn;               // lg, cval_g slots, p_sol, V_j, dinv, Z_j out
+  // one V-cycle over the level images (as v_cycle launches them)
+  double vc = 0.0;
+  const int L = (int)levels.size();
+  const int down = std::min(std::max(tail_first, 1), L - 1);
+  auto row_image = [&](const AmgLevelDev& d) {  // ELL values + columns over the padded rows
+    return std::max(d.w, 1) * (double)d.stride * (4.0 + (d.use16 ? 2.0 : 4.0));
+  };
+  for (int i = 0; i < L; ++i) {
+    const AmgLevelDev& d = levels[i].dev;
+    const double n = d.n, st = d.stride, img = row_image(d);
+    const double smooth = st + img + 16 * n;
+    if (i < down) {
+      const double nc = levels[i + 1].dev.n;
+      vc += (i == 0 ? smooth : 12 * n);                                // pre-smoother (coarse: zero-x, elementwise)
+      if (d.rr_agg && !levels[i].dist)
+        vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
+      else
+        vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
+      vc += 12 * n + 4 * nc;                                           // prolongation
+      vc += smooth;                                                    // post-smoother
+    } else if (i == down) {
+      vc += 4.0 * tail_blob_words + 16.0 * tail_vec_floats;            // single-workgroup tail (LDS image in)
+    }
+  }
+  double inner = 0.0;
+  for (int j = 0; j < M; ++j) {
+    inner += predict + vc + correct + spmv;
+    inner += (j + 2) * 12.0 * Nn + (j + 3) * 12.0 * Nn;    // CGS dots, CGS update + norm
+  }
+  const double residual = spmv + 36 * Nn + 12 * Nn;       // SpMV, axpby, norm
+  const double solve = 12 * Nn + residual + inner + (M + 2) * 12.0 * Nn + residual;
+  return K * (prep + asmb + solve + 36 * Nn);  // prepare: once per Picard iteration (scheme 0)
 }
 
 double Solver::algorithmic_step_bytes() const {

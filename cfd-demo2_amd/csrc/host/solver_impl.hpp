@@ -316,6 +316,7 @@ struct Solver {
   TailBlobLevel* d_tail_desc = nullptr;
   uint32_t tail_blob_words = 0, tail_vec_floats = 0;
   void build_tail_blob(int tf, bool reuse = false);  // reuse: rewrite the existing blob in place
+  void set_resrestrict_blocks();
   std::vector<AmgGpuLevel> levels;
   // the scalar matrix (ELL image, like sval) the hierarchy was built from:
   // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)
@@ -397,6 +398,7 @@ struct Solver {
   size_t debug_len(int id) const;
   void debug_buffer(int id, float* out);
   double algorithmic_step_bytes() const;
+  double layout_step_bytes() const;
   double smoother_bytes() const;
   double smoother_layout_bytes() const;
   // checkpoint / resume (checkpoint.cpp, cfd_state_file_header)

@@ -274,7 +274,13 @@ cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path,
  * the measured sweep time (cfd_profile_smoother's bytes are the reference
  * CSR format's count).                                        */
 double cfd_smoother_layout_bytes(const cfd_solver* s);
-/* Algorithmic bytes of one step under the fixed schedule.    */
+/* Layout-true bytes of one step under the fixed schedule: every kernel's
+ * minimum traffic in this library's layouts (a lower bound of the HBM bytes,
+ * unlike the reference-format count below) times its launches per step.    */
+double cfd_step_layout_bytes(const cfd_solver* s);
+/* Algorithmic bytes of one step under the fixed schedule in the reference's
+ * CSR/f32/u32 format -- a count, larger than this layout's
+ * traffic.                                                                  */
 double cfd_step_algorithmic_bytes(const cfd_solver* s);
 
 /* Debug/parity access to internal device buffers, copied to host.

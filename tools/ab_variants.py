@@ -2,7 +2,7 @@
 libraries for same-box A/B timing:  python tools/ab_variants.py NAME=DEF,DEF ...
 e.g.  u1=CFD_SPMV_U=1  u2=CFD_SPMV_U=2,CFD_PREDICT_U=2
 Libraries land in cfd-demo2_amd/cfd2_amd/_lib/variants/; select one at run
-time with CFD2_AMD_LIB=<path> (tools/gpu_ab.sh)."""
+time with CFD2_AMD_LIB=<path> (tools/gpu_ab_prof.sh: copy the variants into _lib/ab/ for the run)."""
 import os
 import sys
 
