@@ -27,15 +27,16 @@ namespace {
 #ifndef CFD_CGS_NT_ST
 #define CFD_CGS_NT_ST CFD_CGS_NT  // nontemporal stores of the new basis vector
 #endif
-#ifndef CFD_CGS_DOT_SER
-#define CFD_CGS_DOT_SER 1  // one basis load in flight per wavefront (load_cells3)
+// One basis load in flight per wavefront in the CGS kernels (load_cells3 SER)
+// on meshes of at least this many cells (per rank); below it, every load of a
+// wavefront stays in flight together.  With ~15+ blocks per CU the serialised
+// loads win (same-box A/B at C2: update 346 -> 295, dots 294 -> 281 us); with
+// ~4 blocks per CU nothing hides a wavefront's one-at-a-time loads (C1: dots
+// 41.8 -> 31.0, update 40.5 -> 36.2 us unserialised; profiles/r03/ab_log.md).
+#ifndef CFD_CGS_SER_MIN_CELLS
+#define CFD_CGS_SER_MIN_CELLS (1u << 22)
 #endif
-#ifndef CFD_CGS_UPD_SER
-#define CFD_CGS_UPD_SER 1
-#endif
-#ifndef CFD_UPDX_SER
-#define CFD_UPDX_SER 1  // one Z load in flight per thread in k_update_x (A/B C2: 614 -> 583 us)
-#endif
+
 #ifndef CFD_DPP_TREE
 #define CFD_DPP_TREE 1  // wavefront trees of the chunk kernels by DPP (wave_tree64)
 #endif
@@ -1046,17 +1047,28 @@ __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float*
       sp[k] += pp * xp;
     }
 }
+// the two rows' slot headers (u16) and diagonal slots (u8).  Packing both
+// into one u32 per row (one load fewer) lost at C2: SpMV 208 -> 213, Schur
+// prediction 155 -> 160 us (profiles/r03/ab_log.md) -- 2 bytes more per row
+// cost more than the instruction saved.
+__device__ __forceinline__ void row2_headers(const CoupledMatrix& A, uint32_t i0, uint32_t lw[2], uint32_t dr[2]) {
+  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
+  const uchar2 drr = *reinterpret_cast<const uchar2*>(A.drank + i0);
+  lw[0] = lg.x;
+  lw[1] = lg.y;
+  dr[0] = drr.x;
+  dr[1] = drr.y;
+}
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* __restrict__ x,
                                                   float* __restrict__ y) {
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   uint32_t i0;
   if (!row_range2<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
-  const uchar2 drr = *reinterpret_cast<const uchar2*>(A.drank + i0);
+  uint32_t lw[2], dr[2];
+  row2_headers(A, i0, lw, dr);
   const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
-  const uint32_t lw[2] = {lg.x, lg.y}, dr[2] = {drr.x, drr.y};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float su[2] = {0.0f, 0.0f}, sv[2] = {0.0f, 0.0f}, sp[2] = {0.0f, 0.0f};
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
@@ -1073,7 +1085,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* 
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + unit] = <w, V_ii>, ii = 0..j,
 // V_ii = binv[ii] * W_ii, in the cell layout of load_cells3; quarter values
 // ql[16 ii + 4 q + w] in LDS, units at the end.
-template <bool FULL>
+template <bool FULL, bool SER>
 __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, const float* __restrict__ basis,
                                                const float* __restrict__ binv, size_t stride, int j, uint32_t N,
                                                float* ql) {
@@ -1082,7 +1094,7 @@ __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, cons
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[4][3], t[4];
-    load_cells3<FULL, true, CFD_CGS_DOT_SER>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -1092,15 +1104,16 @@ __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, cons
     quarter_trees(t, ql + 16 * ii);
   }
 }
+template <bool SER>
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
                                                      const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride,
                                                      int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
   __shared__ float ql[16 * 64];
   if (block_full(N))
-    cgs_dots_cells<true>(w, basis, binv, stride, j, N, ql);
+    cgs_dots_cells<true, SER>(w, basis, binv, stride, j, N, ql);
   else
-    cgs_dots_cells<false>(w, basis, binv, stride, j, N, ql);
+    cgs_dots_cells<false, SER>(w, basis, binv, stride, j, N, ql);
   __syncthreads();
   const uint32_t UB = 4 / U;
   for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
@@ -1119,14 +1132,14 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 
 // update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
 // updated w is written straight into basis slot j+1 (unnormalised, see binv).
-template <bool FULL>
+template <bool FULL, bool SER>
 __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
                                                  const float* hcol, const float* scol, uint32_t N, float t[4]) {
   float corr[4][3] = {};
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
-    load_cells3<FULL, true, CFD_CGS_UPD_SER>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1142,6 +1155,7 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
   }
   store_cells3_stream<FULL>(basis + (size_t)(j + 1) * stride, N, wn);
 }
+template <bool SER>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
                                                             const float* __restrict__ binv,
@@ -1156,9 +1170,9 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   __syncthreads();
   float t[4];
   if (block_full(N))
-    cgs_update_cells<true>(w, basis, stride, j, hcol, scol, N, t);
+    cgs_update_cells<true, SER>(w, basis, stride, j, hcol, scol, N, t);
   else
-    cgs_update_cells<false>(w, basis, stride, j, hcol, scol, N, t);
+    cgs_update_cells<false, SER>(w, basis, stride, j, hcol, scol, N, t);
   quarter_trees(t, ql);
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
@@ -1615,11 +1629,10 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   const f4u wa = ld4u(wb);
   const f2u wc = ld2u(wb + 4);
   float rhs[2] = {sc * wa.z, sc * wc.y};
-  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
-  const uchar2 drr = *reinterpret_cast<const uchar2*>(A.drank + i0);
+  uint32_t lw[2], dr[2];
+  row2_headers(A, i0, lw, dr);
   const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
-  const uint32_t lw[2] = {lg.x, lg.y}, dr[2] = {drr.x, drr.y};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
     predict2_group<D16, U1, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
@@ -1710,15 +1723,25 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
 }
 
 // solve_triangular (gmres_logic.wgsl:78-104), single lane
-__global__ void k_solve_triangular(const float* H, const float* g, float* y, int k, int m1) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  for (int li = 0; li < k; ++li) {
-    const int i = k - 1 - li;
-    float sum = g[i];
-    for (int jj = i + 1; jj < k; ++jj) sum -= H[(size_t)jj * m1 + i] * y[jj];
-    const float diag = H[(size_t)i * m1 + i];
-    y[i] = (fabsf(diag) > 1e-12f) ? sum / diag : 0.0f;
+// H's first k columns and g are staged in LDS by the whole block, then one
+// lane runs the reference's back substitution from LDS (the same operations
+// in the same order; every H / y access was a dependent global round trip)
+__global__ void __launch_bounds__(256) k_solve_triangular(const float* H, const float* g, float* y, int k, int m1) {
+  __shared__ float hs[64 * 64], gs[64], ys[64];
+  for (int e = threadIdx.x; e < k * m1; e += blockDim.x) hs[e] = H[e];
+  if (threadIdx.x < (unsigned)k) gs[threadIdx.x] = g[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int li = 0; li < k; ++li) {
+      const int i = k - 1 - li;
+      float sum = gs[i];
+      for (int jj = i + 1; jj < k; ++jj) sum -= hs[jj * m1 + i] * ys[jj];
+      const float diag = hs[i * m1 + i];
+      ys[i] = (fabsf(diag) > 1e-12f) ? sum / diag : 0.0f;
+    }
   }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)k) y[threadIdx.x] = ys[threadIdx.x];
 }
 
 // the preconditioned vectors Z_i are read once per restart cycle here (nontemporal, CFD_UPDX_NT)
@@ -1734,13 +1757,15 @@ __device__ __forceinline__ float4 ld4_upd(const float* p) {
   return *reinterpret_cast<const float4*>(p);
 #endif
 }
+template <bool SER>
 __device__ __forceinline__ void upd_wait() {
-#if CFD_UPDX_SER
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+  if constexpr (SER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // basis_size x axpy_from_y (gmres_ops.wgsl:96-105) fused: x = y_i * z_i + x, i ascending
+// SER: one Z load in flight per thread, on meshes of at least
+// CFD_CGS_SER_MIN_CELLS cells (A/B C2: 614 -> 583 us)
+template <bool SER>
 __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __restrict__ z,
                                                      size_t stride, const float* __restrict__ y,
                                                      int k, size_t n) {
@@ -1751,9 +1776,9 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
     int ii = 0;
     for (; ii + 1 < k; ii += 2) {
       const float4 z0 = ld4_upd(z + (size_t)ii * stride + e);
-      upd_wait();
+      upd_wait<SER>();
       const float4 z1 = ld4_upd(z + (size_t)(ii + 1) * stride + e);
-      upd_wait();
+      upd_wait<SER>();
       const float y0 = y[ii], y1 = y[ii + 1];
       xv.x = y0 * z0.x + xv.x;
       xv.y = y0 * z0.y + xv.y;
@@ -2603,18 +2628,26 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      uint32_t U, float* partial, uint32_t np, hipStream_t s) {
-  if (N)
-    hipLaunchKernelGGL(k_cgs_dots, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U, partial,
-                       np);
+  if (!N) return;
+  if (N >= CFD_CGS_SER_MIN_CELLS)
+    hipLaunchKernelGGL(k_cgs_dots<true>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
+                       partial, np);
+  else
+    hipLaunchKernelGGL(k_cgs_dots<false>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
+                       partial, np);
 }
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
                             const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
-  if (N)
-    hipLaunchKernelGGL(k_cgs_update_norm, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1,
-                       N, U, partial);
+  if (!N) return;
+  if (N >= CFD_CGS_SER_MIN_CELLS)
+    hipLaunchKernelGGL(k_cgs_update_norm<true>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
+                       m1, N, U, partial);
+  else
+    hipLaunchKernelGGL(k_cgs_update_norm<false>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
+                       m1, N, U, partial);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, float* host_resid, hipStream_t s) {
@@ -2698,11 +2731,16 @@ void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const flo
     hipLaunchKernelGGL(k_precond_correct<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
 }
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
-  hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(64), 0, s, H, g, y, k, m1);
+  if (k > 64 || m1 > 64) throw std::invalid_argument("solve_triangular: basis larger than 64");
+  hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(256), 0, s, H, g, y, k, m1);
 }
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
                      hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_update_x, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
+  if (!n) return;
+  if (n / 3 >= CFD_CGS_SER_MIN_CELLS)
+    hipLaunchKernelGGL(k_update_x<true>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
+  else
+    hipLaunchKernelGGL(k_update_x<false>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
 // instance for a level: 16/32-bit columns x load mode (see gather_group)
 #define CFD_AMG_INSTANCE(kern, L) \
