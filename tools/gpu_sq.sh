@@ -5,7 +5,7 @@ OUT=$ROOT/gpurun_out/sq
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAVES \
-  --kernel-include-regex "k_spmv|k_precond|k_amg_smooth|k_amg_residual|k_cgs_dots|k_cgs_update|k_amg_restrict" --output-format csv -d $OUT -o run -- \
+  --kernel-include-regex "k_spmv|k_precond|k_amg_smooth|k_amg_residual|k_cgs_dots|k_cgs_update|k_amg_restrict|k_amg_resrestrict" --output-format csv -d $OUT -o run -- \
   python3 $ROOT/bench.py --config c2 --no-cpu-baseline --ref-workloads 0 --steps 1 --warmup 1 > $OUT/bench.json 2> $OUT/bench.log && \
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections, re

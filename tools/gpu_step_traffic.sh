@@ -2,7 +2,7 @@
 # summary (tools/pmc_summary.py) for profiles/<round>; each rocprofv3 pass runs
 # on its own with its own time limit.
 set -o pipefail
-R=${1:-r02}
+R=${1:-r03}
 CFG=${2:-c2}
 ROOT=$GRAFT_REPO_ROOT
 OUT=$ROOT/gpurun_out/steptraffic_${R}_$CFG
