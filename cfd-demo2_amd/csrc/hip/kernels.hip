@@ -1833,9 +1833,12 @@ __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uin
 // Slots are processed in groups of kU with every load of the group issued
 // before the first use (val/col, then the x gathers): ~kU x more memory-level
 // parallelism per wave than a slot-at-a-time loop.  Accumulation order per
-// row is unchanged (slot order).
+// row is unchanged (slot order).  kU = 2 since round 3: same-box A/B over
+// kU = 1..4 (profiles/r03/ab_amg_u_c1.txt, _c2.txt) C1 42.90 -> 42.25 ms,
+// C2 260.8 -> 259.5 ms/step; the 5 M-row level 1 (7 slots) gains most
+// (residual 57.3 -> 51.3 us), level 0 (5 slots) is flat.
 #ifndef CFD_AMG_U
-#define CFD_AMG_U 4
+#define CFD_AMG_U 2
 #endif
 constexpr int kU = CFD_AMG_U;
 
@@ -1886,9 +1889,20 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
   }
 }
 
+// Occupancy floor of the level row kernels (waves per SIMD; 0: the compiler's
+// choice -- 78 / 86 VGPRs, 6 / 5 waves for the smoother / residual)
+#ifndef CFD_AMG_WAVES
+#define CFD_AMG_WAVES 0
+#endif
+#if CFD_AMG_WAVES > 0
+#define CFD_AMG_OCC __attribute__((amdgpu_waves_per_eu(CFD_AMG_WAVES)))
+#else
+#define CFD_AMG_OCC
+#endif
+
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
 template <bool D16, int MODE>
-__global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
+__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ x_out) {
   uint32_t i0;
@@ -1948,7 +1962,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
 template <bool D16, int MODE>
-__global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
+__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b,
                                                          float* __restrict__ rr) {
   uint32_t i0;
@@ -2343,18 +2357,44 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
   extern __shared__ float sm[];
   const uint32_t t = threadIdx.x, nt = blockDim.x;
   uint32_t* bw = reinterpret_cast<uint32_t*>(sm + vec_floats);
-  for (uint32_t w = 4 * t; w < blob_words; w += 4 * nt)
-    *reinterpret_cast<uint4*>(bw + w) = *reinterpret_cast<const uint4*>(blob + w);
   auto base = [&](int l) {
     uint32_t o = 0;
     for (int k = first; k < l; ++k) o += 4 * r4(desc[k].n);
     return sm + o;
   };
   {
+    // every global load of the blob and of b issued before the first LDS
+    // store: one memory round trip instead of one per 16 KiB pass (the blob
+    // is cold in HBM after the fine levels' sweeps: C2 25.2 -> 23.9 us,
+    // profiles/r03/ab_tail_occ_c2.txt).  The launch is always
+    // 1024 threads; blob and b together fit in kTailLdsMax (16 B per row of
+    // b's level alone), so KB / KV loads per thread cover both.
+    constexpr uint32_t NT = 1024, KB = (uint32_t)((kTailLdsMax / 16 + NT - 1) / NT), KV = KB;
     const uint32_t n = desc[first].n;
-    float* B0 = base(first) + 2 * r4(n);
     const float* gb = tail[first].b;
-    for (uint32_t i = t; i < n; i += nt) B0[i] = gb[i];
+    uint4 v[KB];
+    float bv[KV];
+    // clamped, unconditional loads (guarded ones put v[] in scratch)
+#pragma unroll
+    for (uint32_t k = 0; k < KB; ++k)
+      v[k] = *reinterpret_cast<const uint4*>(blob + min(4 * (t + k * NT), blob_words - 4));
+#pragma unroll
+    for (uint32_t k = 0; k < KV; ++k) bv[k] = gb[min(t + k * NT, n - 1)];
+    // pin the loaded registers here so that the compiler cannot sink each
+    // load into its guarded store below (load -> wait -> store per pass)
+#pragma unroll
+    for (uint32_t k = 0; k < KB; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
+#pragma unroll
+    for (uint32_t k = 0; k < KV; ++k) asm volatile("" : "+v"(bv[k]));
+#pragma unroll
+    for (uint32_t k = 0; k < KB; ++k) {
+      const uint32_t w = 4 * (t + k * NT);
+      if (w < blob_words) *reinterpret_cast<uint4*>(bw + w) = v[k];
+    }
+    float* B0 = base(first) + 2 * r4(n);
+#pragma unroll
+    for (uint32_t k = 0; k < KV; ++k)
+      if (t + k * NT < n) B0[t + k * NT] = bv[k];
   }
   __syncthreads();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
@@ -2798,6 +2838,7 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s) {
   const size_t lds = 4 * ((size_t)vec_floats + blob_words);
+  if (lds > kTailLdsMax || blob_words % 4 || blob_words == 0) throw std::invalid_argument("AMG tail blob larger than the kernel's LDS image");
   hipLaunchKernelGGL(k_amg_tail_blob, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats, first,
                      nlev);
 }

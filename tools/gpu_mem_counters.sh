@@ -19,12 +19,12 @@ for r in csv.DictReader(open(f)):
     k = (re.search(r"k_\w+(<[^>]*>)?", r["Kernel_Name"]).group(0), int(r.get("Grid_Size", r.get("Grid_Size_X", 0))))
     acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 names = sorted({n for k in acc for n in acc[k]})
-print("# per-dispatch averages; *_BUSY / *STALL* as a fraction of GRBM_GUI_ACTIVE x units (TA/TD/TCP: 256 CUs, TCC: 16 channels x 8 XCDs)")
+print("# per-dispatch averages; *_BUSY / *STALL* as a fraction of per-XCD active cycles (GRBM_GUI_ACTIVE / 8: rocprofv3 sums it over the 8 XCDs) x 256 CUs")
 for k in sorted(acc, key=lambda k: -sum(acc[k].get("GRBM_GUI_ACTIVE", [0]))):
     m = {n: sum(acc[k][n]) / max(len(acc[k][n]), 1) for n in names}
-    gui = max(m.get("GRBM_GUI_ACTIVE", 1.0), 1.0)
+    gui = max(m.get("GRBM_GUI_ACTIVE", 8.0), 8.0) / 8.0  # per-XCD cycles
     hit, miss = m.get("TCC_HIT_sum", 0.0), m.get("TCC_MISS_sum", 0.0)
-    print(f"{k[0]:28s} {k[1]:9d} cycles {gui:9.0f}  TA busy {m.get('TA_TA_BUSY_sum',0)/gui/256:5.2f}"
+    print(f"{k[0]:28s} {k[1]:9d} cycles/XCD {gui:8.0f}  TA busy {m.get('TA_TA_BUSY_sum',0)/gui/256:5.2f}"
           f"  TA stalled by TC {m.get('TA_ADDR_STALLED_BY_TC_CYCLES_sum',0)/gui/256:5.2f}"
           f"  TD busy {m.get('TD_TD_BUSY_sum',0)/gui/256:5.2f}  TD stalled by TC {m.get('TD_TC_STALL_sum',0)/gui/256:5.2f}"
           f"  TCP pending stall {m.get('TCP_PENDING_STALL_CYCLES_sum',0)/gui/256:5.2f}"
