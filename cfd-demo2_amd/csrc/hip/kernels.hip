@@ -2350,12 +2350,38 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 // columns, dv/de, drank, P and R).  Each phase is then LDS reads + one
 // barrier instead of a global (L2) round trip per matrix slot.  Same row
 // arithmetic, in the same order, as smooth_row / residual_row.
+// Diagnostic build only (-DCFD_TAIL_STAMPS=K, tools/ab_variants.py; read by
+// tools/tail_stamps.py): thread 0 of the K-th launch records s_memtime after
+// every phase; the deltas (shader-clock cycles) land in g_tail_st[1..], their
+// count in g_tail_st[0], read back with cfd_debug_tail_stamps.
+#ifndef CFD_TAIL_STAMPS
+#define CFD_TAIL_STAMPS 0
+#endif
+#if CFD_TAIL_STAMPS
+__device__ unsigned g_tail_calls;
+__device__ uint32_t g_tail_st[64];
+#define TAIL_STAMP()                                                         \
+  do {                                                                       \
+    if (t == 0 && ns < 64) st[ns] = __builtin_amdgcn_s_memtime();            \
+    ++ns;                                                                    \
+  } while (0)
+#else
+#define TAIL_STAMP() \
+  do {               \
+  } while (0)
+#endif
 __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __restrict__ tail,
                                                         const TailBlobLevel* __restrict__ desc,
                                                         const uint32_t* __restrict__ blob, uint32_t blob_words,
-                                                        uint32_t vec_floats, int first, int nlev) {
+                                                        uint32_t vec_floats, int first, int nlev,
+                                                        const float* __restrict__ b_first, uint32_t n_first) {
   extern __shared__ float sm[];
   const uint32_t t = threadIdx.x, nt = blockDim.x;
+#if CFD_TAIL_STAMPS
+  uint64_t st[64];
+  int ns = 0;
+#endif
+  TAIL_STAMP();
   uint32_t* bw = reinterpret_cast<uint32_t*>(sm + vec_floats);
   auto base = [&](int l) {
     uint32_t o = 0;
@@ -2370,8 +2396,10 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     // 1024 threads; blob and b together fit in kTailLdsMax (16 B per row of
     // b's level alone), so KB / KV loads per thread cover both.
     constexpr uint32_t NT = 1024, KB = (uint32_t)((kTailLdsMax / 16 + NT - 1) / NT), KV = KB;
-    const uint32_t n = desc[first].n;
-    const float* gb = tail[first].b;
+    // b and n of the first level as kernel arguments: no dependent load of
+    // the level descriptors before the b loads
+    const uint32_t n = n_first;
+    const float* gb = b_first;
     uint4 v[KB];
     float bv[KV];
     // clamped, unconditional loads (guarded ones put v[] in scratch)
@@ -2397,6 +2425,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       if (t + k * NT < n) B0[t + k * NT] = bv[k];
   }
   __syncthreads();
+  TAIL_STAMP();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
   auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
   auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
@@ -2417,6 +2446,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     const float* de = fw(D.de);
     for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
     __syncthreads();
+  TAIL_STAMP();
     {
       const uint32_t* ro = bw + D.rowoff;
       const float* val = fw(D.val);
@@ -2435,6 +2465,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       }
     }
     __syncthreads();
+  TAIL_STAMP();
     float* CB = base(l + 1) + 2 * r4(desc[l + 1].n);
     {
       const uint16_t* rrow = hw(D.r_row);
@@ -2446,6 +2477,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       }
     }
     __syncthreads();
+  TAIL_STAMP();
   }
   {
     const TailBlobLevel D = desc[nlev - 1];
@@ -2454,6 +2486,25 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     float* XT = X + nr;
     float* B = XT + nr;
     const float* de = fw(D.de);
+    if (D.maxlen == 0) {
+      // coarsest level without off-diagonal entries (C1: 829 rows): every
+      // sweep is row-local, so each thread runs its row's 10 sweeps in
+      // registers with no barrier in between -- the operations of smooth()
+      // with sigma = +0 in the same order (bit-identical; (b - 0) / d is the
+      // same value in every sweep)
+      for (uint32_t i = t; i < D.n; i += nt) {
+        const float q = (B[i] - 0.0f) / de[i];
+        float xp = wmix(0.0f, q, 0.8f), xq = xp;
+        for (int s = 1; s < 10; ++s) {
+          xq = xp;
+          xp = wmix(xq, q, 0.8f);
+        }
+        XT[i] = xq;  // sweep 8 (even sweeps write XT)
+        X[i] = xp;   // sweep 9
+      }
+      __syncthreads();
+      TAIL_STAMP();
+    } else
     for (int s = 0; s < 10; ++s) {
       if (s == 0) {
         for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
@@ -2463,6 +2514,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
         for (uint32_t i = t; i < D.n; i += nt) xout[i] = smooth(D, xin, B, i);
       }
       __syncthreads();
+  TAIL_STAMP();
     }
   }
   for (int l = nlev - 2; l >= first; --l) {
@@ -2479,12 +2531,23 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       XT[i] += corr;
     }
     __syncthreads();
+  TAIL_STAMP();
     for (uint32_t i = t; i < D.n; i += nt) X[i] = smooth(D, XT, B, i);
     __syncthreads();
+  TAIL_STAMP();
   }
   const float* X0 = base(first);
   float* gx = tail[first].x;
   for (uint32_t i = t; i < desc[first].n; i += nt) gx[i] = X0[i];
+#if CFD_TAIL_STAMPS
+  if (t == 0) {
+    const unsigned c = atomicAdd(&g_tail_calls, 1u);
+    if (c == CFD_TAIL_STAMPS) {
+      g_tail_st[0] = (uint32_t)ns;
+      for (int q = 1; q < ns && q < 64; ++q) g_tail_st[q] = (uint32_t)(st[q] - st[q - 1]);
+    }
+  }
+#endif
 }
 
 // ---------------------- check_evolution statistics --------------------------
@@ -2836,11 +2899,13 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
   hipLaunchKernelGGL(k_amg_tail_lds, dim3(1), dim3(1024), lds_bytes, s, tail, first, nlev);
 }
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
-                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s) {
+                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, const float* b_first,
+                          uint32_t n_first, hipStream_t s) {
   const size_t lds = 4 * ((size_t)vec_floats + blob_words);
   if (lds > kTailLdsMax || blob_words % 4 || blob_words == 0) throw std::invalid_argument("AMG tail blob larger than the kernel's LDS image");
+  if (n_first == 0 || 16 * (size_t)n_first > kTailLdsMax) throw std::invalid_argument("AMG tail: first level size");
   hipLaunchKernelGGL(k_amg_tail_blob, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats, first,
-                     nlev);
+                     nlev, b_first, n_first);
 }
 // Per-device kernel attributes: the LDS-resident tail kernels take more than
 // the default 64 KiB of dynamic LDS.  The attribute belongs to the device that
@@ -2917,3 +2982,10 @@ void build_r_m4(const std::vector<uint32_t>& r_row, const std::vector<uint32_t>&
 }
 
 }  // namespace cfd2
+
+#if CFD_TAIL_STAMPS
+extern "C" int cfd_debug_tail_stamps(uint32_t* out, int n) {
+  if (n > 64) n = 64;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd2::g_tail_st), n * sizeof(uint32_t)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -267,6 +267,7 @@ constexpr int kMaxAmgLevels = 20;
 struct TailBlobLevel {
   uint32_t n, nc;
   uint32_t de, dv, rowoff, drank, val, col, agg, r_row, r_col;
+  uint32_t maxlen;  // longest row (off-diagonal entries)
 };
 
 // ---------------- launch wrappers (kernels.hip) ----------------
@@ -350,7 +351,8 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 // a multiple of 4) is copied into LDS after the vectors (vec_floats floats);
 // desc[l] describes level l (l in [first, nlev)).  lds_bytes = 4 * (vec_floats + blob_words).
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
-                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, hipStream_t s);
+                          uint32_t blob_words, uint32_t vec_floats, int first, int nlev, const float* b_first,
+                          uint32_t n_first, hipStream_t s);
 // fine rows [f0, f1) (multiples of 4 but f1 = L.n; f1 = 0: all)
 // residual + restriction fused (k_amg_resrestrict; L.rr_agg > 0, replicated
 // or single-GPU level): coarse_b = R (b - A x), coarse_x cleared or the

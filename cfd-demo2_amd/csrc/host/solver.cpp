@@ -1110,6 +1110,7 @@ void Solver::build_tail_blob(int tf, bool reuse) {
     TailBlobLevel& D = desc[l];
     D.n = n;
     D.nc = d.nc;
+    D.maxlen = n ? *std::max_element(len.begin(), len.end()) : 0;
     D.de = put_f(de.data(), n);
     D.dv = put_f(dv.data(), n);
     D.rowoff = put_u32(ro);
@@ -1278,7 +1279,8 @@ void Solver::v_cycle() {
     }
   }
   if (tf < L && tf == tail_blob_first) {
-    launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf, L, stream);
+    launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf, L, levels[tf].b,
+                         levels[tf].dev.n, stream);
   } else if (tf < L) {
     size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL_LDS=0 disables)
     for (int l = tf; l < L; ++l) lds += 4 * (((size_t)levels[l].dev.n + 3) & ~(size_t)3) * sizeof(float);
