@@ -882,6 +882,14 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
 // before issuing the next slot), and the first group does not wait for the
 // row lengths.  The first group is sized to cover a whole interior row
 // (5 entries of a quad cell's coupled row).
+// SpMV: the first slot group's cval_a / cval_g loads issued with the row
+// headers, before the wait for them (C2 216 -> 197 us; the same for the
+// Schur prediction lost 150 -> 158 us: profiles/r03/ab_coupled_pre_c2.txt;
+// the regular rows' x gathers issued speculatively as well gained nothing
+// more, 198 -> 200 us: ab_spmv_spec_c2.txt)
+#ifndef CFD_COUPLED_PRE
+#define CFD_COUPLED_PRE 1
+#endif
 #ifndef CFD_SPMV_U1
 #define CFD_SPMV_U1 5
 #endif
@@ -976,18 +984,26 @@ __device__ __forceinline__ bool lg2_on(uint32_t w, uint32_t r) { return r < (w &
 // REG (first slot group of a wave of regular rows, r0 = 0): columns
 // row + tmode[slot] (no column loads), and the two rows' x entries are six
 // consecutive floats (one 16-byte + one 8-byte gather)
-template <bool D16, int U, bool REG = false>
+// PRE: the group's cval_a / cval_g slots were loaded by the caller (first
+// group: issued right after the row headers, before the wait for them)
+template <bool D16, int U, bool REG = false, bool PRE = false>
 __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
                                             uint32_t r0, uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
-                                            const float2 d2[2], float su[2], float sv[2], float sp[2]) {
+                                            const float2 d2[2], float su[2], float sv[2], float sp[2],
+                                            const float4* pa = nullptr, const float4* pg = nullptr) {
   float4 a[U], g[U];
   int c[U][2];
   float xg[U][2][3];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    a[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
-    g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    if constexpr (PRE) {
+      a[u] = pa[u];
+      g[u] = pg[u];
+    } else {
+      a[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
+      g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    }
     if constexpr (REG) {
       c[u][0] = (int)i0 + A.tmode[u];
       c[u][1] = c[u][0] + 1;
@@ -1071,10 +1087,24 @@ __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* 
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float su[2] = {0.0f, 0.0f}, sv[2] = {0.0f, 0.0f}, sp[2] = {0.0f, 0.0f};
+#if CFD_COUPLED_PRE
+  float4 pa[U1], pg[U1];
+#pragma unroll
+  for (int u = 0; u < U1; ++u) {
+    const size_t off = (size_t)min((uint32_t)u, (uint32_t)A.ws - 1u) * A.ld + i0;
+    pa[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
+    pg[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+  }
+  if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
+    spmv2_group<D16, U1, true, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
+  else
+    spmv2_group<D16, U1, false, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
+#else
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
     spmv2_group<D16, U1, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
   else
     spmv2_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
+#endif
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv2_group<D16, U>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
   float* yo = y + 3 * (size_t)i0;  // 8-byte aligned (i0 even)
   typedef float f2v __attribute__((ext_vector_type(2)));
