@@ -1879,10 +1879,21 @@ constexpr int kU = CFD_AMG_U;
 // on the thread's longest row (avoids reading the padding of short rows);
 // peeled loads with predicated gathers were slower there (A/B level 1: 62
 // vs 57 us).
-template <bool D16, int MODE, bool ALWAYS = false>
+typedef int i4u __attribute__((ext_vector_type(4), aligned(4)));
+
+// The prolongation prolongate_op (amg.wgsl:56-75) of a fine row f, applied to
+// its value as it is read: x'[f] = x[f] + (0 + 1 * xc[agg[f]]) -- the two f32
+// roundings of k_amg_prolong (0 + v turns -0 into +0, the add follows).
+__device__ __forceinline__ float prolonged(float xf, float xcv) { return xf + (0.0f + 1.0f * xcv); }
+
+// PRO: every gathered x value is the prolonged one (k_amg_smooth<..., true>):
+// agg is gathered with the same columns as x (a 16-byte load where x is), then
+// the coarse values -- one more dependent round trip instead of a launch.
+template <bool D16, int MODE, bool ALWAYS = false, bool PRO = false>
 __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln,
-                                             float4 v[kU], float xg[kU][4]) {
+                                             float4 v[kU], float xg[kU][4],
+                                             const float* __restrict__ xc = nullptr) {
   int c[kU][4];
 #pragma unroll
   for (int u = 0; u < kU; ++u) {
@@ -1896,6 +1907,7 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       for (int k = 0; k < 4; ++k) c[u][k] = (int)i0 + k;
     }
   }
+  [[maybe_unused]] int ag[kU][4];
   if constexpr (ALWAYS && MODE == 1 && CFD_VGATHER) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -1904,18 +1916,43 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       xg[u][1] = q.y;
       xg[u][2] = q.z;
       xg[u][3] = q.w;
+      if constexpr (PRO) {
+        const i4u a = *reinterpret_cast<const i4u*>(L.agg + c[u][0]);
+        ag[u][0] = a.x;
+        ag[u][1] = a.y;
+        ag[u][2] = a.z;
+        ag[u][3] = a.w;
+      }
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u)
       if (!consec4(c[u])) {
 #pragma unroll
-        for (int k = 1; k < 4; ++k) xg[u][k] = x[c[u][k]];
+        for (int k = 1; k < 4; ++k) {
+          xg[u][k] = x[c[u][k]];
+          if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
+        }
       }
   } else {
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) xg[u][k] = gat<ALWAYS && MODE == 1>(r0 + u < u4(ln, k), x + c[u][k]);
+      for (int k = 0; k < 4; ++k) {
+        xg[u][k] = gat<ALWAYS && MODE == 1>(r0 + u < u4(ln, k), x + c[u][k]);
+        // unused slots hold the row's own (valid) column: agg of a real or padding row
+        if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
+      }
+  }
+  if constexpr (PRO) {
+    float cv[kU][4];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cv[u][k] = xc[ag[u][k]];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xg[u][k] = prolonged(xg[u][k], cv[u][k]);
   }
 }
 
@@ -1930,11 +1967,16 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 #define CFD_AMG_OCC
 #endif
 
-// smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8)
-template <bool D16, int MODE>
+// smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8).
+// PRO (post-smoother of a single-GPU / replicated level): the prolongation
+// from the coarse level xc that precedes it (k_amg_prolong) is applied to
+// every x value as it is read, so x' = x + P xc is never stored -- the same
+// f32 operations per value, one launch and one pass over x / agg fewer.
+template <bool D16, int MODE, bool PRO = false>
 __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b,
-                                                       float* __restrict__ x_out) {
+                                                       float* __restrict__ x_out,
+                                                       const float* __restrict__ xc = nullptr) {
   uint32_t i0;
   if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
@@ -1943,7 +1985,7 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
   auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16, MODE, true>(L, x, i0, r0, rmax, ln, v, xg);
+    gather_group<D16, MODE, true, PRO>(L, x, i0, r0, rmax, ln, v, xg, xc);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -1958,8 +2000,20 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
     for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
   }
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  float4 xx = *reinterpret_cast<const float4*>(x + i0);
   const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
+  if constexpr (PRO) {  // the row's own value, as k_amg_prolong (padding rows get + 0)
+    const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
+    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+    c0 += 1.0f * xc[ag.x];
+    if (i0 + 1 < L.n) c1 += 1.0f * xc[ag.y];
+    if (i0 + 2 < L.n) c2 += 1.0f * xc[ag.z];
+    if (i0 + 3 < L.n) c3 += 1.0f * xc[ag.w];
+    xx.x += c0;
+    xx.y += c1;
+    xx.z += c2;
+    xx.w += c3;
+  }
   float4 o;
   o.x = wmix(xx.x, (bb.x - sg[0]) / dd.x, 0.8f);
   o.y = wmix(xx.y, (bb.y - sg[1]) / dd.y, 0.8f);
@@ -2885,9 +2939,18 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
   auto fn = CFD_AMG_INSTANCE(k_amg_smooth, L);
   if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
-    hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out);
+    hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out, nullptr);
   else
-    hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out);
+    hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, nullptr);
+}
+void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b, float* x_out,
+                               hipStream_t s) {
+  if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
+  if (!L.agg || !xc) throw std::invalid_argument("amg_smooth_prolong: level without a coarse level");
+  const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
+  auto fn = L.use16 ? (L.full ? k_amg_smooth<true, 1, true> : k_amg_smooth<true, 0, true>)
+                    : (L.full ? k_amg_smooth<false, 1, true> : k_amg_smooth<false, 0, true>);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, xc);
 }
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);

@@ -233,6 +233,10 @@ struct AmgLevelDev {
   uint32_t rr_agg;
 };
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
+// zeroed entries after every level's agg array: the fused prolongation reads
+// agg with 16-byte loads from any column (as the x gathers, whose vectors
+// carry the same slack)
+constexpr size_t kAggSlack = 64;
 
 // Halo pack (distributed): up to 8 fields packed per launch.
 struct PackField {
@@ -327,6 +331,11 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
 // ev0/ev1 (optional): timing events recorded by the GPU at kernel start / end
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
                        hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// post-smoother with the prolongation fused: x_out = smooth(x + P xc), bit-identical
+// to launch_amg_prolong(L, x, xc) then launch_amg_smooth(L, x, b, x_out), but x is
+// only read (single-GPU / replicated levels: every column an owned row)
+void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b,
+                               float* x_out, hipStream_t s);
 // pre-smoother of a level whose x is identically +0 (bit-identical to launch_amg_smooth then)
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,

@@ -203,7 +203,7 @@ bool Solver::device_levels(AmgSetupLevel& cur_in, int li0, const std::vector<uin
     const double t_agg = secs(t0);
     std::vector<uint32_t> aggp(st, 0);
     for (uint32_t i = 0; i < n; ++i) aggp[i] = agg[i];
-    G.dev.agg = arena.upload(aggp, stream);
+    G.dev.agg = arena.upload(aggp, stream, kAggSlack);
     G.dev.r_row = arena.upload(r_row, stream);
     G.dev.r_col = arena.upload(r_col, stream);
     {
@@ -750,7 +750,7 @@ bool Solver::build_amg_device_dist() {
         G.rc_hi = 0;
         G.pf_lo = nown;
       }
-      G.dev.agg = arena.upload(aggp, stream);
+      G.dev.agg = arena.upload(aggp, stream, kAggSlack);
       G.dev.r_row = arena.upload(r_row, stream);
       G.dev.r_col = arena.upload(r_col, stream);
       std::vector<int32_t> m4;

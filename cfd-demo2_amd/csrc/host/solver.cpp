@@ -849,7 +849,7 @@ void Solver::build_amg_host() {
         r_col = HL.r_col;
         G.dev.nc = HL.nc;
       }
-      G.dev.agg = arena.upload(agg, stream);
+      G.dev.agg = arena.upload(agg, stream, kAggSlack);
       G.dev.r_row = arena.upload(r_row, stream);
       G.dev.r_col = arena.upload(r_col, stream);
       {
@@ -930,6 +930,14 @@ void Solver::ensure_amg() {
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
   const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
   fuse_presmooth = !(fz_env && fz_env[0] == '0');
+  // post-smoothers with the prolongation fused (single-GPU / replicated levels
+  // from CFD_AMG_FUSED_PROLONG=<level> on -- "off": never -- with at most
+  // CFD_AMG_FUSED_PROLONG_ROWS rows)
+  const char* fp_env = std::getenv("CFD_AMG_FUSED_PROLONG");
+  fuse_prolong_from = 0;
+  if (fp_env) fuse_prolong_from = (fp_env[0] == 'o') ? kMaxAmgLevels : (int)std::strtol(fp_env, nullptr, 10);
+  const char* fpr_env = std::getenv("CFD_AMG_FUSED_PROLONG_ROWS");
+  fuse_prolong_rows = fpr_env ? std::strtoull(fpr_env, nullptr, 10) : (1ull << 20);
   const char* tl_env = std::getenv("CFD_AMG_TAIL_LDS");
   tail_lds = !(tl_env && tl_env[0] == '0');
   const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
@@ -1298,6 +1306,12 @@ void Solver::v_cycle() {
       if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n);
       halo_end();
       if (split > 0) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, split);
+    } else if (fused_prolong(ii)) {
+      // the prolongation applied inside the post-smoother's reads (x stays un-prolonged)
+      AmgGpuLevel& F = levels[ii];
+      launch_amg_smooth_prolong(F.dev, F.x, levels[ii + 1].x, F.b, F.xt, stream);
+      std::swap(F.x, F.xt);
+      continue;
     } else {
       launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
     }
@@ -1933,8 +1947,10 @@ double Solver::layout_step_bytes() const {
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
       else
         vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
-      vc += 12 * n + 4 * nc;                                           // prolongation
-      vc += smooth;                                                    // post-smoother
+      if (fused_prolong(i))
+        vc += smooth + 4 * n + 4 * nc;                                 // post-smoother reading x + P xc
+      else
+        vc += (12 * n + 4 * nc) + smooth;                              // prolongation, post-smoother
     } else if (i == down) {
       vc += 4.0 * tail_blob_words + 16.0 * tail_vec_floats;            // single-workgroup tail (LDS image in)
     }

@@ -45,8 +45,11 @@ class DeviceArena {
     return static_cast<T*>(p);
   }
   template <class T>
-  T* upload(const std::vector<T>& v, hipStream_t s) {
-    T* p = alloc<T>(v.size());
+  T* upload(const std::vector<T>& v, hipStream_t s, size_t slack = 0) {
+    // slack: zeroed elements after the data (16-byte vector reads that start
+    // at any valid index, e.g. the fused prolongation's agg gathers)
+    T* p = alloc<T>(v.size() + slack);
+    if (slack) CFD_HIP(hipMemsetAsync(p + v.size(), 0, slack * sizeof(T), s));
     if (!v.empty()) CFD_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
     return p;
   }
@@ -309,6 +312,11 @@ struct Solver {
   bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
   bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
+  int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
+  uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
+  bool fused_prolong(int li) const {
+    return li >= fuse_prolong_from && !levels[li].dist && levels[li].dev.n <= fuse_prolong_rows;
+  }
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   // k_amg_tail_blob: LDS image of the tail levels [tail_blob_first, L) (-1: none)
   int tail_blob_first = -1;

@@ -183,7 +183,8 @@ def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
     _three_way(mesh, nranks, cfg, setup, 2, f"overlapped {which}", oracle=(which != "c1"))
 
 
-@pytest.mark.parametrize("env", [{"CFD_HALO_PACK": "1"}, {"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"}],
+@pytest.mark.parametrize("env", [{"CFD_HALO_PACK": "1"}, {"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"},
+                                 {"CFD_AMG_FUSED_PROLONG": "off"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_group_variants_parity(env, replicate_rows, monkeypatch):
     """Distributed runs through the packed halo path and the alternative AMG
