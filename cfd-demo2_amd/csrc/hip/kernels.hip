@@ -1211,19 +1211,42 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
 // (gmres_logic.wgsl:24-76).
-__device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens, float* g, float* binv,
-                                float* resid_hist, float* host_resid = nullptr) {
-  const float norm = sqrtf(s);
-  H[(size_t)j * m1 + j + 1] = norm;
-  binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
+__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
+                                                                  float* givens, float* g, float* binv,
+                                                                  float* resid_hist, float* host_resid) {
+  __shared__ float la[kRedMaxSegments], lb[65];
+  // Hessenberg column j and the rotations so far, staged in LDS by the block
+  // (issued before the reduction): the serial Givens chain then makes LDS
+  // round trips instead of dependent global ones
   float* Hc = H + (size_t)j * m1;
-  for (int ii = 0; ii < j; ++ii) {
-    const float hij = Hc[ii], hi1j = Hc[ii + 1];
-    const float cc = givens[2 * ii], ss = givens[2 * ii + 1];
-    Hc[ii] = cc * hij + ss * hi1j;
-    Hc[ii + 1] = -ss * hij + cc * hi1j;
+  float hv = 0.0f, gva = 0.0f, gvb = 0.0f;
+  const uint32_t t = threadIdx.x;
+  if (t <= (uint32_t)j) hv = Hc[t];
+  if (t < (uint32_t)j) {
+    gva = givens[2 * t];
+    gvb = givens[2 * t + 1];
   }
-  const float hjj = Hc[j], hj1j = Hc[j + 1];
+  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);  // ends with a barrier
+  float* hc = la;         // [j + 2]
+  float* gv = la + 128;   // [2 j]
+  if (t <= (uint32_t)j) hc[t] = hv;
+  if (t < (uint32_t)j) {
+    gv[2 * t] = gva;
+    gv[2 * t + 1] = gvb;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  // norm_givens_out's operations, on the staged values
+  const float norm = sqrtf(s);
+  hc[j + 1] = norm;
+  binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
+  for (int ii = 0; ii < j; ++ii) {
+    const float hij = hc[ii], hi1j = hc[ii + 1];
+    const float cc = gv[2 * ii], ss = gv[2 * ii + 1];
+    hc[ii] = cc * hij + ss * hi1j;
+    hc[ii + 1] = -ss * hij + cc * hi1j;
+  }
+  const float hjj = hc[j], hj1j = hc[j + 1];
   float cc = 1.0f, ss = 0.0f;
   const float rho = sqrtf(hjj * hjj + hj1j * hj1j);
   if (fabsf(rho) > 1e-20f) {
@@ -1232,22 +1255,17 @@ __device__ void norm_givens_out(float s, int j, float* H, int m1, float* givens,
   }
   givens[2 * j] = cc;
   givens[2 * j + 1] = ss;
-  Hc[j] = rho;
-  Hc[j + 1] = 0.0f;
+  hc[j] = rho;
+  hc[j + 1] = 0.0f;
+  for (int ii = 0; ii <= j + 1; ++ii) Hc[ii] = hc[ii];
   const float gj = g[j], gj1 = g[j + 1];
   g[j] = cc * gj + ss * gj1;
-  g[j + 1] = -ss * gj + cc * gj1;
-  resid_hist[j] = fabsf(g[j + 1]);
+  const float gn = -ss * gj + cc * gj1;
+  g[j + 1] = gn;
+  resid_hist[j] = fabsf(gn);
   // the host's lag-model read (coupled_solver.rs:326-435): written straight into
   // pinned host memory, so no copy is enqueued per iteration
-  if (host_resid) host_resid[0] = resid_hist[j];
-}
-__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
-                                                                  float* givens, float* g, float* binv,
-                                                                  float* resid_hist, float* host_resid) {
-  __shared__ float la[kRedMaxSegments], lb[65];
-  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);
-  if (threadIdx.x == 0) norm_givens_out(s, j, H, m1, givens, g, binv, resid_hist, host_resid);
+  if (host_resid) host_resid[0] = fabsf(gn);
 }
 
 // predict_and_form_schur (schur_precond.wgsl:142-188), 4 cells per thread.
@@ -1958,6 +1976,11 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 
 // Occupancy floor of the level row kernels (waves per SIMD; 0: the compiler's
 // choice -- 78 / 86 VGPRs, 6 / 5 waves for the smoother / residual)
+// Row operands (b, x, diagonal) of the smoother / residual loaded at the top
+// (1) or after the slot loop (0)
+#ifndef CFD_AMG_EARLY
+#define CFD_AMG_EARLY 0
+#endif
 #ifndef CFD_AMG_WAVES
 #define CFD_AMG_WAVES 0
 #endif
@@ -1980,6 +2003,12 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
   uint32_t i0;
   if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
+#if CFD_AMG_EARLY
+  // the row's own operands issued with the row lengths (no round trip after the slots)
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
+#endif
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   auto step = [&](uint32_t r0, uint32_t rmax) {
@@ -1999,9 +2028,11 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
   } else {
     for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
   }
+#if !CFD_AMG_EARLY
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
   float4 xx = *reinterpret_cast<const float4*>(x + i0);
   const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
+#endif
   if constexpr (PRO) {  // the row's own value, as k_amg_prolong (padding rows get + 0)
     const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
     float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
@@ -2055,6 +2086,9 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
   const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
+#if CFD_AMG_EARLY
+  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+#endif
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   auto step = [&](uint32_t r0, uint32_t rmax) {
@@ -2080,7 +2114,9 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (u4(dr, k) >= r0) ax[k] += f4(dv, k) * f4(xx, k);
+#if !CFD_AMG_EARLY
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+#endif
   float4 o;
   o.x = bb.x - ax[0];
   o.y = bb.y - ax[1];
