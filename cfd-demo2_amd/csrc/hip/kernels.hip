@@ -1995,13 +1995,11 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 // from the coarse level xc that precedes it (k_amg_prolong) is applied to
 // every x value as it is read, so x' = x + P xc is never stored -- the same
 // f32 operations per value, one launch and one pass over x / agg fewer.
+// smooth4: the 4 rows i0..i0+3
 template <bool D16, int MODE, bool PRO = false>
-__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
-                                                       const float* __restrict__ b,
-                                                       float* __restrict__ x_out,
-                                                       const float* __restrict__ xc = nullptr) {
-  uint32_t i0;
-  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
+__device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __restrict__ x,
+                                          const float* __restrict__ b, uint32_t i0,
+                                          const float* __restrict__ xc = nullptr) {
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
 #if CFD_AMG_EARLY
   // the row's own operands issued with the row lengths (no round trip after the slots)
@@ -2050,7 +2048,16 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
   o.y = wmix(xx.y, (bb.y - sg[1]) / dd.y, 0.8f);
   o.z = wmix(xx.z, (bb.z - sg[2]) / dd.z, 0.8f);
   o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
-  *reinterpret_cast<float4*>(x_out + i0) = o;
+  return o;
+}
+template <bool D16, int MODE, bool PRO = false>
+__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
+                                                       const float* __restrict__ b,
+                                                       float* __restrict__ x_out,
+                                                       const float* __restrict__ xc = nullptr) {
+  uint32_t i0;
+  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO>(L, x, b, i0, xc);
 }
 
 // smooth_op on a level whose x is identically +0 (every coarse level's
@@ -2077,11 +2084,8 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
 template <bool D16, int MODE>
-__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
-                                                         const float* __restrict__ b,
-                                                         float* __restrict__ rr) {
-  uint32_t i0;
-  if (!row_range<CFD_REV_RESIDUAL>(L.r0, L.r1, L.r2, L.r3, i0)) return;
+__device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* __restrict__ x,
+                                            const float* __restrict__ b, uint32_t i0) {
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
   const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
@@ -2122,7 +2126,15 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev
   o.y = bb.y - ax[1];
   o.z = bb.z - ax[2];
   o.w = bb.w - ax[3];
-  *reinterpret_cast<float4*>(rr + i0) = o;
+  return o;
+}
+template <bool D16, int MODE>
+__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ rr) {
+  uint32_t i0;
+  if (!row_range<CFD_REV_RESIDUAL>(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  *reinterpret_cast<float4*>(rr + i0) = residual4<D16, MODE>(L, x, b, i0);
 }
 
 // relax_pressure (schur_precond.wgsl:52-90) on large meshes, 4 rows per thread
@@ -2169,6 +2181,42 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const
 #ifndef CFD_RESTRICT_M4
 #define CFD_RESTRICT_M4 1
 #endif
+// coarse value I of the restriction: sum_{f in R row I, ascending} 1.0 * r[f]
+__device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float* __restrict__ r, uint32_t I) {
+  float sum = 0.0f;
+  if (CFD_RESTRICT_M4 && L.r_m4) {
+    // the first 4 members in one 16-byte load, then their values
+    const int4 m = L.r_m4[I];
+    const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
+    const int f[4] = {m.x, m.y, m.z, over ? -2 - m.w : m.w};
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = r[max(f[q], 0)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (f[q] >= 0) sum += 1.0f * v[q];
+    if (over)  // the members after the fourth, in ascending order
+      for (uint32_t k = L.r_row[I] + 4; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
+  } else {
+    // members fetched 4 at a time (indices clamped to the row's last member,
+    // unused values skipped): one round trip for the indices and one for the
+    // values per 4 members instead of one dependent pair per member
+    const uint32_t k0 = L.r_row[I], k1 = L.r_row[I + 1];
+    for (uint32_t k = k0; k < k1; k += 4) {
+      uint32_t f[4];
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = L.r_col[min(k + q, k1 - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = r[f[q]];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k + q < k1) sum += 1.0f * v[q];
+    }
+  }
+  return sum;
+}
+
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
 // also clears the coarse solution (amg.rs:721-725 `clear`, fused), including
 // its ghost entries [-glo, 0) and [stride_c, stride_c + ghi) on a distributed level
@@ -2181,37 +2229,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
                                                          uint32_t I1) {
   const uint32_t I = I0 + row_id();
   if (I < I1) {
-    float sum = 0.0f;
-    if (CFD_RESTRICT_M4 && L.r_m4) {
-      // the first 4 members in one 16-byte load, then their values
-      const int4 m = L.r_m4[I];
-      const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
-      const int f[4] = {m.x, m.y, m.z, over ? -2 - m.w : m.w};
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = r[max(f[q], 0)];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (f[q] >= 0) sum += 1.0f * v[q];
-      if (over)  // the members after the fourth, in ascending order
-        for (uint32_t k = L.r_row[I] + 4; k < L.r_row[I + 1]; ++k) sum += 1.0f * r[L.r_col[k]];
-    } else {
-      // members fetched 4 at a time (indices clamped to the row's last member,
-      // unused values skipped): one round trip for the indices and one for the
-      // values per 4 members instead of one dependent pair per member
-      const uint32_t k0 = L.r_row[I], k1 = L.r_row[I + 1];
-      for (uint32_t k = k0; k < k1; k += 4) {
-        uint32_t f[4];
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) f[q] = L.r_col[min(k + q, k1 - 1)];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = r[f[q]];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (k + q < k1) sum += 1.0f * v[q];
-      }
-    }
+    const float sum = restrict_sum(L, r, I);
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
       sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
