@@ -106,6 +106,9 @@ __device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock 
 #ifndef CFD_REV_RESIDUAL
 #define CFD_REV_RESIDUAL 1
 #endif
+#ifndef CFD_REV_SMOOTH
+#define CFD_REV_SMOOTH 0  // the AMG smoother sweeps bottom-up (A/B knob)
+#endif
 
 // First row of this thread's 4 in a launch over [r0, r1) and [r2, r3) (the
 // second range lets a distributed rank process both boundary strips of a
@@ -2056,7 +2059,7 @@ __global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L
                                                        float* __restrict__ x_out,
                                                        const float* __restrict__ xc = nullptr) {
   uint32_t i0;
-  if (!row_range(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  if (!row_range<CFD_REV_SMOOTH>(L.r0, L.r1, L.r2, L.r3, i0)) return;
   *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO>(L, x, b, i0, xc);
 }
 
