@@ -95,19 +95,25 @@ __device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock 
 // Kernels that run top-down (xcd_block<true>) to reuse the Infinity Cache lines
 // of the kernel before them (build-time tunables, tools/ab_variants.py).  Same-box
 // A/B at C2 (profiles/r01/ab_reverse_order.txt): k_amg_residual, which follows
-// the bottom-up pre-smoother over the same level matrix, 83.1 -> 67.4 us at
-// level 0; k_spmv, which follows k_precond_correct over the same cval_g / column
-// slots, 233.5 -> 223.1 us; 278.9 -> 273.5 ms/step.  The CGS update after the
-// dots gains nothing (its nontemporal basis reads do not stay in the MALL, and
-// temporal ones cost 20 %), so the CGS kernels keep one direction.
+// the pre-smoother over the same level matrix, 83.1 -> 67.4 us at level 0 when
+// the two sweep in opposite directions; k_spmv, which follows k_precond_correct
+// over the same cval_g / column slots, 233.5 -> 223.1 us; 278.9 -> 273.5
+// ms/step.  Round 3: the smoother top-down and the residual (and the fused
+// residual + restriction) bottom-up instead -- the same alternation, and now
+// each smoother also runs against the bottom-up kernel before it (the Schur
+// prediction writing its b and x, the prolongation): level-0 smoother 77.7 ->
+// 74.7 us, C2 -1.0 / -1.25 ms/step in two same-box pairs
+// (profiles/r03/ab_rev_schur_early_c2.txt, ab_early_operands_c2.txt).  The CGS
+// update after the dots gains nothing (its nontemporal basis reads do not stay
+// in the MALL, and temporal ones cost 20 %), so the CGS kernels keep one direction.
 #ifndef CFD_REV_SPMV
 #define CFD_REV_SPMV 1
 #endif
 #ifndef CFD_REV_RESIDUAL
-#define CFD_REV_RESIDUAL 1
+#define CFD_REV_RESIDUAL 0
 #endif
 #ifndef CFD_REV_SMOOTH
-#define CFD_REV_SMOOTH 0  // the AMG smoother sweeps bottom-up (A/B knob)
+#define CFD_REV_SMOOTH 1
 #endif
 
 // First row of this thread's 4 in a launch over [r0, r1) and [r2, r3) (the
@@ -1595,6 +1601,15 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
 }
 
 // ---- Schur predict / correct with 2 cells per thread (CFD_SCHUR_ROWS = 2) ----
+// Row operands of the 2-cell Schur kernels loaded with the row header (1)
+// or after the slot loop (0): the prediction's dinv_p, the correction's
+// V_j, dinv_uv and own p_sol -- one dependent round trip fewer per wave.
+// Same-box A/B at C2 (profiles/r03/ab_rev_schur_early_c2.txt): prediction
+// 152.3 -> 144.9, correction 135.8 -> 132.4 us, 254.8 -> 253.1 ms/step;
+// C1 39.95 -> 39.22.
+#ifndef CFD_SCHUR_EARLY
+#define CFD_SCHUR_EARLY 1
+#endif
 #ifndef CFD_SCHUR_ROWS
 #define CFD_SCHUR_ROWS 2
 #endif
@@ -1684,6 +1699,9 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   row2_headers(A, i0, lw, dr);
   const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
+#if CFD_SCHUR_EARLY
+  const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
+#endif
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
     predict2_group<D16, U1, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
@@ -1691,7 +1709,9 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
     predict2_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
     predict2_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, lw, dr, d2, rhs);
+#if !CFD_SCHUR_EARLY
   const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
+#endif
   *reinterpret_cast<float2*>(temp_p + i0) = make_float2(rhs[0], rhs[1]);
   *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
   if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
@@ -1742,6 +1762,15 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   uint32_t i0;
   if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
+#if CFD_SCHUR_EARLY
+  // the row pair's own operands issued with the header (no round trip after the slots)
+  const float sc = binv[jv];
+  const float* wb = w_in + 3 * (size_t)i0;
+  const f4u wa = ld4u(wb);
+  const f2u wc = ld2u(wb + 4);
+  const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
+  const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
+#endif
   const uint32_t lw[2] = {lg.x, lg.y};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float cu[2] = {0.0f, 0.0f}, cv[2] = {0.0f, 0.0f};
@@ -1750,13 +1779,15 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   else
     correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
+#if !CFD_SCHUR_EARLY
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;
   const f4u wa = ld4u(wb);
   const f2u wc = ld2u(wb + 4);
-  const float wo[6] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y};
   const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
   const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
+#endif
+  const float wo[6] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y};
   const float dk[2] = {du.x, du.y}, pk[2] = {ps.x, ps.y};
   float o[6];
 #pragma unroll
@@ -1979,6 +2010,19 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 
 // Occupancy floor of the level row kernels (waves per SIMD; 0: the compiler's
 // choice -- 78 / 86 VGPRs, 6 / 5 waves for the smoother / residual)
+// Operands that do not depend on the members' residuals issued first: the
+// fused residual + restriction's member ranges and coarse diagonal, the
+// restriction's coarse diagonal (1); or where they are used (0).  Same-box
+// A/B (profiles/r03/ab_early_operands_c*.txt): C2 restriction 34.6 -> 32.2 us
+// (level 0), C1 fused residual + restriction -0.6 ... -0.8 us per level.
+#ifndef CFD_AMG_PRE2
+#define CFD_AMG_PRE2 1
+#endif
+// The fused post-smoother's own prolongation term (agg -> x_c) issued before
+// the slots (1) or after them (0): 1 was slower on every C1 level (+0.1 ... +0.5 us)
+#ifndef CFD_AMG_PRO_EARLY
+#define CFD_AMG_PRO_EARLY 0
+#endif
 // Row operands (b, x, diagonal) of the smoother / residual loaded at the top
 // (1) or after the slot loop (0)
 #ifndef CFD_AMG_EARLY
@@ -2004,6 +2048,16 @@ __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __r
                                           const float* __restrict__ b, uint32_t i0,
                                           const float* __restrict__ xc = nullptr) {
   const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
+  [[maybe_unused]] float pc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if constexpr (PRO && CFD_AMG_PRO_EARLY) {
+    // the row's own prolongation term, as k_amg_prolong (padding rows get + 0),
+    // issued before the slots: its agg -> x_c round trips overlap them
+    const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
+    pc[0] += 1.0f * xc[ag.x];
+    if (i0 + 1 < L.n) pc[1] += 1.0f * xc[ag.y];
+    if (i0 + 2 < L.n) pc[2] += 1.0f * xc[ag.z];
+    if (i0 + 3 < L.n) pc[3] += 1.0f * xc[ag.w];
+  }
 #if CFD_AMG_EARLY
   // the row's own operands issued with the row lengths (no round trip after the slots)
   const float4 bb = *reinterpret_cast<const float4*>(b + i0);
@@ -2035,16 +2089,17 @@ __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __r
   const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
 #endif
   if constexpr (PRO) {  // the row's own value, as k_amg_prolong (padding rows get + 0)
-    const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
-    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
-    c0 += 1.0f * xc[ag.x];
-    if (i0 + 1 < L.n) c1 += 1.0f * xc[ag.y];
-    if (i0 + 2 < L.n) c2 += 1.0f * xc[ag.z];
-    if (i0 + 3 < L.n) c3 += 1.0f * xc[ag.w];
-    xx.x += c0;
-    xx.y += c1;
-    xx.z += c2;
-    xx.w += c3;
+    if constexpr (!CFD_AMG_PRO_EARLY) {
+      const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
+      pc[0] += 1.0f * xc[ag.x];
+      if (i0 + 1 < L.n) pc[1] += 1.0f * xc[ag.y];
+      if (i0 + 2 < L.n) pc[2] += 1.0f * xc[ag.z];
+      if (i0 + 3 < L.n) pc[3] += 1.0f * xc[ag.w];
+    }
+    xx.x += pc[0];
+    xx.y += pc[1];
+    xx.z += pc[2];
+    xx.w += pc[3];
   }
   float4 o;
   o.x = wmix(xx.x, (bb.x - sg[0]) / dd.x, 0.8f);
@@ -2232,10 +2287,12 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
                                                          uint32_t I1) {
   const uint32_t I = I0 + row_id();
   if (I < I1) {
+    // the coarse diagonal loaded with the members (no round trip after the sum)
+    const float dec = (CFD_AMG_PRE2 && sm_out) ? sm_de[I] : 1.0f;
     const float sum = restrict_sum(L, r, I);
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
-      sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
+      sm_out[I] = wmix(0.0f, (sum - 0.0f) / (CFD_AMG_PRE2 ? dec : sm_de[I]), 0.8f);
     else
       cx[I] = 0.0f;
     return;
@@ -2269,6 +2326,15 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
   const uint32_t I1 = min(I0 + L.rr_agg, L.nc);
   const uint32_t p0 = L.r_row[I0], p1 = L.r_row[I1];
   const uint32_t w = (uint32_t)max(L.w, 1);
+  // this thread's aggregate's member range and coarse diagonal, loaded before
+  // the residual phase (no dependent round trips after the barrier)
+  [[maybe_unused]] uint32_t mk0 = 0, mk1 = 0;
+  [[maybe_unused]] float dec = 1.0f;
+  if (CFD_AMG_PRE2 && I0 + threadIdx.x < I1) {
+    mk0 = L.r_row[I0 + threadIdx.x];
+    mk1 = L.r_row[I0 + threadIdx.x + 1];
+    if (sm_out) dec = sm_de[I0 + threadIdx.x];
+  }
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
     const uint32_t f = L.r_col[p];
     const uint32_t len = L.len[f], dr = L.drank[f];
@@ -2300,11 +2366,16 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
   const uint32_t t = threadIdx.x;
   if (I0 + t >= I1) return;
   const uint32_t I = I0 + t;
+  if (!CFD_AMG_PRE2) {
+    mk0 = L.r_row[I];
+    mk1 = L.r_row[I + 1];
+    if (sm_out) dec = sm_de[I];
+  }
   float sum = 0.0f;
-  for (uint32_t k = L.r_row[I]; k < L.r_row[I + 1]; ++k) sum += 1.0f * rl[k - p0];
+  for (uint32_t k = mk0; k < mk1; ++k) sum += 1.0f * rl[k - p0];
   cb[I] = sum;
   if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
-    sm_out[I] = wmix(0.0f, (sum - 0.0f) / sm_de[I], 0.8f);
+    sm_out[I] = wmix(0.0f, (sum - 0.0f) / dec, 0.8f);
   else
     cx[I] = 0.0f;
 }
