@@ -2582,6 +2582,11 @@ __device__ uint32_t g_tail_st[64];
   do {               \
   } while (0)
 #endif
+// Fused tail phases (1): the zero-x pre-smoother with the residual, the
+// prolongation with the post-smoother (two barriers fewer per level)
+#ifndef CFD_TAIL_FUSE
+#define CFD_TAIL_FUSE 1
+#endif
 __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __restrict__ tail,
                                                         const TailBlobLevel* __restrict__ desc,
                                                         const uint32_t* __restrict__ blob, uint32_t blob_words,
@@ -2656,6 +2661,31 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     float* B = XT + nr;
     float* Rr = B + nr;
     const float* de = fw(D.de);
+    if (CFD_TAIL_FUSE) {
+      // zero-x pre-smoother and residual in one phase: a neighbour's smoothed
+      // value is recomputed from its b and diagonal (the same operations as
+      // the sweep), the row's own is stored for the up-sweep
+      const uint32_t* ro = bw + D.rowoff;
+      const float* val = fw(D.val);
+      const float* dv = fw(D.dv);
+      const uint16_t* col = hw(D.col);
+      const uint8_t* drank = reinterpret_cast<const uint8_t*>(bw + D.drank);
+      for (uint32_t i = t; i < D.n; i += nt) {
+        const float xti = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
+        XT[i] = xti;
+        const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
+        float ax = 0.0f;
+        for (uint32_t r = 0; r <= len; ++r) {
+          if (r == dr) ax += dv[i] * xti;
+          if (r == len) break;
+          const uint32_t j = col[e0 + r];
+          ax += val[e0 + r] * wmix(0.0f, (B[j] - 0.0f) / de[j], 0.8f);
+        }
+        Rr[i] = B[i] - ax;
+      }
+      __syncthreads();
+      TAIL_STAMP();
+    } else {
     for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
     __syncthreads();
   TAIL_STAMP();
@@ -2678,6 +2708,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     }
     __syncthreads();
   TAIL_STAMP();
+    }
     float* CB = base(l + 1) + 2 * r4(desc[l + 1].n);
     {
       const uint16_t* rrow = hw(D.r_row);
@@ -2737,6 +2768,24 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     float* B = XT + nr;
     const float* XC = base(l + 1);
     const uint16_t* agg = hw(D.agg);
+    if (CFD_TAIL_FUSE) {
+      // prolongation and post-smoother in one phase: every value the sweep
+      // reads is prolonged as it is read (k_amg_smooth<..., PRO>'s rule)
+      const uint32_t* ro = bw + D.rowoff;
+      const float* val = fw(D.val);
+      const uint16_t* col = hw(D.col);
+      const float* de = fw(D.de);
+      for (uint32_t i = t; i < D.n; i += nt) {
+        float sigma = 0.0f;
+        for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) {
+          const uint32_t j = col[e];
+          sigma += val[e] * prolonged(XT[j], XC[agg[j]]);
+        }
+        X[i] = wmix(prolonged(XT[i], XC[agg[i]]), (B[i] - sigma) / de[i], 0.8f);
+      }
+      __syncthreads();
+      TAIL_STAMP();
+    } else {
     for (uint32_t i = t; i < D.n; i += nt) {
       float corr = 0.0f;
       corr += 1.0f * XC[agg[i]];
@@ -2747,6 +2796,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     for (uint32_t i = t; i < D.n; i += nt) X[i] = smooth(D, XT, B, i);
     __syncthreads();
   TAIL_STAMP();
+    }
   }
   const float* X0 = base(first);
   float* gx = tail[first].x;
