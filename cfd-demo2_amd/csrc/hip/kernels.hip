@@ -792,14 +792,6 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int
   if (threadIdx.x == 0) norm_out(s, mode, out, inv, g0, host_out);
 }
 
-// axpby (gmres_ops.wgsl:108-117) with alpha = 1, beta = -1: V0 = b - A x
-__global__ void __launch_bounds__(kBlock) k_residual_axpby(const float* __restrict__ b,
-                                                           const float* __restrict__ w,
-                                                           float* v0, size_t n) {
-  const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (e < n) v0[e] = 1.0f * b[e] + -1.0f * w[e];
-}
-
 __device__ __forceinline__ void load2x4(const float2* p, float2 v[4]) {
   const float4 a = *reinterpret_cast<const float4*>(p);
   const float4 b = *reinterpret_cast<const float4*>(p + 2);
@@ -1084,9 +1076,12 @@ __device__ __forceinline__ void row2_headers(const CoupledMatrix& A, uint32_t i0
   dr[0] = drr.x;
   dr[1] = drr.y;
 }
+// b != null: y = 1 * b + -1 * (A x), the residual's axpby (gmres_ops.wgsl:108-117)
+// applied to each output element as it is stored (compute_residual_into: the
+// product itself is not needed)
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* __restrict__ x,
-                                                  float* __restrict__ y) {
+                                                  float* __restrict__ y, const float* __restrict__ b) {
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   uint32_t i0;
   if (!row_range2<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
@@ -1117,6 +1112,15 @@ __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* 
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv2_group<D16, U>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
   float* yo = y + 3 * (size_t)i0;  // 8-byte aligned (i0 even)
   typedef float f2v __attribute__((ext_vector_type(2)));
+  if (b) {
+    const float* bo = b + 3 * (size_t)i0;
+    const f4u b4 = ld4u(bo);
+    const f2u b2 = ld2u(bo + 4);
+    *reinterpret_cast<f4u*>(yo) = f4u{1.0f * b4.x + -1.0f * su[0], 1.0f * b4.y + -1.0f * sv[0],
+                                      1.0f * b4.z + -1.0f * sp[0], 1.0f * b4.w + -1.0f * su[1]};
+    *reinterpret_cast<f2v*>(yo + 4) = f2v{1.0f * b2.x + -1.0f * sv[1], 1.0f * b2.y + -1.0f * sp[1]};
+    return;
+  }
   *reinterpret_cast<f4u*>(yo) = f4u{su[0], sv[0], sp[0], su[1]};
   *reinterpret_cast<f2v*>(yo + 4) = f2v{sv[1], sp[1]};
 }
@@ -2972,19 +2976,17 @@ void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, floa
   hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0, g_len,
                      host_out);
 }
-void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_residual_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, b, w, v0, n);
-}
-void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s) {
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
   if (CFD_SPMV_ROWS == 2) {
     const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
     if (A.use16)
-      hipLaunchKernelGGL(k_spmv2<true>, dim3(nb2), dim3(kBlock), 0, s, A, x, y);
+      hipLaunchKernelGGL(k_spmv2<true>, dim3(nb2), dim3(kBlock), 0, s, A, x, y, b);
     else
-      hipLaunchKernelGGL(k_spmv2<false>, dim3(nb2), dim3(kBlock), 0, s, A, x, y);
+      hipLaunchKernelGGL(k_spmv2<false>, dim3(nb2), dim3(kBlock), 0, s, A, x, y, b);
     return;
   }
+  if (b) throw std::invalid_argument("launch_spmv: the fused residual needs the 2-cell SpMV");
   const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
     hipLaunchKernelGGL(k_spmv<true>, dim3(nb), dim3(kBlock), 0, s, A, x, y);

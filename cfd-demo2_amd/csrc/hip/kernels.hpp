@@ -288,8 +288,8 @@ void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, 
 // g0 (mode 2): g0[0] = norm, g0[1..g_len) = 0; host_out (device view of pinned host memory, or null) = norm
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, int g_len, float* host_out,
                          hipStream_t s);
-void launch_residual_axpby(const float* b, const float* w, float* v0, size_t n, hipStream_t s);
-void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s);
+// b != null: y = b - A x with the residual axpby's operations (1 * b + -1 * (A x))
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b = nullptr);
 // basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,

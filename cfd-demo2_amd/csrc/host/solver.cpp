@@ -1414,9 +1414,8 @@ void Solver::residual_into_v0_launch() {
     A.r1 = b;
     A.r2 = a2;
     A.r3 = b2;
-    launch_spmv(A, x, w, stream);
+    launch_spmv(A, x, basis, stream, rhs);  // V0 = 1 * b + -1 * (A x) as the SpMV stores it
   });
-  launch_residual_axpby(rhs, w, basis, 3 * (size_t)N, stream);
   norm_launch(basis, 2, 1);
 }
 
@@ -1960,7 +1959,7 @@ double Solver::layout_step_bytes() const {
     inner += predict + vc + correct + spmv;
     inner += (j + 2) * 12.0 * Nn + (j + 3) * 12.0 * Nn;    // CGS dots, CGS update + norm
   }
-  const double residual = spmv + 36 * Nn + 12 * Nn;       // SpMV, axpby, norm
+  const double residual = spmv + 12 * Nn + 12 * Nn;       // SpMV storing b - A x (b read), norm
   const double solve = 12 * Nn + residual + inner + (M + 2) * 12.0 * Nn + residual;
   return K * (prep + asmb + solve + 36 * Nn);  // prepare: once per Picard iteration (scheme 0)
 }
