@@ -21,12 +21,10 @@ namespace cfd2 {
 
 namespace {
 
-#ifndef CFD_CGS_NT
-#define CFD_CGS_NT 1
-#endif
-#ifndef CFD_CGS_NT_ST
-#define CFD_CGS_NT_ST CFD_CGS_NT  // nontemporal stores of the new basis vector
-#endif
+// Tuning constants below are plain numbers (A/B-tuned with
+// tools/ab_variants.py); every compile-time switch between two code paths
+// was removed once its A/B was decided (round 4; git history keeps the losers).
+//
 // One basis load in flight per wavefront in the CGS kernels (load_cells3 SER)
 // on meshes of at least this many cells (per rank); below it, every load of a
 // wavefront stays in flight together.  With ~15+ blocks per CU the serialised
@@ -37,9 +35,6 @@ namespace {
 #define CFD_CGS_SER_MIN_CELLS (1u << 22)
 #endif
 
-#ifndef CFD_DPP_TREE
-#define CFD_DPP_TREE 1  // wavefront trees of the chunk kernels by DPP (wave_tree64)
-#endif
 #ifndef CFD_RED_SEGS
 #define CFD_RED_SEGS 4  // independent partial loads per lane in the finishing kernels
 #endif
@@ -106,15 +101,9 @@ __device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock 
 // (profiles/r03/ab_rev_schur_early_c2.txt, ab_early_operands_c2.txt).  The CGS
 // update after the dots gains nothing (its nontemporal basis reads do not stay
 // in the MALL, and temporal ones cost 20 %), so the CGS kernels keep one direction.
-#ifndef CFD_REV_SPMV
-#define CFD_REV_SPMV 1
-#endif
-#ifndef CFD_REV_RESIDUAL
-#define CFD_REV_RESIDUAL 0
-#endif
-#ifndef CFD_REV_SMOOTH
-#define CFD_REV_SMOOTH 1
-#endif
+constexpr bool kRevSpmv = true;       // k_spmv2: top-down, after the bottom-up Schur correction
+constexpr bool kRevResidual = false;  // k_amg_residual / k_amg_resrestrict: bottom-up
+constexpr bool kRevSmooth = true;     // k_amg_smooth: top-down
 
 // First row of this thread's 4 in a launch over [r0, r1) and [r2, r3) (the
 // second range lets a distributed rank process both boundary strips of a
@@ -667,7 +656,7 @@ __device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[
     if (FULL || c < N) {
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
-        if constexpr (NT && CFD_CGS_NT)
+        if constexpr (NT)
           v[q][e] = __builtin_nontemporal_load(p + 3 * c + e);
         else
           v[q][e] = p[3 * c + e];
@@ -685,13 +674,7 @@ __device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const 
     const size_t c = cell_q(q);
     if (FULL || c < N) {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) {
-#if CFD_CGS_NT_ST
-        __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
-#else
-        p[3 * c + e] = v[q][e];
-#endif
-      }
+      for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
     }
   }
 }
@@ -707,7 +690,6 @@ __device__ __forceinline__ float row_down(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + S, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float wave_tree64(float v) {
-#if CFD_DPP_TREE
   v = v + row_down<1>(v);
   v = v + row_down<2>(v);
   v = v + row_down<4>(v);
@@ -717,9 +699,6 @@ __device__ __forceinline__ float wave_tree64(float v) {
   const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
   const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
   return (r0 + r1) + (r2 + r3);
-#else
-  return wave_tree(v);
-#endif
 }
 // quarters of the block's chunks: lds[4 q + w] = wave_tree of wavefront w's
 // cell terms t[q] (written by lane 0)
@@ -792,45 +771,15 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_reduce_final(RedSrc r, int
   if (threadIdx.x == 0) norm_out(s, mode, out, inv, g0, host_out);
 }
 
-__device__ __forceinline__ void load2x4(const float2* p, float2 v[4]) {
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  const float4 b = *reinterpret_cast<const float4*>(p + 2);
-  v[0] = make_float2(a.x, a.y);
-  v[1] = make_float2(a.z, a.w);
-  v[2] = make_float2(b.x, b.y);
-  v[3] = make_float2(b.z, b.w);
-}
-template <bool D16>
-__device__ __forceinline__ void ccols4(const CoupledMatrix& A, size_t off, uint32_t i0, int c[4]) {
-  if constexpr (D16) {
-    const short4 d = *reinterpret_cast<const short4*>(A.col16 + off);
-    c[0] = (int)i0 + (int)d.x;
-    c[1] = (int)i0 + 1 + (int)d.y;
-    c[2] = (int)i0 + 2 + (int)d.z;
-    c[3] = (int)i0 + 3 + (int)d.w;
-  } else {
-    const int4 q = *reinterpret_cast<const int4*>(A.col + off);
-    c[0] = q.x;
-    c[1] = q.y;
-    c[2] = q.z;
-    c[3] = q.w;
-  }
-}
-// Gathers of the 4-cells-per-thread kernels.  Unused ELL slots and padding
-// rows hold the row's own (valid) index, so a gather can be issued
-// unconditionally (ALWAYS): no branch per load, and the three loads of one
-// cell's (u, v, p) merge into one dwordx3; the value of an unused slot is
-// never consumed (every accumulation skips r >= len), so results are
-// unchanged.  Same-box A/B (tools/gpu_ab_prof.sh, C2): a win for k_spmv
-// (253 -> 246 us) and k_amg_smooth (84 -> 81 us), a loss for the Schur
-// kernels and k_amg_residual (whose extra diagonal pass would load a whole
-// unused slot group), so those keep the predicated form.
-#ifndef CFD_GATHER_ALWAYS
-#define CFD_GATHER_ALWAYS 1
-#endif
+// Gathers of the row kernels.  Unused ELL slots and padding rows hold the
+// row's own (valid) index, so a gather can be issued unconditionally
+// (ALWAYS): no branch per load; the value of an unused slot is never consumed
+// (every accumulation skips r >= len), so results are unchanged.  Same-box
+// A/B (round 1, C2): k_amg_smooth 84 -> 81 us; k_amg_residual keeps the
+// predicated form on its MODE 0 levels.
 template <bool ALWAYS = false>
 __device__ __forceinline__ float gat(bool on, const float* p) {
-  if constexpr (ALWAYS && CFD_GATHER_ALWAYS) {
+  if constexpr (ALWAYS) {
     (void)on;
     return *p;
   } else {
@@ -838,22 +787,16 @@ __device__ __forceinline__ float gat(bool on, const float* p) {
   }
 }
 
-// Vector gathers: the columns of one slot for 4 consecutive rows are, for
-// every interior row of a face stencil, 4 consecutive cells (c, c+1, c+2,
-// c+3): one 16-byte load (dword-aligned: gfx950 global loads need only
-// 4-byte alignment for multi-dword accesses) fetches all four, and only
-// threads whose slot is not consecutive (boundary / cut cells) issue the
-// per-row loads.  Cuts the gather instructions per wave ~4x for scalar
-// vectors (the row kernels are VMEM-issue bound: SQ_WAIT_INST_ANY ~0.5-0.7
-// of wave cycles, tools/gpu_sq.sh).  Every vector read this
-// way has >= 64 floats of padding past its last (ghost) entry.
-#ifndef CFD_VGATHER
-#define CFD_VGATHER 1
-#endif
-// k_spmv keeps one dwordx3 per (cell, slot): its 12-float vector form was
-// slower in the same-box A/B (234 -> 250 us) while the scalar-vector kernels
-// gained (level-0 smoother 84 -> 78 us, Schur predict 198 -> 185, correct
-// 166 -> 159)
+// Vector gathers: the columns of one slot for consecutive rows are, for
+// every interior row of a face stencil, consecutive cells (c, c+1, ...): one
+// 16-byte load (dword-aligned: gfx950 global loads need only 4-byte alignment
+// for multi-dword accesses) fetches them all, and only threads whose slot is
+// not consecutive (boundary / cut cells) issue the per-row loads.  Cuts the
+// gather instructions per wave ~4x for scalar vectors (the row kernels are
+// VMEM-issue bound: SQ_WAIT_INST_ANY ~0.5-0.7 of wave cycles,
+// tools/gpu_sq.sh; round 1: level-0 smoother 84 -> 78 us, Schur predict
+// 198 -> 185, correct 166 -> 159).  Every vector read this way has >= 64
+// floats of padding past its last (ghost) entry.
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ f2u ld2u(const float* p) { return *reinterpret_cast<const f2u*>(p); }
@@ -862,7 +805,47 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
   return c[1] == c[0] + 1 && c[2] == c[0] + 2 && c[3] == c[0] + 3;
 }
 
-// Slot-group sizes of the 4-cells-per-thread kernels (all loads of a group are
+// Loads of a kernel's once-read streams (matrix slots, row headers, the rows'
+// own operands) with the nontemporal policy (NT: global_load ... nt) or the
+// default one.  NT is chosen per launch for the kernels that are the LAST
+// readers of their matrix before it is evicted anyway, so its lines do not
+// displace, in the 256 MB Infinity Cache, the vectors the next kernels read
+// (Solver::nt_mask).  Same bits either way.
+template <bool NT, class V>
+__device__ __forceinline__ V ldx(const V* p) {
+  if constexpr (!NT) {
+    return *p;
+  } else {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    V r;
+    if constexpr (sizeof(V) == 16) {
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+      __builtin_memcpy(&r, &t, 16);
+    } else if constexpr (sizeof(V) == 8) {
+      const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+      __builtin_memcpy(&r, &t, 8);
+    } else if constexpr (sizeof(V) == 4) {
+      const uint32_t t = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+      __builtin_memcpy(&r, &t, 4);
+    } else if constexpr (sizeof(V) == 2) {
+      const uint16_t t = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(p));
+      __builtin_memcpy(&r, &t, 2);
+    } else {
+      static_assert(sizeof(V) == 1, "ldx: 1, 2, 4, 8 or 16 bytes");
+      const uint8_t t = __builtin_nontemporal_load(reinterpret_cast<const uint8_t*>(p));
+      __builtin_memcpy(&r, &t, 1);
+    }
+    return r;
+  }
+}
+// typed views for ldx of an address inside an array of another element type
+template <bool NT, class V, class T>
+__device__ __forceinline__ V ldv(const T* p) {
+  return ldx<NT>(reinterpret_cast<const V*>(p));
+}
+
+// Slot-group sizes of the coupled row kernels (all loads of a group are
 // issued before the first use).  Build-time tunables (tools/ab_variants.py).
 #ifndef CFD_SPMV_U
 #define CFD_SPMV_U 4
@@ -881,92 +864,21 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
 // per slot the compiler issues a whole group's matrix loads back to back
 // (a predicated load per slot made it wait for each slot's column load
 // before issuing the next slot), and the first group does not wait for the
-// row lengths.  The first group is sized to cover a whole interior row
+// row lengths.  The first group (U1) is sized to cover a whole interior row
 // (5 entries of a quad cell's coupled row).
-// SpMV: the first slot group's cval_a / cval_g loads issued with the row
+// SpMV: the first slot group's cval_a / cval_g loads are issued with the row
 // headers, before the wait for them (C2 216 -> 197 us; the same for the
 // Schur prediction lost 150 -> 158 us: profiles/r03/ab_coupled_pre_c2.txt;
 // the regular rows' x gathers issued speculatively as well gained nothing
 // more, 198 -> 200 us: ab_spmv_spec_c2.txt)
-#ifndef CFD_COUPLED_PRE
-#define CFD_COUPLED_PRE 1
-#endif
 #ifndef CFD_SPMV_U1
 #define CFD_SPMV_U1 5
 #endif
 
-// spmv (gmres_ops.wgsl:63-81) on compressed blocks, 4 cells (12 rows) per
-// thread; per-row term order identical to the CSR row (neighbour-major, u,v,p).
-template <bool D16, int U>
-__device__ __forceinline__ void spmv_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
-                                           uint32_t r0, uint32_t rmax, const ushort4 ln, const uchar4 dr,
-                                           const float2 d2[4], float su[4], float sv[4], float sp[4]) {
-  float2 a[U][4], g[U][4];
-  int c[U][4];
-  float xg[U][4][3];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    load2x4(A.cval_a + off, a[u]);
-    load2x4(A.cval_g + off, g[u]);
-    ccols4<D16>(A, off, i0, c[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool on = lg_on(ln, k, r0 + u);
-      const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-      xg[u][k][0] = gat<true>(on, x + j);
-      xg[u][k][1] = gat<true>(on, x + j + 1);
-      xg[u][k][2] = gat<true>(on, x + j + 2);
-    }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t r = r0 + u;
-      if (!lg_on(ln, k, r)) continue;
-      const bool dg = (r == u4(dr, k));
-      const float uu = a[u][k].x, pp = a[u][k].y, up = g[u][k].x, vp = g[u][k].y;
-      const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
-      const float xu = xg[u][k][0], xv = xg[u][k][1], xp = xg[u][k][2];
-      su[k] += uu * xu;
-      su[k] += 0.0f * xv;
-      su[k] += up * xp;
-      sv[k] += 0.0f * xu;
-      sv[k] += uu * xv;
-      sv[k] += vp * xp;
-      sp[k] += pu * xu;
-      sp[k] += pv * xv;
-      sp[k] += pp * xp;
-    }
-}
-
-template <bool D16>
-__global__ void __launch_bounds__(kBlock) k_spmv(CoupledMatrix A, const float* __restrict__ x,
-                                                 float* __restrict__ y) {
-  constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
-  uint32_t i0;
-  if (!row_range<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
-  const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
-  float2 d2[4];
-  load2x4(A.cdiag2 + i0, d2);
-  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
-  float su[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sp[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  spmv_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, su, sv, sp);
-  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv_group<D16, U>(A, x, i0, r0, maxlen - 1u, ln, dr, d2, su, sv, sp);
-  const float o[12] = {su[0], sv[0], sp[0], su[1], sv[1], sp[1], su[2], sv[2], sp[2], su[3], sv[3], sp[3]};
-  store12(y + 3 * (size_t)i0, o);
-}
-
-// The same SpMV with 2 cells (6 rows) per thread: half the registers per slot
-// group (102 instead of 196 VGPRs: 4 wavefronts per SIMD instead of 2), one
-// 16-byte load per slot array; same-box A/B at C2: 225.8 -> 218.0 us.
-#ifndef CFD_SPMV_ROWS
-#define CFD_SPMV_ROWS 2
-#endif
+// The coupled row kernels (SpMV, Schur predict / correct) take 2 cells (6
+// rows) per thread: half the registers per slot group of the 4-cell form
+// (102 instead of 196 VGPRs: 4 wavefronts per SIMD instead of 2), one 16-byte
+// load per slot array; same-box A/B at C2 (round 2): SpMV 225.8 -> 218.0 us.
 template <bool REV = false>
 __device__ __forceinline__ bool row_range2(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
   const uint32_t t = row_id<REV>(), na = (r1 - r0 + 1) / 2;
@@ -981,13 +893,26 @@ inline unsigned rows2x_grid(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3) 
   const size_t t = (size_t)(r1 - r0 + 1) / 2 + (r3 > r2 ? (size_t)(r3 - r2 + 1) / 2 : 0);
   return (unsigned)((t + 255) / 256);
 }
+// the two rows' columns of slot offset `off`
+template <bool D16, bool NT = false>
+__device__ __forceinline__ void ccols2(const CoupledMatrix& A, size_t off, uint32_t i0, int c[2]) {
+  if constexpr (D16) {
+    const short2 d = ldv<NT, short2>(A.col16 + off);
+    c[0] = (int)i0 + (int)d.x;
+    c[1] = (int)i0 + 1 + (int)d.y;
+  } else {
+    const int2 q = ldv<NT, int2>(A.col + off);
+    c[0] = q.x;
+    c[1] = q.y;
+  }
+}
 __device__ __forceinline__ bool lg2_on(uint32_t w, uint32_t r) { return r < (w & kLgUsedMask) && !((w >> 8 >> r) & 1u); }
 // REG (first slot group of a wave of regular rows, r0 = 0): columns
 // row + tmode[slot] (no column loads), and the two rows' x entries are six
 // consecutive floats (one 16-byte + one 8-byte gather)
 // PRE: the group's cval_a / cval_g slots were loaded by the caller (first
 // group: issued right after the row headers, before the wait for them)
-template <bool D16, int U, bool REG = false, bool PRE = false>
+template <bool D16, int U, bool REG = false, bool PRE = false, bool NT = false>
 __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float* __restrict__ x, uint32_t i0,
                                             uint32_t r0, uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
                                             const float2 d2[2], float su[2], float sv[2], float sp[2],
@@ -1002,20 +927,14 @@ __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float*
       a[u] = pa[u];
       g[u] = pg[u];
     } else {
-      a[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
-      g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+      a[u] = ldv<NT, float4>(A.cval_a + off);
+      g[u] = ldv<NT, float4>(A.cval_g + off);
     }
     if constexpr (REG) {
       c[u][0] = (int)i0 + A.tmode[u];
       c[u][1] = c[u][0] + 1;
-    } else if constexpr (D16) {
-      const short2 d = *reinterpret_cast<const short2*>(A.col16 + off);
-      c[u][0] = (int)i0 + (int)d.x;
-      c[u][1] = (int)i0 + 1 + (int)d.y;
     } else {
-      const int2 q = *reinterpret_cast<const int2*>(A.col + off);
-      c[u][0] = q.x;
-      c[u][1] = q.y;
+      ccols2<D16, NT>(A, off, i0, c[u]);
     }
   }
   if constexpr (REG) {
@@ -1068,9 +987,10 @@ __device__ __forceinline__ void spmv2_group(const CoupledMatrix& A, const float*
 // into one u32 per row (one load fewer) lost at C2: SpMV 208 -> 213, Schur
 // prediction 155 -> 160 us (profiles/r03/ab_log.md) -- 2 bytes more per row
 // cost more than the instruction saved.
+template <bool NT = false>
 __device__ __forceinline__ void row2_headers(const CoupledMatrix& A, uint32_t i0, uint32_t lw[2], uint32_t dr[2]) {
-  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
-  const uchar2 drr = *reinterpret_cast<const uchar2*>(A.drank + i0);
+  const ushort2 lg = ldv<NT, ushort2>(A.lg + i0);
+  const uchar2 drr = ldv<NT, uchar2>(A.drank + i0);
   lw[0] = lg.x;
   lw[1] = lg.y;
   dr[0] = drr.x;
@@ -1079,43 +999,38 @@ __device__ __forceinline__ void row2_headers(const CoupledMatrix& A, uint32_t i0
 // b != null: y = 1 * b + -1 * (A x), the residual's axpby (gmres_ops.wgsl:108-117)
 // applied to each output element as it is stored (compute_residual_into: the
 // product itself is not needed)
-template <bool D16>
+template <bool D16, bool NT>
 __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* __restrict__ x,
                                                   float* __restrict__ y, const float* __restrict__ b) {
   constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
   uint32_t i0;
-  if (!row_range2<CFD_REV_SPMV>(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  if (!row_range2<kRevSpmv>(A.r0, A.r1, A.r2, A.r3, i0)) return;
   uint32_t lw[2], dr[2];
-  row2_headers(A, i0, lw, dr);
-  const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
+  row2_headers<NT>(A, i0, lw, dr);
+  const float4 dd = ldv<NT, float4>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float su[2] = {0.0f, 0.0f}, sv[2] = {0.0f, 0.0f}, sp[2] = {0.0f, 0.0f};
-#if CFD_COUPLED_PRE
+  // the first slot group's values issued with the row headers (see CFD_SPMV_U1)
   float4 pa[U1], pg[U1];
 #pragma unroll
   for (int u = 0; u < U1; ++u) {
     const size_t off = (size_t)min((uint32_t)u, (uint32_t)A.ws - 1u) * A.ld + i0;
-    pa[u] = *reinterpret_cast<const float4*>(A.cval_a + off);
-    pg[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    pa[u] = ldv<NT, float4>(A.cval_a + off);
+    pg[u] = ldv<NT, float4>(A.cval_g + off);
   }
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
-    spmv2_group<D16, U1, true, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
+    spmv2_group<D16, U1, true, true, NT>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
   else
-    spmv2_group<D16, U1, false, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
-#else
-  if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
-    spmv2_group<D16, U1, true>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
-  else
-    spmv2_group<D16, U1>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp);
-#endif
-  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) spmv2_group<D16, U>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
+    spmv2_group<D16, U1, false, true, NT>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
+    spmv2_group<D16, U, false, false, NT>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
   float* yo = y + 3 * (size_t)i0;  // 8-byte aligned (i0 even)
   typedef float f2v __attribute__((ext_vector_type(2)));
   if (b) {
     const float* bo = b + 3 * (size_t)i0;
-    const f4u b4 = ld4u(bo);
-    const f2u b2 = ld2u(bo + 4);
+    const f4u b4 = ldv<NT, f4u>(bo);
+    const f2u b2 = ldv<NT, f2u>(bo + 4);
     *reinterpret_cast<f4u*>(yo) = f4u{1.0f * b4.x + -1.0f * su[0], 1.0f * b4.y + -1.0f * sv[0],
                                       1.0f * b4.z + -1.0f * sp[0], 1.0f * b4.w + -1.0f * su[1]};
     *reinterpret_cast<f2v*>(yo + 4) = f2v{1.0f * b2.x + -1.0f * sv[1], 1.0f * b2.y + -1.0f * sp[1]};
@@ -1281,117 +1196,9 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int 
   if (host_resid) host_resid[0] = fabsf(gn);
 }
 
-// predict_and_form_schur (schur_precond.wgsl:142-188), 4 cells per thread.
-// z_u, z_v of the prediction are recomputed by k_precond_correct (same two
-// multiplies), so this kernel writes only the Schur rhs and the first Jacobi
-// iterate.  The term `A_pp * 0.0` of the reference loop is dropped: it can
-// only flip the sign of a zero rhs_p, and its A_pp read is the largest byte
-// cost of the row.
-#ifndef CFD_SCHUR_GATHER_ALWAYS
-#define CFD_SCHUR_GATHER_ALWAYS 1
-#endif
 #ifndef CFD_PREDICT_U1
 #define CFD_PREDICT_U1 5
 #endif
-template <bool D16, int U>
-__device__ __forceinline__ void predict_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
-                                              const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
-                                              uint32_t rmax, const ushort4 ln, const uchar4 dr, const float2 d2[4],
-                                              float rhs[4]) {
-  float2 g[U][4];
-  int c[U][4];
-  float gd[U][4], gu[U][4], gv[U][4];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    load2x4(A.cval_g + off, g[u]);
-    ccols4<D16>(A, off, i0, c[u]);
-  }
-  if constexpr (CFD_VGATHER) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const f4u d = ld4u(dinv_uv + c[u][0]);
-      const float* b = w_in + 3 * (ptrdiff_t)c[u][0];
-      const f4u q0 = ld4u(b), q1 = ld4u(b + 4), q2 = ld4u(b + 8);
-      const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-      const float dd[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        gd[u][k] = dd[k];
-        gu[u][k] = f[3 * k];
-        gv[u][k] = f[3 * k + 1];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (!consec4(c[u])) {
-#pragma unroll
-        for (int k = 1; k < 4; ++k) {
-          const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-          gd[u][k] = dinv_uv[c[u][k]];
-          gu[u][k] = w_in[j];
-          gv[u][k] = w_in[j + 1];
-        }
-      }
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool on = lg_on(ln, k, r0 + u);
-        const ptrdiff_t j = 3 * (ptrdiff_t)c[u][k];
-        gd[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, dinv_uv + c[u][k]);
-        gu[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j);
-        gv[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(on, w_in + j + 1);
-      }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t r = r0 + u;
-      if (!lg_on(ln, k, r)) continue;
-      const bool dg = (r == u4(dr, k));
-      const float pu = dg ? d2[k].x : g[u][k].x, pv = dg ? d2[k].y : g[u][k].y;
-      const float ru = sc * gu[u][k], rv = sc * gv[u][k];
-      const float zu = ru * gd[u][k];
-      const float zv = rv * gd[u][k];
-      rhs[k] -= pu * zu;
-      rhs[k] -= pv * zv;
-    }
-}
-
-template <bool D16>
-__global__ void __launch_bounds__(kBlock) k_precond_predict(CoupledMatrix A,
-                                                            const float* __restrict__ w_in,
-                                                            const float* __restrict__ binv, int jv,
-                                                            const float* __restrict__ dinv_uv,
-                                                            const float* __restrict__ dinv_p,
-                                                            float* temp_p, float* p_sol,
-                                                            float* p_prev) {
-  constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
-  uint32_t i0;
-  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const float sc = binv[jv];
-  float wo[12];
-  load12(w_in + 3 * (size_t)i0, wo);
-  float rhs[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) rhs[k] = sc * wo[3 * k + 2];
-  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
-  const uchar4 dr = *reinterpret_cast<const uchar4*>(A.drank + i0);
-  float2 d2[4];
-  load2x4(A.cdiag2 + i0, d2);
-  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
-  predict_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, ln, dr, d2, rhs);
-  for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
-    predict_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, ln, dr, d2, rhs);
-  const float4 dp = *reinterpret_cast<const float4*>(dinv_p + i0);
-  *reinterpret_cast<float4*>(temp_p + i0) = make_float4(rhs[0], rhs[1], rhs[2], rhs[3]);
-  *reinterpret_cast<float4*>(p_sol + i0) =
-      make_float4(dp.x * rhs[0], dp.y * rhs[1], dp.z * rhs[2], dp.w * rhs[3]);
-  if (p_prev) *reinterpret_cast<float4*>(p_prev + i0) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-}
 
 // relax_pressure (schur_precond.wgsl:52-90), omega = 1.2, live scalar matrix
 __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t ld, const int32_t* __restrict__ col,
@@ -1522,114 +1329,18 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   }
 }
 
-// correct_velocity (schur_precond.wgsl:93-139) fused with the velocity
-// prediction of predict_and_form_schur: z_u = d_u r_u - d_u * sum(A_up p_sol);
-// 4 cells per thread.
 #ifndef CFD_CORRECT_U1
 #define CFD_CORRECT_U1 5
 #endif
-template <bool D16, int U>
-__device__ __forceinline__ void correct_group(const CoupledMatrix& A, const float* __restrict__ p_sol,
-                                              uint32_t i0, uint32_t r0, uint32_t rmax, const ushort4 ln, float cu[4],
-                                              float cv[4]) {
-  float2 g[U][4];
-  int c[U][4];
-  float pj[U][4];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    load2x4(A.cval_g + off, g[u]);
-    ccols4<D16>(A, off, i0, c[u]);
-  }
-  if constexpr (CFD_VGATHER) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const f4u q = ld4u(p_sol + c[u][0]);
-      pj[u][0] = q.x;
-      pj[u][1] = q.y;
-      pj[u][2] = q.z;
-      pj[u][3] = q.w;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (!consec4(c[u])) {
-#pragma unroll
-        for (int k = 1; k < 4; ++k) pj[u][k] = p_sol[c[u][k]];
-      }
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) pj[u][k] = gat<CFD_SCHUR_GATHER_ALWAYS>(lg_on(ln, k, r0 + u), p_sol + c[u][k]);
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!lg_on(ln, k, r0 + u)) continue;
-      cu[k] += g[u][k].x * pj[u][k];
-      cv[k] += g[u][k].y * pj[u][k];
-    }
-}
 
-template <bool D16>
-__global__ void __launch_bounds__(kBlock) k_precond_correct(CoupledMatrix A,
-                                                            const float* __restrict__ w_in,
-                                                            const float* __restrict__ binv, int jv,
-                                                            const float* __restrict__ p_sol,
-                                                            const float* __restrict__ dinv_uv,
-                                                            float* __restrict__ z) {
-  constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
-  uint32_t i0;
-  if (!row_range(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const ushort4 ln = *reinterpret_cast<const ushort4*>(A.lg + i0);
-  const uint32_t maxlen = max(max(lg_used(ln, 0), lg_used(ln, 1)), max(lg_used(ln, 2), lg_used(ln, 3)));
-  float cu[4] = {0.0f, 0.0f, 0.0f, 0.0f}, cv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  correct_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, ln, cu, cv);
-  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, ln, cu, cv);
-  const float sc = binv[jv];
-  float wo[12], o[12];
-  load12(w_in + 3 * (size_t)i0, wo);
-  const float4 du4 = *reinterpret_cast<const float4*>(dinv_uv + i0);
-  const float4 ps4 = *reinterpret_cast<const float4*>(p_sol + i0);
-  const float du[4] = {du4.x, du4.y, du4.z, du4.w}, ps[4] = {ps4.x, ps4.y, ps4.z, ps4.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float ru = sc * wo[3 * k], rv = sc * wo[3 * k + 1];
-    const float zu = du[k] * ru, zv = du[k] * rv;
-    o[3 * k] = zu - du[k] * cu[k];
-    o[3 * k + 1] = zv - du[k] * cv[k];
-    o[3 * k + 2] = ps[k];
-  }
-  store12(z + 3 * (size_t)i0, o);
-}
-
-// ---- Schur predict / correct with 2 cells per thread (CFD_SCHUR_ROWS = 2) ----
-// Row operands of the 2-cell Schur kernels loaded with the row header (1)
-// or after the slot loop (0): the prediction's dinv_p, the correction's
-// V_j, dinv_uv and own p_sol -- one dependent round trip fewer per wave.
+// ---- Schur predict / correct, 2 cells per thread ----
+// The row operands of the Schur kernels are loaded with the row header, not
+// after the slot loop: the prediction's dinv_p, the correction's V_j,
+// dinv_uv and own p_sol -- one dependent round trip fewer per wave.
 // Same-box A/B at C2 (profiles/r03/ab_rev_schur_early_c2.txt): prediction
 // 152.3 -> 144.9, correction 135.8 -> 132.4 us, 254.8 -> 253.1 ms/step;
 // C1 39.95 -> 39.22.
-#ifndef CFD_SCHUR_EARLY
-#define CFD_SCHUR_EARLY 1
-#endif
-#ifndef CFD_SCHUR_ROWS
-#define CFD_SCHUR_ROWS 2
-#endif
-template <bool D16>
-__device__ __forceinline__ void ccols2(const CoupledMatrix& A, size_t off, uint32_t i0, int c[2]) {
-  if constexpr (D16) {
-    const short2 d = *reinterpret_cast<const short2*>(A.col16 + off);
-    c[0] = (int)i0 + (int)d.x;
-    c[1] = (int)i0 + 1 + (int)d.y;
-  } else {
-    const int2 q = *reinterpret_cast<const int2*>(A.col + off);
-    c[0] = q.x;
-    c[1] = q.y;
-  }
-}
-template <bool D16, int U, bool REG = false>  // REG: see spmv2_group
+template <bool D16, int U, bool REG = false, bool NT = false>  // REG: see spmv2_group
 __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
                                                const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
                                                uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
@@ -1640,12 +1351,12 @@ __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const flo
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
+    g[u] = ldv<NT, float4>(A.cval_g + off);
     if constexpr (REG) {
       c[u][0] = (int)i0 + A.tmode[u];
       c[u][1] = c[u][0] + 1;
     } else {
-      ccols2<D16>(A, off, i0, c[u]);
+      ccols2<D16, NT>(A, off, i0, c[u]);
     }
   }
 #pragma unroll
@@ -1685,7 +1396,7 @@ __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const flo
       rhs[k] -= pv * zv;
     }
 }
-template <bool D16>
+template <bool D16, bool NT>
 __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, const float* __restrict__ w_in,
                                                              const float* __restrict__ binv, int jv,
                                                              const float* __restrict__ dinv_uv,
@@ -1700,22 +1411,17 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   const f2u wc = ld2u(wb + 4);
   float rhs[2] = {sc * wa.z, sc * wc.y};
   uint32_t lw[2], dr[2];
-  row2_headers(A, i0, lw, dr);
-  const float4 dd = *reinterpret_cast<const float4*>(A.cdiag2 + i0);
+  row2_headers<NT>(A, i0, lw, dr);
+  const float4 dd = ldv<NT, float4>(A.cdiag2 + i0);
   const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
-#if CFD_SCHUR_EARLY
-  const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
-#endif
+  const float2 dp = ldv<NT, float2>(dinv_p + i0);
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
-    predict2_group<D16, U1, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
+    predict2_group<D16, U1, true, NT>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
   else
-    predict2_group<D16, U1>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
+    predict2_group<D16, U1, false, NT>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
-    predict2_group<D16, U>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, lw, dr, d2, rhs);
-#if !CFD_SCHUR_EARLY
-  const float2 dp = *reinterpret_cast<const float2*>(dinv_p + i0);
-#endif
+    predict2_group<D16, U, false, NT>(A, w_in, sc, dinv_uv, i0, r0, maxlen - 1u, lw, dr, d2, rhs);
   *reinterpret_cast<float2*>(temp_p + i0) = make_float2(rhs[0], rhs[1]);
   *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
   if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
@@ -1766,7 +1472,6 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   uint32_t i0;
   if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
-#if CFD_SCHUR_EARLY
   // the row pair's own operands issued with the header (no round trip after the slots)
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;
@@ -1774,7 +1479,6 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   const f2u wc = ld2u(wb + 4);
   const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
   const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
-#endif
   const uint32_t lw[2] = {lg.x, lg.y};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float cu[2] = {0.0f, 0.0f}, cv[2] = {0.0f, 0.0f};
@@ -1783,14 +1487,6 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   else
     correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
   for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
-#if !CFD_SCHUR_EARLY
-  const float sc = binv[jv];
-  const float* wb = w_in + 3 * (size_t)i0;
-  const f4u wa = ld4u(wb);
-  const f2u wc = ld2u(wb + 4);
-  const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
-  const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
-#endif
   const float wo[6] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y};
   const float dk[2] = {du.x, du.y}, pk[2] = {ps.x, ps.y};
   float o[6];
@@ -1830,19 +1526,8 @@ __global__ void __launch_bounds__(256) k_solve_triangular(const float* H, const 
   if (threadIdx.x < (unsigned)k) y[threadIdx.x] = ys[threadIdx.x];
 }
 
-// the preconditioned vectors Z_i are read once per restart cycle here (nontemporal, CFD_UPDX_NT)
-#ifndef CFD_UPDX_NT
-#define CFD_UPDX_NT 1
-#endif
-__device__ __forceinline__ float4 ld4_upd(const float* p) {
-#if CFD_UPDX_NT
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-#else
-  return *reinterpret_cast<const float4*>(p);
-#endif
-}
+// the preconditioned vectors Z_i are read once per restart cycle here (nontemporal)
+__device__ __forceinline__ float4 ld4_upd(const float* p) { return ldv<true, float4>(p); }
 template <bool SER>
 __device__ __forceinline__ void upd_wait() {
   if constexpr (SER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1897,24 +1582,23 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
 // Each thread owns 4 consecutive rows: b, x, de and every ELL slot are one
 // 16-byte load per thread (coalesced 1 KiB per wavefront), column deltas are
 // 8 bytes per slot, lengths 4 bytes; only the x gathers are scalar.
-template <bool D16>
+template <bool D16, bool NT = false>
 __device__ __forceinline__ void load_cols4(const AmgLevelDev& L, size_t off, uint32_t i0,
                                            int c[4]) {
   if constexpr (D16) {
-    const short4 d = *reinterpret_cast<const short4*>(L.col16 + off);
+    const short4 d = ldv<NT, short4>(L.col16 + off);
     c[0] = (int)i0 + (int)d.x;
     c[1] = (int)i0 + 1 + (int)d.y;
     c[2] = (int)i0 + 2 + (int)d.z;
     c[3] = (int)i0 + 3 + (int)d.w;
   } else {
-    const int4 q = *reinterpret_cast<const int4*>(L.col32 + off);
+    const int4 q = ldv<NT, int4>(L.col32 + off);
     c[0] = q.x;
     c[1] = q.y;
     c[2] = q.z;
     c[3] = q.w;
   }
 }
-
 
 // Slots are processed in groups of kU with every load of the group issued
 // before the first use (val/col, then the x gathers): ~kU x more memory-level
@@ -1945,7 +1629,7 @@ __device__ __forceinline__ float prolonged(float xf, float xcv) { return xf + (0
 // PRO: every gathered x value is the prolonged one (k_amg_smooth<..., true>):
 // agg is gathered with the same columns as x (a 16-byte load where x is), then
 // the coarse values -- one more dependent round trip instead of a launch.
-template <bool D16, int MODE, bool ALWAYS = false, bool PRO = false>
+template <bool D16, int MODE, bool ALWAYS = false, bool PRO = false, bool NT = false>
 __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* __restrict__ x,
                                              uint32_t i0, uint32_t r0, uint32_t rmax, const uchar4 ln,
                                              float4 v[kU], float xg[kU][4],
@@ -1955,8 +1639,8 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
   for (int u = 0; u < kU; ++u) {
     if (MODE != 0 || r0 + u <= rmax) {
       const size_t off = (size_t)min(r0 + u, rmax) * L.stride + i0;
-      v[u] = *reinterpret_cast<const float4*>(L.val + off);
-      load_cols4<D16>(L, off, i0, c[u]);
+      v[u] = ldv<NT, float4>(L.val + off);
+      load_cols4<D16, NT>(L, off, i0, c[u]);
     } else {
       v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
@@ -1964,7 +1648,7 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
     }
   }
   [[maybe_unused]] int ag[kU][4];
-  if constexpr (ALWAYS && MODE == 1 && CFD_VGATHER) {
+  if constexpr (ALWAYS && MODE == 1) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const f4u q = ld4u(x + c[u][0]);
@@ -2012,68 +1696,27 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
   }
 }
 
-// Occupancy floor of the level row kernels (waves per SIMD; 0: the compiler's
-// choice -- 78 / 86 VGPRs, 6 / 5 waves for the smoother / residual)
-// Operands that do not depend on the members' residuals issued first: the
-// fused residual + restriction's member ranges and coarse diagonal, the
-// restriction's coarse diagonal (1); or where they are used (0).  Same-box
-// A/B (profiles/r03/ab_early_operands_c*.txt): C2 restriction 34.6 -> 32.2 us
-// (level 0), C1 fused residual + restriction -0.6 ... -0.8 us per level.
-#ifndef CFD_AMG_PRE2
-#define CFD_AMG_PRE2 1
-#endif
-// The fused post-smoother's own prolongation term (agg -> x_c) issued before
-// the slots (1) or after them (0): 1 was slower on every C1 level (+0.1 ... +0.5 us)
-#ifndef CFD_AMG_PRO_EARLY
-#define CFD_AMG_PRO_EARLY 0
-#endif
-// Row operands (b, x, diagonal) of the smoother / residual loaded at the top
-// (1) or after the slot loop (0)
-#ifndef CFD_AMG_EARLY
-#define CFD_AMG_EARLY 0
-#endif
-#ifndef CFD_AMG_WAVES
-#define CFD_AMG_WAVES 0
-#endif
-#if CFD_AMG_WAVES > 0
-#define CFD_AMG_OCC __attribute__((amdgpu_waves_per_eu(CFD_AMG_WAVES)))
-#else
-#define CFD_AMG_OCC
-#endif
-
 // smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8).
 // PRO (post-smoother of a single-GPU / replicated level): the prolongation
 // from the coarse level xc that precedes it (k_amg_prolong) is applied to
 // every x value as it is read, so x' = x + P xc is never stored -- the same
 // f32 operations per value, one launch and one pass over x / agg fewer.
 // smooth4: the 4 rows i0..i0+3
-template <bool D16, int MODE, bool PRO = false>
+// The row operands (b, x, diagonal) are loaded after the slot loop (loading
+// them with the row lengths was inside the noise, round 3); in the fused
+// post-smoother the row's own prolongation term (agg -> x_c) comes after the
+// slots as well (before them: +0.1 ... +0.5 us on every C1 level).
+template <bool D16, int MODE, bool PRO = false, bool NT = false>
 __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __restrict__ x,
                                           const float* __restrict__ b, uint32_t i0,
                                           const float* __restrict__ xc = nullptr) {
-  const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
-  [[maybe_unused]] float pc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if constexpr (PRO && CFD_AMG_PRO_EARLY) {
-    // the row's own prolongation term, as k_amg_prolong (padding rows get + 0),
-    // issued before the slots: its agg -> x_c round trips overlap them
-    const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
-    pc[0] += 1.0f * xc[ag.x];
-    if (i0 + 1 < L.n) pc[1] += 1.0f * xc[ag.y];
-    if (i0 + 2 < L.n) pc[2] += 1.0f * xc[ag.z];
-    if (i0 + 3 < L.n) pc[3] += 1.0f * xc[ag.w];
-  }
-#if CFD_AMG_EARLY
-  // the row's own operands issued with the row lengths (no round trip after the slots)
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-  float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
-#endif
+  const uchar4 ln = ldv<NT, uchar4>(L.len + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16, MODE, true, PRO>(L, x, i0, r0, rmax, ln, v, xg, xc);
+    gather_group<D16, MODE, true, PRO, NT>(L, x, i0, r0, rmax, ln, v, xg, xc);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -2087,19 +1730,16 @@ __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __r
   } else {
     for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
   }
-#if !CFD_AMG_EARLY
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
+  const float4 bb = ldv<NT, float4>(b + i0);
   float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dd = *reinterpret_cast<const float4*>(L.de + i0);
-#endif
+  const float4 dd = ldv<NT, float4>(L.de + i0);
   if constexpr (PRO) {  // the row's own value, as k_amg_prolong (padding rows get + 0)
-    if constexpr (!CFD_AMG_PRO_EARLY) {
-      const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
-      pc[0] += 1.0f * xc[ag.x];
-      if (i0 + 1 < L.n) pc[1] += 1.0f * xc[ag.y];
-      if (i0 + 2 < L.n) pc[2] += 1.0f * xc[ag.z];
-      if (i0 + 3 < L.n) pc[3] += 1.0f * xc[ag.w];
-    }
+    float pc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
+    pc[0] += 1.0f * xc[ag.x];
+    if (i0 + 1 < L.n) pc[1] += 1.0f * xc[ag.y];
+    if (i0 + 2 < L.n) pc[2] += 1.0f * xc[ag.z];
+    if (i0 + 3 < L.n) pc[3] += 1.0f * xc[ag.w];
     xx.x += pc[0];
     xx.y += pc[1];
     xx.z += pc[2];
@@ -2112,14 +1752,13 @@ __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __r
   o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
   return o;
 }
-template <bool D16, int MODE, bool PRO = false>
-__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
-                                                       const float* __restrict__ b,
-                                                       float* __restrict__ x_out,
-                                                       const float* __restrict__ xc = nullptr) {
+template <bool D16, int MODE, bool PRO = false, bool NT = false>
+__global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
+                                                       const float* __restrict__ b, float* __restrict__ x_out,
+                                                       const float* __restrict__ xc) {
   uint32_t i0;
-  if (!row_range<CFD_REV_SMOOTH>(L.r0, L.r1, L.r2, L.r3, i0)) return;
-  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO>(L, x, b, i0, xc);
+  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(L, x, b, i0, xc);
 }
 
 // smooth_op on a level whose x is identically +0 (every coarse level's
@@ -2140,27 +1779,21 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
   *reinterpret_cast<float4*>(x_out + i0) = o;
 }
 
-#ifndef CFD_RESID_GATHER_ALWAYS
-#define CFD_RESID_GATHER_ALWAYS 1
-#endif
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
-template <bool D16, int MODE>
+template <bool D16, int MODE, bool NT = false>
 __device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* __restrict__ x,
                                             const float* __restrict__ b, uint32_t i0) {
-  const uchar4 ln = *reinterpret_cast<const uchar4*>(L.len + i0);
-  const uchar4 dr = *reinterpret_cast<const uchar4*>(L.drank + i0);
+  const uchar4 ln = ldv<NT, uchar4>(L.len + i0);
+  const uchar4 dr = ldv<NT, uchar4>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dv = *reinterpret_cast<const float4*>(L.dv + i0);
-#if CFD_AMG_EARLY
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-#endif
+  const float4 dv = ldv<NT, float4>(L.dv + i0);
   const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
   float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   auto step = [&](uint32_t r0, uint32_t rmax) {
     float4 v[kU];
     float xg[kU][4];
-    gather_group<D16, MODE, CFD_RESID_GATHER_ALWAYS>(L, x, i0, r0, rmax, ln, v, xg);
+    gather_group<D16, MODE, true, false, NT>(L, x, i0, r0, rmax, ln, v, xg);
 #pragma unroll
     for (int u = 0; u < kU; ++u)
 #pragma unroll
@@ -2180,9 +1813,7 @@ __device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* _
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (u4(dr, k) >= r0) ax[k] += f4(dv, k) * f4(xx, k);
-#if !CFD_AMG_EARLY
-  const float4 bb = *reinterpret_cast<const float4*>(b + i0);
-#endif
+  const float4 bb = ldv<NT, float4>(b + i0);
   float4 o;
   o.x = bb.x - ax[0];
   o.y = bb.y - ax[1];
@@ -2190,13 +1821,12 @@ __device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* _
   o.w = bb.w - ax[3];
   return o;
 }
-template <bool D16, int MODE>
-__global__ void __launch_bounds__(kBlock) CFD_AMG_OCC k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
-                                                         const float* __restrict__ b,
-                                                         float* __restrict__ rr) {
+template <bool D16, int MODE, bool NT = false>
+__global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
+                                                         const float* __restrict__ b, float* __restrict__ rr) {
   uint32_t i0;
-  if (!row_range<CFD_REV_RESIDUAL>(L.r0, L.r1, L.r2, L.r3, i0)) return;
-  *reinterpret_cast<float4*>(rr + i0) = residual4<D16, MODE>(L, x, b, i0);
+  if (!row_range<kRevResidual>(L.r0, L.r1, L.r2, L.r3, i0)) return;
+  *reinterpret_cast<float4*>(rr + i0) = residual4<D16, MODE, NT>(L, x, b, i0);
 }
 
 // relax_pressure (schur_precond.wgsl:52-90) on large meshes, 4 rows per thread
@@ -2240,13 +1870,10 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const
   *reinterpret_cast<float4*>(dst + i0) = make_float4(y[0], y[1], y[2], y[3]);
 }
 
-#ifndef CFD_RESTRICT_M4
-#define CFD_RESTRICT_M4 1
-#endif
 // coarse value I of the restriction: sum_{f in R row I, ascending} 1.0 * r[f]
 __device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float* __restrict__ r, uint32_t I) {
   float sum = 0.0f;
-  if (CFD_RESTRICT_M4 && L.r_m4) {
+  if (L.r_m4) {
     // the first 4 members in one 16-byte load, then their values
     const int4 m = L.r_m4[I];
     const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
@@ -2292,11 +1919,11 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
   const uint32_t I = I0 + row_id();
   if (I < I1) {
     // the coarse diagonal loaded with the members (no round trip after the sum)
-    const float dec = (CFD_AMG_PRE2 && sm_out) ? sm_de[I] : 1.0f;
+    const float dec = sm_out ? sm_de[I] : 1.0f;
     const float sum = restrict_sum(L, r, I);
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
-      sm_out[I] = wmix(0.0f, (sum - 0.0f) / (CFD_AMG_PRE2 ? dec : sm_de[I]), 0.8f);
+      sm_out[I] = wmix(0.0f, (sum - 0.0f) / dec, 0.8f);
     else
       cx[I] = 0.0f;
     return;
@@ -2325,7 +1952,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
                                                             float* __restrict__ cx, float* __restrict__ sm_out,
                                                             const float* __restrict__ sm_de) {
   __shared__ float rl[kRRCap];
-  const uint32_t I0 = xcd_block<CFD_REV_RESIDUAL>() * L.rr_agg;
+  const uint32_t I0 = xcd_block<kRevResidual>() * L.rr_agg;
   if (I0 >= L.nc) return;
   const uint32_t I1 = min(I0 + L.rr_agg, L.nc);
   const uint32_t p0 = L.r_row[I0], p1 = L.r_row[I1];
@@ -2334,7 +1961,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
   // the residual phase (no dependent round trips after the barrier)
   [[maybe_unused]] uint32_t mk0 = 0, mk1 = 0;
   [[maybe_unused]] float dec = 1.0f;
-  if (CFD_AMG_PRE2 && I0 + threadIdx.x < I1) {
+  if (I0 + threadIdx.x < I1) {
     mk0 = L.r_row[I0 + threadIdx.x];
     mk1 = L.r_row[I0 + threadIdx.x + 1];
     if (sm_out) dec = sm_de[I0 + threadIdx.x];
@@ -2370,11 +1997,6 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
   const uint32_t t = threadIdx.x;
   if (I0 + t >= I1) return;
   const uint32_t I = I0 + t;
-  if (!CFD_AMG_PRE2) {
-    mk0 = L.r_row[I];
-    mk1 = L.r_row[I + 1];
-    if (sm_out) dec = sm_de[I];
-  }
   float sum = 0.0f;
   for (uint32_t k = mk0; k < mk1; ++k) sum += 1.0f * rl[k - p0];
   cb[I] = sum;
@@ -2566,31 +2188,8 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 // columns, dv/de, drank, P and R).  Each phase is then LDS reads + one
 // barrier instead of a global (L2) round trip per matrix slot.  Same row
 // arithmetic, in the same order, as smooth_row / residual_row.
-// Diagnostic build only (-DCFD_TAIL_STAMPS=K, tools/ab_variants.py; read by
-// tools/tail_stamps.py): thread 0 of the K-th launch records s_memtime after
-// every phase; the deltas (shader-clock cycles) land in g_tail_st[1..], their
-// count in g_tail_st[0], read back with cfd_debug_tail_stamps.
-#ifndef CFD_TAIL_STAMPS
-#define CFD_TAIL_STAMPS 0
-#endif
-#if CFD_TAIL_STAMPS
-__device__ unsigned g_tail_calls;
-__device__ uint32_t g_tail_st[64];
-#define TAIL_STAMP()                                                         \
-  do {                                                                       \
-    if (t == 0 && ns < 64) st[ns] = __builtin_amdgcn_s_memtime();            \
-    ++ns;                                                                    \
-  } while (0)
-#else
-#define TAIL_STAMP() \
-  do {               \
-  } while (0)
-#endif
-// Fused tail phases (1): the zero-x pre-smoother with the residual, the
-// prolongation with the post-smoother (two barriers fewer per level)
-#ifndef CFD_TAIL_FUSE
-#define CFD_TAIL_FUSE 1
-#endif
+// The zero-x pre-smoother is fused with the residual, and the prolongation
+// with the post-smoother (two barriers fewer per level, round 3).
 __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __restrict__ tail,
                                                         const TailBlobLevel* __restrict__ desc,
                                                         const uint32_t* __restrict__ blob, uint32_t blob_words,
@@ -2598,11 +2197,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
                                                         const float* __restrict__ b_first, uint32_t n_first) {
   extern __shared__ float sm[];
   const uint32_t t = threadIdx.x, nt = blockDim.x;
-#if CFD_TAIL_STAMPS
-  uint64_t st[64];
-  int ns = 0;
-#endif
-  TAIL_STAMP();
   uint32_t* bw = reinterpret_cast<uint32_t*>(sm + vec_floats);
   auto base = [&](int l) {
     uint32_t o = 0;
@@ -2646,7 +2240,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       if (t + k * NT < n) B0[t + k * NT] = bv[k];
   }
   __syncthreads();
-  TAIL_STAMP();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
   auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
   auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
@@ -2665,54 +2258,28 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     float* B = XT + nr;
     float* Rr = B + nr;
     const float* de = fw(D.de);
-    if (CFD_TAIL_FUSE) {
-      // zero-x pre-smoother and residual in one phase: a neighbour's smoothed
-      // value is recomputed from its b and diagonal (the same operations as
-      // the sweep), the row's own is stored for the up-sweep
-      const uint32_t* ro = bw + D.rowoff;
-      const float* val = fw(D.val);
-      const float* dv = fw(D.dv);
-      const uint16_t* col = hw(D.col);
-      const uint8_t* drank = reinterpret_cast<const uint8_t*>(bw + D.drank);
-      for (uint32_t i = t; i < D.n; i += nt) {
-        const float xti = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
-        XT[i] = xti;
-        const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
-        float ax = 0.0f;
-        for (uint32_t r = 0; r <= len; ++r) {
-          if (r == dr) ax += dv[i] * xti;
-          if (r == len) break;
-          const uint32_t j = col[e0 + r];
-          ax += val[e0 + r] * wmix(0.0f, (B[j] - 0.0f) / de[j], 0.8f);
-        }
-        Rr[i] = B[i] - ax;
+    // zero-x pre-smoother and residual in one phase: a neighbour's smoothed
+    // value is recomputed from its b and diagonal (the same operations as
+    // the sweep), the row's own is stored for the up-sweep
+    const uint32_t* ro = bw + D.rowoff;
+    const float* val = fw(D.val);
+    const float* dv = fw(D.dv);
+    const uint16_t* col = hw(D.col);
+    const uint8_t* drank = reinterpret_cast<const uint8_t*>(bw + D.drank);
+    for (uint32_t i = t; i < D.n; i += nt) {
+      const float xti = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
+      XT[i] = xti;
+      const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
+      float ax = 0.0f;
+      for (uint32_t r = 0; r <= len; ++r) {
+        if (r == dr) ax += dv[i] * xti;
+        if (r == len) break;
+        const uint32_t j = col[e0 + r];
+        ax += val[e0 + r] * wmix(0.0f, (B[j] - 0.0f) / de[j], 0.8f);
       }
-      __syncthreads();
-      TAIL_STAMP();
-    } else {
-    for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
-    __syncthreads();
-  TAIL_STAMP();
-    {
-      const uint32_t* ro = bw + D.rowoff;
-      const float* val = fw(D.val);
-      const float* dv = fw(D.dv);
-      const uint16_t* col = hw(D.col);
-      const uint8_t* drank = reinterpret_cast<const uint8_t*>(bw + D.drank);
-      for (uint32_t i = t; i < D.n; i += nt) {
-        const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
-        float ax = 0.0f;
-        for (uint32_t r = 0; r <= len; ++r) {
-          if (r == dr) ax += dv[i] * XT[i];
-          if (r == len) break;
-          ax += val[e0 + r] * XT[col[e0 + r]];
-        }
-        Rr[i] = B[i] - ax;
-      }
+      Rr[i] = B[i] - ax;
     }
     __syncthreads();
-  TAIL_STAMP();
-    }
     float* CB = base(l + 1) + 2 * r4(desc[l + 1].n);
     {
       const uint16_t* rrow = hw(D.r_row);
@@ -2724,7 +2291,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       }
     }
     __syncthreads();
-  TAIL_STAMP();
   }
   {
     const TailBlobLevel D = desc[nlev - 1];
@@ -2750,18 +2316,17 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
         X[i] = xp;   // sweep 9
       }
       __syncthreads();
-      TAIL_STAMP();
-    } else
-    for (int s = 0; s < 10; ++s) {
-      if (s == 0) {
-        for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
-      } else {
-        const float* xin = (s & 1) ? XT : X;
-        float* xout = (s & 1) ? X : XT;
-        for (uint32_t i = t; i < D.n; i += nt) xout[i] = smooth(D, xin, B, i);
+    } else {
+      for (int s = 0; s < 10; ++s) {
+        if (s == 0) {
+          for (uint32_t i = t; i < D.n; i += nt) XT[i] = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
+        } else {
+          const float* xin = (s & 1) ? XT : X;
+          float* xout = (s & 1) ? X : XT;
+          for (uint32_t i = t; i < D.n; i += nt) xout[i] = smooth(D, xin, B, i);
+        }
+        __syncthreads();
       }
-      __syncthreads();
-  TAIL_STAMP();
     }
   }
   for (int l = nlev - 2; l >= first; --l) {
@@ -2772,48 +2337,25 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     float* B = XT + nr;
     const float* XC = base(l + 1);
     const uint16_t* agg = hw(D.agg);
-    if (CFD_TAIL_FUSE) {
-      // prolongation and post-smoother in one phase: every value the sweep
-      // reads is prolonged as it is read (k_amg_smooth<..., PRO>'s rule)
-      const uint32_t* ro = bw + D.rowoff;
-      const float* val = fw(D.val);
-      const uint16_t* col = hw(D.col);
-      const float* de = fw(D.de);
-      for (uint32_t i = t; i < D.n; i += nt) {
-        float sigma = 0.0f;
-        for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) {
-          const uint32_t j = col[e];
-          sigma += val[e] * prolonged(XT[j], XC[agg[j]]);
-        }
-        X[i] = wmix(prolonged(XT[i], XC[agg[i]]), (B[i] - sigma) / de[i], 0.8f);
-      }
-      __syncthreads();
-      TAIL_STAMP();
-    } else {
+    // prolongation and post-smoother in one phase: every value the sweep
+    // reads is prolonged as it is read (k_amg_smooth<..., PRO>'s rule)
+    const uint32_t* ro = bw + D.rowoff;
+    const float* val = fw(D.val);
+    const uint16_t* col = hw(D.col);
+    const float* de = fw(D.de);
     for (uint32_t i = t; i < D.n; i += nt) {
-      float corr = 0.0f;
-      corr += 1.0f * XC[agg[i]];
-      XT[i] += corr;
+      float sigma = 0.0f;
+      for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) {
+        const uint32_t j = col[e];
+        sigma += val[e] * prolonged(XT[j], XC[agg[j]]);
+      }
+      X[i] = wmix(prolonged(XT[i], XC[agg[i]]), (B[i] - sigma) / de[i], 0.8f);
     }
     __syncthreads();
-  TAIL_STAMP();
-    for (uint32_t i = t; i < D.n; i += nt) X[i] = smooth(D, XT, B, i);
-    __syncthreads();
-  TAIL_STAMP();
-    }
   }
   const float* X0 = base(first);
   float* gx = tail[first].x;
   for (uint32_t i = t; i < desc[first].n; i += nt) gx[i] = X0[i];
-#if CFD_TAIL_STAMPS
-  if (t == 0) {
-    const unsigned c = atomicAdd(&g_tail_calls, 1u);
-    if (c == CFD_TAIL_STAMPS) {
-      g_tail_st[0] = (uint32_t)ns;
-      for (int q = 1; q < ns && q < 64; ++q) g_tail_st[q] = (uint32_t)(st[q] - st[q - 1]);
-    }
-  }
-#endif
 }
 
 // ---------------------- check_evolution statistics --------------------------
@@ -2976,22 +2518,12 @@ void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, floa
   hipLaunchKernelGGL(k_reduce_final, dim3(1), dim3(kRedFinalThreads), 0, s, r, mode, out, inv, g0, g_len,
                      host_out);
 }
-void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b) {
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b, bool nt) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
-  if (CFD_SPMV_ROWS == 2) {
-    const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
-    if (A.use16)
-      hipLaunchKernelGGL(k_spmv2<true>, dim3(nb2), dim3(kBlock), 0, s, A, x, y, b);
-    else
-      hipLaunchKernelGGL(k_spmv2<false>, dim3(nb2), dim3(kBlock), 0, s, A, x, y, b);
-    return;
-  }
-  if (b) throw std::invalid_argument("launch_spmv: the fused residual needs the 2-cell SpMV");
-  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
-  if (A.use16)
-    hipLaunchKernelGGL(k_spmv<true>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
-  else
-    hipLaunchKernelGGL(k_spmv<false>, dim3(nb), dim3(kBlock), 0, s, A, x, y);
+  const unsigned nb = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
+  auto fn = A.use16 ? (nt ? k_spmv2<true, true> : k_spmv2<true, false>)
+                    : (nt ? k_spmv2<false, true> : k_spmv2<false, false>);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, x, y, b);
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      uint32_t U, float* partial, uint32_t np, hipStream_t s) {
@@ -3023,25 +2555,12 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 }
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
-                            float* p_prev, hipStream_t s) {
+                            float* p_prev, hipStream_t s, bool nt) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
-  if (CFD_SCHUR_ROWS == 2) {
-    const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
-    if (A.use16)
-      hipLaunchKernelGGL(k_precond_predict2<true>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
-                         temp_p, p_sol, p_prev);
-    else
-      hipLaunchKernelGGL(k_precond_predict2<false>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv,
-                         dinv_p, temp_p, p_sol, p_prev);
-    return;
-  }
-  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
-  if (A.use16)
-    hipLaunchKernelGGL(k_precond_predict<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
-                       temp_p, p_sol, p_prev);
-  else
-    hipLaunchKernelGGL(k_precond_predict<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p,
-                       temp_p, p_sol, p_prev);
+  const unsigned nb = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
+  auto fn = A.use16 ? (nt ? k_precond_predict2<true, true> : k_precond_predict2<true, false>)
+                    : (nt ? k_precond_predict2<false, true> : k_precond_predict2<false, false>);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p, temp_p, p_sol, p_prev);
 }
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len, const float* sval,
                            const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
@@ -3082,20 +2601,11 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
-  if (CFD_SCHUR_ROWS == 2) {
-    const unsigned nb2 = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
-    if (A.use16)
-      hipLaunchKernelGGL(k_precond_correct2<true>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
-    else
-      hipLaunchKernelGGL(k_precond_correct2<false>, dim3(nb2), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv,
-                         z);
-    return;
-  }
-  const unsigned nb = rows2_grid(A.r0, A.r1, A.r2, A.r3);
+  const unsigned nb = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
   if (A.use16)
-    hipLaunchKernelGGL(k_precond_correct<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+    hipLaunchKernelGGL(k_precond_correct2<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
   else
-    hipLaunchKernelGGL(k_precond_correct<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+    hipLaunchKernelGGL(k_precond_correct2<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
 }
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
   if (k > 64 || m1 > 64) throw std::invalid_argument("solve_triangular: basis larger than 64");
@@ -3109,15 +2619,16 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
   else
     hipLaunchKernelGGL(k_update_x<false>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
 }
-// instance for a level: 16/32-bit columns x load mode (see gather_group)
-#define CFD_AMG_INSTANCE(kern, L) \
-  ((L).use16 ? ((L).full ? kern<true, 1> : kern<true, 0>) : ((L).full ? kern<false, 1> : kern<false, 0>))
+// instance for a level: 16/32-bit columns x load mode (see gather_group) x load policy
+#define CFD_AMG_INSTANCE(kern, L, ...)                                                  \
+  ((L).use16 ? ((L).full ? kern<true, 1, __VA_ARGS__> : kern<true, 0, __VA_ARGS__>) \
+             : ((L).full ? kern<false, 1, __VA_ARGS__> : kern<false, 0, __VA_ARGS__>))
 
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out, hipStream_t s,
-                       hipEvent_t ev0, hipEvent_t ev1) {
+                       hipEvent_t ev0, hipEvent_t ev1, bool nt) {
   if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
-  auto fn = CFD_AMG_INSTANCE(k_amg_smooth, L);
+  auto fn = nt ? CFD_AMG_INSTANCE(k_amg_smooth, L, false, true) : CFD_AMG_INSTANCE(k_amg_smooth, L, false, false);
   if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
     hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out, nullptr);
   else
@@ -3135,10 +2646,10 @@ void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
 }
-void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s) {
+void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s, bool nt) {
   if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
-  auto fn = CFD_AMG_INSTANCE(k_amg_residual, L);
+  auto fn = nt ? CFD_AMG_INSTANCE(k_amg_residual, L, true) : CFD_AMG_INSTANCE(k_amg_residual, L, false);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
@@ -3256,9 +2767,3 @@ void build_r_m4(const std::vector<uint32_t>& r_row, const std::vector<uint32_t>&
 
 }  // namespace cfd2
 
-#if CFD_TAIL_STAMPS
-extern "C" int cfd_debug_tail_stamps(uint32_t* out, int n) {
-  if (n > 64) n = 64;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd2::g_tail_st), n * sizeof(uint32_t)) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -289,7 +289,9 @@ void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, 
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, int g_len, float* host_out,
                          hipStream_t s);
 // b != null: y = b - A x with the residual axpby's operations (1 * b + -1 * (A x))
-void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b = nullptr);
+// nt: the matrix and b are read with the nontemporal policy (kernels.hip ldx)
+void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s, const float* b = nullptr,
+                 bool nt = false);
 // basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
@@ -306,7 +308,7 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 // r_in = binv[j] * W_j
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
-                            float* p_prev, hipStream_t s);
+                            float* p_prev, hipStream_t s, bool nt = false);
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
@@ -329,8 +331,9 @@ void launch_solve_triangular(const float* H, const float* g, float* y, int k, in
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
                      hipStream_t s);
 // ev0/ev1 (optional): timing events recorded by the GPU at kernel start / end
+// nt: the level matrix, b and the diagonal read with the nontemporal policy
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
-                       hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                       hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool nt = false);
 // post-smoother with the prolongation fused: x_out = smooth(x + P xc), bit-identical
 // to launch_amg_prolong(L, x, xc) then launch_amg_smooth(L, x, b, x_out), but x is
 // only read (single-GPU / replicated levels: every column an owned row)
@@ -339,7 +342,7 @@ void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float
 // pre-smoother of a level whose x is identically +0 (bit-identical to launch_amg_smooth then)
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,
-                         hipStream_t s);
+                         hipStream_t s, bool nt = false);
 // coarse_b = R r and coarse_x = 0 (the reference's separate `clear` pass fused); on a
 // distributed coarse level also clears its ghosts: [-glo, 0) and [stride_c, stride_c + ghi)
 // sm_out != null: instead of clearing coarse_x, write the coarse level's

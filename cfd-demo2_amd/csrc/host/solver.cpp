@@ -87,6 +87,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
+  if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -1180,16 +1181,16 @@ void Solver::prof_grow(size_t n) {
   }
 }
 
-void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero) {
+void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bool nt) {
   AmgGpuLevel& L = levels[li];
   if (x_zero) {
     launch_amg_smooth_zero(L.dev, b, L.xt, stream);
   } else if (li == 0 && prof_take()) {
     const auto ev = prof_pair();
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second);
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second, nt);
     prof_launches++;
   } else {
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream);
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, nullptr, nullptr, nt);
   }
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
@@ -1209,10 +1210,12 @@ void Solver::v_cycle() {
   const int tf = (prof && L == 1) ? L : std::max({tail_first, 1, D});
   const int down = std::min(tf, L - 1);
   // smoother sweep; on a distributed level the x halo overlaps the interior rows
-  auto sm = [&](int i, bool x_zero) {
+  // post: the up-sweep's smoother (nontemporal matrix loads with nt_mask bit 1)
+  auto sm = [&](int i, bool x_zero, bool post = false) {
     AmgGpuLevel& Lv = levels[i];
+    const bool ntl = nt(post ? 1u : 16u);
     if (!Lv.dist || x_zero) {
-      amg_smooth(i, Lv.x, Lv.b, x_zero);
+      amg_smooth(i, Lv.x, Lv.b, x_zero, ntl);
       return;
     }
     const bool timed = i == 0 && prof_take();  // kernel time only: each part timed separately
@@ -1224,9 +1227,9 @@ void Solver::v_cycle() {
       d.r3 = b2;
       if (timed) {
         const auto ev = prof_pair();
-        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second);
+        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second, ntl);
       } else {
-        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream);
+        launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, nullptr, nullptr, ntl);
       }
     });
     if (timed) prof_launches++;
@@ -1240,7 +1243,7 @@ void Solver::v_cycle() {
       d.r1 = b;
       d.r2 = a2;
       d.r3 = b2;
-      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream);
+      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream, nt(2));
     };
     if (Lv.dist)
       overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, f);
@@ -1315,7 +1318,7 @@ void Solver::v_cycle() {
     } else {
       launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream);
     }
-    sm(ii, false);
+    sm(ii, false, true);
   }
   // every level performs an even number of sweeps, so level 0 ends in p_sol
   if (levels[0].x != p_sol) throw std::logic_error("AMG level-0 ping-pong parity");
@@ -1333,7 +1336,7 @@ void Solver::precondition(int j, float* z) {
     Ar.r1 = b;
     Ar.r2 = a2;
     Ar.r3 = b2;
-    launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream);
+    launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream, nt(4));
   });
   bool in_sol = true;
   if (!jacobi) {
@@ -1414,7 +1417,7 @@ void Solver::residual_into_v0_launch() {
     A.r1 = b;
     A.r2 = a2;
     A.r3 = b2;
-    launch_spmv(A, x, basis, stream, rhs);  // V0 = 1 * b + -1 * (A x) as the SpMV stores it
+    launch_spmv(A, x, basis, stream, rhs, nt(8));  // V0 = 1 * b + -1 * (A x) as the SpMV stores it
   });
   norm_launch(basis, 2, 1);
 }
@@ -1481,7 +1484,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         A.r1 = b;
         A.r2 = a2;
         A.r3 = b2;
-        launch_spmv(A, zj, w, stream);
+        launch_spmv(A, zj, w, stream, nullptr, nt(8));
       });
       launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);

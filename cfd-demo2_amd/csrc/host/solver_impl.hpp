@@ -312,6 +312,12 @@ struct Solver {
   bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
   bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
+  // nontemporal loads of the matrix streams (kernels.hip ldx), per kernel, for
+  // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
+  // 1 post-smoother of the split levels, 2 AMG residual, 4 Schur prediction,
+  // 8 SpMV, 16 pre-smoother.  Same bits either way.
+  unsigned nt_mask = 0;
+  bool nt(unsigned bit) const { return (nt_mask & bit) != 0; }
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {
@@ -431,7 +437,7 @@ struct Solver {
   void set_amg_full_policy(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
   void v_cycle();
-  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false);
+  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false);
   std::pair<hipEvent_t, hipEvent_t> prof_pair();
  public:
   static constexpr size_t kProfPoolMax = 1u << 15;
