@@ -252,6 +252,37 @@ def reference_workloads(max_seconds=60.0, only=None):
     return out
 
 
+def comm_timing_summary(t):
+    """Per-FGMRES-iteration communication times of the extra timed step
+    (cfd_comm_timing), by category: max and mean over ranks of the compute
+    stream's exposed wait and of the transport's own time, in us; AMG halos
+    per level.  `exposed_us_per_iteration` (max over ranks of the summed
+    waits) against `iteration_us` (the step time with timing on / its
+    iterations) gives the predicted parallel efficiency 1 - exposed / iteration
+    (DESIGN.md section 7.1)."""
+    its = t["iterations"]
+    cats = {}
+    for r, entries in enumerate(t["ranks"]):
+        for e in entries:
+            key = e["category"] + (f"_l{e['level']}" if e["level"] >= 0 else "")
+            c = cats.setdefault(key, {"calls": [], "wait_us": [], "comm_us": [], "bytes": []})
+            c["calls"].append(e["calls"] / its)
+            c["wait_us"].append(e["wait_us"] / its)
+            c["comm_us"].append(e["comm_us"] / its)
+            c["bytes"].append(e["bytes"] / its)
+    out = {}
+    for k, c in sorted(cats.items()):
+        out[k] = {"calls": max(c["calls"]), "bytes": max(c["bytes"]),
+                  "wait_us_max": max(c["wait_us"]), "wait_us_mean": sum(c["wait_us"]) / len(c["wait_us"]),
+                  "comm_us_max": max(c["comm_us"]), "comm_us_mean": sum(c["comm_us"]) / len(c["comm_us"])}
+    exposed = max(sum(e["wait_us"] for e in entries) / its for entries in t["ranks"]) if t["ranks"] else 0.0
+    it_us = 1e3 * t["step_ms_with_timing"] / its
+    return {"per_iteration": out, "exposed_us_per_iteration": exposed, "iteration_us": it_us,
+            "predicted_efficiency": 1.0 - exposed / it_us if it_us > 0 else None,
+            "note": "one extra step after the timed ones, halos / all-gathers bracketed by timing events; "
+                    "wait = compute-stream stall, comm = transport time (RCCL: includes peer skew)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -355,7 +386,8 @@ def main():
     else:
         mesh = make_mesh()
     n_global = mesh.num_cells()
-    log(f"[rank {rank}] mesh {n_global} cells / {mesh.num_faces()} faces in {time.perf_counter() - t0:.1f}s")
+    setup_s = {"mesh": time.perf_counter() - t0}
+    log(f"[rank {rank}] mesh {n_global} cells / {mesh.num_faces()} faces in {setup_s['mesh']:.1f}s")
 
     cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner, amg_rebuild_interval=args.amg_rebuild)
     t0 = time.perf_counter()
@@ -390,7 +422,8 @@ def main():
         import gc
         gc.collect()
         mesh = None
-    log(f"[rank {rank}] solver created in {time.perf_counter() - t0:.1f}s (owns {n_cells} cells)")
+    setup_s["create"] = time.perf_counter() - t0
+    log(f"[rank {rank}] solver created in {setup_s['create']:.1f}s (owns {n_cells} cells)")
 
     def barrier_sync():
         # device fence (the torch.cuda.synchronize() of the contract: the
@@ -403,6 +436,7 @@ def main():
     for k in range(args.warmup):
         t0 = time.perf_counter()
         solver.step()
+        setup_s.setdefault("first_step", time.perf_counter() - t0)  # t = 0 step: includes the AMG setup
         log(f"[rank {rank}] warmup step {k}: {time.perf_counter() - t0:.3f}s")
     barrier_sync()
     solver.profile_enable(True)
@@ -433,7 +467,29 @@ def main():
         dist.all_gather_object(allc, comm[0])
         comm = allc
     comm_line = None
+    timing = None
     if len(comm) > 1:
+        # one more step, outside the timed region, with every halo / all-gather
+        # bracketed by timing events: exposed (compute-stream) wait and transport
+        # time per category, per FGMRES iteration, on every rank
+        for hnd in handles:
+            hnd.comm_timing_enable(True)
+        t1 = time.perf_counter()
+        solver.step()
+        solver.synchronize()
+        timed_step_ms = 1e3 * (time.perf_counter() - t1)
+        its = max(1, int(solver.step_info().total_linear_iterations))
+        mine = [hnd.comm_timing() for hnd in handles]
+        for hnd in handles:
+            hnd.comm_timing_enable(False)
+        if dist is not None:
+            allt = [None] * world
+            dist.all_gather_object(allt, mine[0])
+            mine = allt
+            ts = [None] * world
+            dist.all_gather_object(ts, timed_step_ms)
+            timed_step_ms = max(ts)
+        timing = {"iterations": its, "step_ms_with_timing": timed_step_ms, "ranks": mine}
         iters = max(1, args.steps * int(info.total_linear_iterations))
         comm_line = {
             "transport": comm[0]["transport"],
@@ -447,6 +503,8 @@ def main():
             "halo_bytes_per_iteration": max(c["bytes_sent"] for c in comm) / iters,
             "allgather_bytes_per_iteration": max(c["bytes_gathered"] for c in comm) / iters,
         }
+        comm_line["timing"] = comm_timing_summary(timing)
+        comm_line["setup_s_rank0"] = setup_s
 
     ms_per_step = 1e3 * elapsed / args.steps
     inproc = args.inproc_ranks > 1
@@ -543,8 +601,8 @@ def main():
         # measured traffic), so count / step time is not an HBM rate
         "step_reference_format_bytes": step_bytes,
         # layout-true bytes of one step (this rank): each kernel's minimum
-        # traffic in this library's layouts x its launches; a lower bound of
-        # the step's HBM traffic, so its rate is a lower bound of the achieved one
+        # traffic at kernel level in this library's layouts x its launches (not
+        # a bound on HBM traffic: some lines come from the Infinity Cache)
         "step_layout_bytes": {
             "bytes_per_step": step_layout,
             "gbs": step_layout / (ms_per_step / 1e3) / 1e9,

@@ -99,6 +99,21 @@ class StepInfo(C.Structure):
     ]
 
 
+class CommTimingEntry(C.Structure):  # cfd_comm_timing_entry
+    _fields_ = [
+        ("category", C.c_int32),
+        ("level", C.c_int32),
+        ("calls", C.c_uint64),
+        ("bytes", C.c_uint64),
+        ("wait_us", C.c_double),
+        ("comm_us", C.c_double),
+    ]
+
+
+COMM_CATEGORIES = {0: "krylov_halo", 1: "state_halo", 2: "reduction_allgather", 3: "replicated_level_allgather",
+                   4: "amg_halo"}
+
+
 class CommStats(C.Structure):  # cfd_comm_stats
     _fields_ = [
         ("transport", C.c_int32),
@@ -172,7 +187,8 @@ EXPORTED = [
     "cfd_dist_unique_id", "cfd_solver_create_dist", "cfd_solver_create_dist_host", "cfd_group_create",
     "cfd_group_step",
     "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest", "cfd_dist_comm_stats",
-    "cfd_debug_group_fault",
+    "cfd_debug_group_fault", "cfd_debug_group_fault_midstep", "cfd_group_reset", "cfd_group_needs_restore",
+    "cfd_comm_timing_enable", "cfd_comm_timing",
 ]
 
 _lib = None

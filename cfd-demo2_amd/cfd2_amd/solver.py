@@ -86,6 +86,12 @@ def _bind():
     L.cfd_group_state_save.argtypes = [C.POINTER(_vp), C.c_int32, C.c_char_p]
     L.cfd_dist_comm_stats.argtypes = [_vp, C.POINTER(_ffi.CommStats), C.c_int32]
     L.cfd_debug_group_fault.argtypes = [C.POINTER(_vp), C.c_int32, C.c_int32]
+    L.cfd_debug_group_fault_midstep.argtypes = [C.POINTER(_vp), C.c_int32, C.c_int32]
+    L.cfd_group_reset.argtypes = [C.POINTER(_vp), C.c_int32]
+    L.cfd_group_needs_restore.argtypes = [C.POINTER(_vp), C.c_int32]
+    L.cfd_group_needs_restore.restype = C.c_int32
+    L.cfd_comm_timing_enable.argtypes = [_vp, C.c_int32]
+    L.cfd_comm_timing.argtypes = [_vp, C.POINTER(_ffi.CommTimingEntry), C.c_int32, C.POINTER(C.c_int32)]
     _bound = True
     return L
 
@@ -337,6 +343,23 @@ class GpuSolver:
         d["transport"] = _ffi.TRANSPORTS.get(c.transport, str(c.transport))
         return d
 
+    def comm_timing_enable(self, enable=True) -> None:
+        """cfd_comm_timing_enable: time every halo / all-gather (resets the totals)."""
+        self._call("cfd_comm_timing_enable", 1 if enable else 0)
+
+    def comm_timing(self) -> list:
+        """cfd_comm_timing: per category (AMG halos per level) the calls, bytes,
+        the compute stream's exposed wait and the transport's own time (us)."""
+        cap = 64
+        buf = (_ffi.CommTimingEntry * cap)()
+        n = C.c_int32(0)
+        self._call("cfd_comm_timing", buf, cap, C.byref(n))
+        out = []
+        for e in buf[:n.value]:
+            out.append({"category": _ffi.COMM_CATEGORIES.get(e.category, str(e.category)), "level": e.level,
+                        "calls": e.calls, "bytes": e.bytes, "wait_us": e.wait_us, "comm_us": e.comm_us})
+        return out
+
 
 def dist_unique_id() -> bytes:
     """RCCL unique id (rank 0 creates it, every rank passes it to create_dist)."""
@@ -406,6 +429,21 @@ class GpuGroup:
         """cfd_debug_group_fault: raises (the injected failure of ``fail_rank``)."""
         _ffi.check(_bind().cfd_debug_group_fault(self._harr, self.nranks, int(fail_rank)),
                    "cfd_debug_group_fault")
+
+    def debug_fault_midstep(self, fail_rank: int) -> None:
+        """cfd_debug_group_fault_midstep: a group step in which ``fail_rank``
+        fails right after its first prepare(); raises, and the group is then
+        marked needs-restore."""
+        _ffi.check(_bind().cfd_debug_group_fault_midstep(self._harr, self.nranks, int(fail_rank)),
+                   "cfd_debug_group_fault_midstep")
+
+    @property
+    def needs_restore(self) -> bool:
+        return bool(_bind().cfd_group_needs_restore(self._harr, self.nranks))
+
+    def reset(self) -> None:
+        """cfd_group_reset: accept the ranks' current state after a failed step."""
+        _ffi.check(_bind().cfd_group_reset(self._harr, self.nranks), "cfd_group_reset")
 
     def save_state(self, path):
         _ffi.check(_bind().cfd_group_state_save(self._harr, self.nranks, os.fsencode(path)),

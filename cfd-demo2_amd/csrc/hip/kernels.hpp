@@ -275,8 +275,9 @@ struct TailBlobLevel {
 };
 
 // ---------------- launch wrappers (kernels.hip) ----------------
-void launch_prepare(const PrepareArgs& a, hipStream_t s);
-void launch_assemble(const AssembleArgs& a, hipStream_t s);
+// nt: the static face-slot geometry read with the nontemporal policy
+void launch_prepare(const PrepareArgs& a, hipStream_t s, bool nt = false);
+void launch_assemble(const AssembleArgs& a, hipStream_t s, bool nt = false);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 // (and to host_out[0..1], a device view of pinned host memory, when non-null)
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
@@ -325,7 +326,7 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
                                  const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
                                  float* temp, uint32_t iters, hipStream_t s);
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
-                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s);
+                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s, bool nt = false);
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,
                              hipStream_t s);
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,

@@ -3,6 +3,7 @@
 // exceptions become status codes (the reference panics).
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -184,7 +185,10 @@ cfd_status cfd_state_save(cfd_solver* s, const char* path) {
 cfd_status cfd_state_load(cfd_solver* s, const char* path) {
   CHECK_S(s);
   if (!path) return set_error(CFD_ERR_INVALID, "null path");
-  return guard([&] { s->s->load_state(path); });
+  return guard([&] {
+    s->s->load_state(path);
+    s->s->needs_restore = false;  // a consistent state on this rank again
+  });
 }
 uint32_t cfd_num_cells(const cfd_solver* s) { return (s && s->s) ? s->s->N : 0; }
 uint32_t cfd_num_faces(const cfd_solver* s) { return (s && s->s) ? s->s->F : 0; }
@@ -316,16 +320,20 @@ cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, in
   auto group = std::make_shared<cfd2::LocalGroup>(nranks);
   std::vector<cfd2::Solver*> made;
   const cfd_status st = guard([&] {
-    // ranks on distinct devices copy from each other's memory (LocalComm):
-    // enable peer access both ways once per device pair
+    // ranks on distinct devices copy from each other's memory (LocalComm,
+    // hipMemcpyPeerAsync): enable peer access both ways once per device pair
+    // where the devices support it; elsewhere the runtime stages the copies
+    // through host memory (slower, still correct)
     for (int a = 0; a < nranks; ++a)
       for (int b = 0; b < nranks; ++b) {
         if (devices[a] == devices[b]) continue;
         int can = 0;
         CFD_HIP(hipDeviceCanAccessPeer(&can, devices[a], devices[b]));
-        if (!can)
-          throw std::invalid_argument("device " + std::to_string(devices[a]) + " cannot access device " +
-                                      std::to_string(devices[b]) + " (peer access)");
+        if (!can) {
+          std::fprintf(stderr, "cfd_group_create: device %d cannot access device %d; peer copies are staged\n",
+                       devices[a], devices[b]);
+          continue;
+        }
         CFD_HIP(hipSetDevice(devices[a]));
         const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
         if (e == hipErrorPeerAccessAlreadyEnabled)
@@ -349,11 +357,21 @@ cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, in
 }  // extern "C"
 
 namespace {
-// a collective call on every rank of an in-process group, one host thread each
+// a collective call on every rank of an in-process group, one host thread each.
+// mutates: the call advances the solver state (a step).  If it fails on any
+// rank, the ranks may have stopped at different points of it, so every rank is
+// marked needs_restore and later mutating calls are refused until each rank is
+// restored (cfd_state_load) or the group is explicitly reset (cfd_group_reset).
 template <class F>
-cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
+cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f, bool mutates = false) {
   if (!h || n < 1) return set_error(CFD_ERR_INVALID, "bad argument");
   for (int r = 0; r < n; ++r) CHECK_S(h[r]);
+  if (mutates)
+    for (int r = 0; r < n; ++r)
+      if (h[r]->s->needs_restore)
+        return set_error(CFD_ERR_INVALID, "rank " + std::to_string(r) +
+                                              ": group needs restore after a failed step (cfd_state_load on "
+                                              "every rank, or cfd_group_reset)");
   std::vector<cfd_status> st(n, CFD_OK);
   std::vector<std::string> msg(n);
   std::vector<std::thread> th;
@@ -374,7 +392,11 @@ cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
   int first = -1;
   for (int r = 0; r < n; ++r)
     if (st[r] != CFD_OK && (first < 0 || msg[first].find("group aborted") != std::string::npos)) first = r;
-  if (first >= 0) return set_error(st[first], "rank " + std::to_string(first) + ": " + msg[first]);
+  if (first >= 0) {
+    if (mutates)
+      for (int r = 0; r < n; ++r) h[r]->s->needs_restore = true;
+    return set_error(st[first], "rank " + std::to_string(first) + ": " + msg[first]);
+  }
   return CFD_OK;
 }
 }  // namespace
@@ -382,7 +404,21 @@ cfd_status group_run(cfd_solver* const* h, int32_t n, F&& f) {
 extern "C" {
 
 cfd_status cfd_group_step(cfd_solver* const* h, int32_t n) {
-  return group_run(h, n, [](cfd2::Solver& s) { s.step(); });
+  return group_run(h, n, [](cfd2::Solver& s) { s.step(); }, true);
+}
+
+cfd_status cfd_group_reset(cfd_solver* const* h, int32_t n) {
+  if (!h || n < 1) return set_error(CFD_ERR_INVALID, "bad argument");
+  for (int r = 0; r < n; ++r) CHECK_S(h[r]);
+  for (int r = 0; r < n; ++r) h[r]->s->needs_restore = false;
+  return CFD_OK;
+}
+
+int32_t cfd_group_needs_restore(cfd_solver* const* h, int32_t n) {
+  if (!h || n < 1) return 0;
+  for (int r = 0; r < n; ++r)
+    if (h[r] && h[r]->s && h[r]->s->needs_restore) return 1;
+  return 0;
 }
 
 cfd_status cfd_group_state_save(cfd_solver* const* h, int32_t n, const char* path) {
@@ -442,6 +478,46 @@ cfd_status cfd_dist_comm_stats(cfd_solver* s, cfd_comm_stats* out, int32_t reset
     if (reset) c->stats = cfd2::CommStats{};
   }
   return CFD_OK;
+}
+
+cfd_status cfd_comm_timing_enable(cfd_solver* s, int32_t enable) {
+  CHECK_S(s);
+  return guard([&] {
+    s->s->comm_prof_reset();
+    s->s->comm_prof = enable != 0;
+  });
+}
+
+cfd_status cfd_comm_timing(cfd_solver* s, cfd_comm_timing_entry* out, int32_t cap, int32_t* count) {
+  CHECK_S(s);
+  if (!count || (cap > 0 && !out)) return set_error(CFD_ERR_INVALID, "null argument");
+  return guard([&] {
+    cfd2::Solver& S = *s->s;
+    S.comm_drain();
+    int32_t k = 0;
+    for (int c = 0; c < cfd2::Solver::kCommCats && k < cap; ++c) {
+      const auto& t = S.comm_times[c];
+      if (!t.calls) continue;
+      cfd_comm_timing_entry& e = out[k++];
+      e.category = std::min(c, (int)cfd2::Solver::kCommAmgHalo);
+      e.level = c >= cfd2::Solver::kCommAmgHalo ? c - cfd2::Solver::kCommAmgHalo : -1;
+      e.calls = t.calls;
+      e.bytes = t.bytes;
+      e.wait_us = 1e3 * t.wait_ms;
+      e.comm_us = 1e3 * t.comm_ms;
+    }
+    *count = k;
+  });
+}
+
+cfd_status cfd_debug_group_fault_midstep(cfd_solver* const* h, int32_t n, int32_t fail_rank) {
+  return group_run(
+      h, n,
+      [fail_rank](cfd2::Solver& s) {
+        s.debug_fault_after_prepare = fail_rank;
+        s.step();
+      },
+      true);
 }
 
 cfd_status cfd_debug_group_fault(cfd_solver* const* h, int32_t n, int32_t fail_rank) {

@@ -217,6 +217,8 @@ Solver::~Solver() {
   for (auto e : ev_outer)
     if (e) (void)hipEventDestroy(e);
   for (auto e : prof_ev) (void)hipEventDestroy(e);
+  if (cstream) (void)hipStreamSynchronize(cstream);
+  for (auto e : comm_ev_pool) (void)hipEventDestroy(e);
   if (h_pin) (void)hipHostFree(h_pin);
   if (cstream) (void)hipStreamSynchronize(cstream);
   if (hev_pack) (void)hipEventDestroy(hev_pack);
@@ -336,7 +338,53 @@ void Solver::halo(HaloPlan& plan, std::initializer_list<HField> fields) {
   halo_end();
 }
 
-void Solver::halo_end() { CFD_HIP(hipStreamWaitEvent(stream, hev_done, 0)); }
+void Solver::halo_end() {
+  if (!comm_prof) {
+    CFD_HIP(hipStreamWaitEvent(stream, hev_done, 0));
+    return;
+  }
+  // the compute stream's stall on the exchange: from reaching the wait to its release
+  hipEvent_t a = comm_event(), b = comm_event();
+  CFD_HIP(hipEventRecord(a, stream));
+  CFD_HIP(hipStreamWaitEvent(stream, hev_done, 0));
+  CFD_HIP(hipEventRecord(b, stream));
+  comm_recs.push_back({halo_cat, 0, a, b});
+}
+
+hipEvent_t Solver::comm_event() {
+  if (comm_ev_used == comm_ev_pool.size()) {
+    if (comm_ev_pool.size() >= (1u << 14)) {  // fold what is pending, reuse the pool
+      comm_drain();
+    } else {
+      for (int k = 0; k < 256; ++k) {
+        hipEvent_t e;
+        CFD_HIP(hipEventCreate(&e));
+        comm_ev_pool.push_back(e);
+      }
+    }
+  }
+  return comm_ev_pool[comm_ev_used++];
+}
+
+void Solver::comm_drain() {
+  if (comm_recs.empty()) return;
+  CFD_HIP(hipStreamSynchronize(stream));
+  if (cstream) CFD_HIP(hipStreamSynchronize(cstream));
+  for (const CommRec& r : comm_recs) {
+    float ms = 0.0f;
+    CFD_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    CommTimes& t = comm_times[r.cat];
+    if (r.kind == 0 || r.kind == 2) t.wait_ms += ms;
+    if (r.kind == 1 || r.kind == 2) t.comm_ms += ms;
+  }
+  comm_recs.clear();
+  comm_ev_used = 0;
+}
+
+void Solver::comm_prof_reset() {
+  comm_drain();
+  for (CommTimes& t : comm_times) t = CommTimes{};
+}
 
 void Solver::halo_begin(HaloPlan& plan, std::initializer_list<HField> fields) {
   const uint32_t ns = (uint32_t)plan.send_idx.size();
@@ -368,7 +416,19 @@ void Solver::halo_begin(HaloPlan& plan, std::initializer_list<HField> fields) {
   }
   CFD_HIP(hipEventRecord(hev_pack, stream));
   CFD_HIP(hipStreamWaitEvent(cstream, hev_pack, 0));
-  comm->exchange(msgs, cstream);
+  halo_cat = comm_cat;
+  if (comm_prof) {
+    hipEvent_t a = comm_event(), b = comm_event();
+    CFD_HIP(hipEventRecord(a, cstream));
+    comm->exchange(msgs, cstream);
+    CFD_HIP(hipEventRecord(b, cstream));
+    comm_recs.push_back({halo_cat, 1, a, b});
+    CommTimes& t = comm_times[halo_cat];
+    t.calls++;
+    for (const Msg& mm : msgs) t.bytes += mm.sbytes;
+  } else {
+    comm->exchange(msgs, cstream);
+  }
   CFD_HIP(hipEventRecord(hev_done, cstream));
 }
 
@@ -396,7 +456,8 @@ RedSrc Solver::combine(const float* part, int nvec) {
     return r;
   }
   launch_seg_reduce(part, pstride, nunits, r.G, nvec, red_local, maxseg, stream);
-  comm->allgather(red_local, red_gather, (size_t)nvec * maxseg * sizeof(float), stream);
+  const size_t bytes = (size_t)nvec * maxseg * sizeof(float);
+  timed_gather(kCommReduceGather, bytes, [&] { comm->allgather(red_local, red_gather, bytes, stream); });
   r.p = red_gather;
   r.stride = maxseg;
   r.seg_src = d_seg_src;
@@ -415,7 +476,8 @@ RedSrcD Solver::combine_d(const double* part, int nvec) {
     return r;
   }
   launch_seg_reduce_d(part, pstride, nunits, r.G, nvec, red_local_d, maxseg, stream);
-  comm->allgather(red_local_d, red_gather_d, (size_t)nvec * maxseg * sizeof(double), stream);
+  const size_t bytes = (size_t)nvec * maxseg * sizeof(double);
+  timed_gather(kCommReduceGather, bytes, [&] { comm->allgather(red_local_d, red_gather_d, bytes, stream); });
   r.p = red_gather_d;
   r.stride = maxseg;
   r.seg_src = d_seg_src;
@@ -443,7 +505,7 @@ void Solver::prepare() {
   a.flux_s = flux_s;
   a.grad_u = grad_u;
   a.grad_v = grad_v;
-  launch_prepare(a, stream);
+  launch_prepare(a, stream, nt(64));
   check_launch("prepare");
   // commit d_p / grad_p (snapshot semantics): swap the scratch into the slot
   std::swap(S().dp, dp_scratch);
@@ -474,7 +536,7 @@ void Solver::assemble() {
   a.rhs = rhs;
   a.dinv_uv = dinv_uv;
   a.dinv_p = dinv_p;
-  launch_assemble(a, stream);
+  launch_assemble(a, stream, nt(64));
   check_launch("assemble");
   if (dist()) halo(cell_plan, {{dinv_uv, 1}});  // the Schur prediction reads neighbours' D_u^-1
 }
@@ -1219,6 +1281,7 @@ void Solver::v_cycle() {
       return;
     }
     const bool timed = i == 0 && prof_take();  // kernel time only: each part timed separately
+    const CommScope cs(this, amg_cat(i));
     overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
       AmgLevelDev d = Lv.dev;
       d.r0 = a;
@@ -1243,12 +1306,14 @@ void Solver::v_cycle() {
       d.r1 = b;
       d.r2 = a2;
       d.r3 = b2;
-      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream, nt(2));
+      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream, i == 0 && nt(2));
     };
-    if (Lv.dist)
+    if (Lv.dist) {
+      const CommScope cs(this, amg_cat(i));
       overlapped(Lv.plan, {{Lv.x, 1}}, Lv.dev.n, f);
-    else
+    } else {
       f(0, Lv.dev.n, 0, 0);
+    }
   };
   bool presmoothed = false;  // level i's zero-x pre-smoother already ran inside the restriction
   for (int i = 0; i < down; ++i) {
@@ -1278,6 +1343,7 @@ void Solver::v_cycle() {
       const uint32_t cg_hi = into_dist ? C.ghi : (uint32_t)(C.nglob - C.C1);
       float* so = into_dist ? smo : nullptr;
       const uint32_t split = Lv.dev.n >= overlap_min_rows ? Lv.rc_hi : 0u;  // as overlapped()
+      const CommScope cs(this, amg_cat(i));
       halo_begin(Lv.plan, {{Lv.r, 1}});
       if (split > 0) launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false);
       halo_end();
@@ -1286,7 +1352,7 @@ void Solver::v_cycle() {
     if (Lv.dist && !C.dist) {  // into the first replicated level: own slice, all-gather
       std::vector<size_t> off(R + 1);
       for (int q = 0; q <= R; ++q) off[q] = C.part[q] * sizeof(float);
-      comm->allgatherv_inplace(C.b, off, stream);
+      timed_gather(kCommRepGather, off[R] - off[rk + 1] + off[rk], [&] { comm->allgatherv_inplace(C.b, off, stream); });
     }
   }
   if (tf < L && tf == tail_blob_first) {
@@ -1305,6 +1371,7 @@ void Solver::v_cycle() {
     if (levels[ii + 1].dist) {  // the rows of owned aggregates overlap the coarse-x exchange
       AmgGpuLevel& F = levels[ii];
       const uint32_t split = F.dev.n >= overlap_min_rows ? F.pf_lo : F.dev.n;  // as overlapped()
+      const CommScope cs(this, amg_cat(ii + 1));
       halo_begin(levels[ii + 1].plan, {{levels[ii + 1].x, 1}});
       if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n);
       halo_end();
@@ -1330,6 +1397,7 @@ void Solver::precondition(int j, float* z) {
   const bool jacobi = constants.precond_type != 1;
   float* v = basis + (size_t)j * stride;  // V_j = binv[j] * W_j
   // the prediction reads neighbours' r_u, r_v
+  const CommScope cs(this, kCommKrylovHalo);
   overlapped(cell_plan, {{v, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix Ar = A;
     Ar.r0 = a;
@@ -1383,7 +1451,7 @@ void Solver::precondition(int j, float* z) {
     Ar.r1 = b;
     Ar.r2 = a2;
     Ar.r3 = b2;
-    launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream);
+    launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream, nt(32));
   });
 }
 
@@ -1411,6 +1479,7 @@ float Solver::residual_into_v0_blocking() {
 
 void Solver::residual_into_v0_launch() {
   // g = [||r||, 0, ...]: the zero fill is part of the norm's finishing kernel
+  const CommScope cs(this, kCommKrylovHalo);
   overlapped(cell_plan, {{x, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
     CoupledMatrix A = cmat();
     A.r0 = a;
@@ -1478,6 +1547,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       ++total;
       float* zj = zvec + (size_t)j * stride;
       precondition(j, zj);
+      const CommScope cs(this, kCommKrylovHalo);
       overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
         CoupledMatrix A = cmat();
         A.r0 = a;
@@ -1673,8 +1743,11 @@ void Solver::step() {  // coupled_solver.rs:33-499
   }
   rotate();
   constants.component = 0;
+  const int fault_rank = debug_fault_after_prepare;  // test hook, one step only
+  debug_fault_after_prepare = -1;
   if (dist()) halo_state(true);  // the rotated slot's ghosts (last written 3 steps ago)
   prepare();
+  if (fault_rank == rk) throw std::runtime_error("injected fault after prepare");
   const bool fixed = cfg.fixed_outer > 0;
   const int max_iters = fixed ? cfg.fixed_outer : std::max(cfg.n_outer_correctors, 10);
   const double tol_u = 1e-5, tol_p = 1e-4;
@@ -1702,7 +1775,8 @@ void Solver::step() {  // coupled_solver.rs:33-499
     check_launch("update_fields");
     if (dist()) {
       halo_state(false);  // the next prepare reads neighbours' u, p
-      comm->allgather(maxbits, mx_gather, 2 * sizeof(uint32_t), stream);
+      timed_gather(kCommReduceGather, 2 * sizeof(uint32_t),
+                   [&] { comm->allgather(maxbits, mx_gather, 2 * sizeof(uint32_t), stream); });
       launch_max_combine(mx_gather, R, maxbits, host_slot, stream);
     }
     if (iter == 0) {
@@ -1915,9 +1989,10 @@ double Solver::smoother_layout_bytes() const {
 // Layout-true bytes of one step under the fixed schedule: per kernel, the
 // bytes its arrays in THIS library's layouts must move (each element once:
 // neighbour gathers counted once, as SURVEY §8(d) counts them), times its
-// launches per step.  Unlike the reference-format count this is a lower bound
-// of the HBM traffic the kernels generate, so count / step time <= the
-// achieved rate (compare with the PMC step traffic, step_counter_traffic).
+// launches per step: the minimum traffic at kernel level.  It is not a lower
+// bound of the HBM traffic: the kernel order is tuned so that some lines come
+// from the Infinity Cache, so the PMC step traffic
+// (step_counter_traffic) can be below it.
 double Solver::layout_step_bytes() const {
   const double Nn = N;
   double S = 0.0, Sint = 0.0;  // used face slots, internal ones
@@ -1944,7 +2019,10 @@ double Solver::layout_step_bytes() const {
     const double smooth = st + img + 16 * n;
     if (i < down) {
       const double nc = levels[i + 1].dev.n;
-      vc += (i == 0 ? smooth : 12 * n);                                // pre-smoother (coarse: zero-x, elementwise)
+      // pre-smoother (coarse: zero-x, elementwise; not launched when fused into
+      // the previous level's restriction, whose 12 nc term counts it)
+      const bool presmoothed = i > 0 && fuse_presmooth && (!levels[i - 1].dist || levels[i].dist);
+      vc += (i == 0 ? smooth : (presmoothed ? 0.0 : 12 * n));
       if (d.rr_agg && !levels[i].dist)
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
       else

@@ -314,9 +314,18 @@ struct Solver {
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
   // nontemporal loads of the matrix streams (kernels.hip ldx), per kernel, for
   // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
-  // 1 post-smoother of the split levels, 2 AMG residual, 4 Schur prediction,
-  // 8 SpMV, 16 pre-smoother.  Same bits either way.
+  // 1 post-smoother of the split levels, 2 level-0 AMG residual, 4 Schur
+  // prediction, 8 SpMV, 16 pre-smoother, 32 Schur correction, 64 the face-slot
+  // geometry of prepare / assemble.  Same bits either way.
   unsigned nt_mask = 0;
+  // an in-process group step failed on some rank: the ranks stopped at
+  // different points of the step (ring rotation, time, FGMRES state), so the
+  // group refuses to step until its state is restored on every rank
+  // (cfd_state_load) or the caller accepts it (cfd_group_reset)
+  bool needs_restore = false;
+  // test hook (cfd_debug_group_fault_midstep): throw right after the step's
+  // first prepare() when this rank's index matches
+  int debug_fault_after_prepare = -1;
   bool nt(unsigned bit) const { return (nt_mask & bit) != 0; }
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
@@ -521,6 +530,70 @@ struct Solver {
   }
   hipStream_t cstream = nullptr;  // RCCL / peer-copy stream of the halo exchanges
   hipEvent_t hev_pack = nullptr, hev_done = nullptr;
+
+ public:
+  // ---- timing of the distributed communication (cfd_comm_timing) ----
+  // While comm_prof is on, every halo exchange and all-gather of the step is
+  // bracketed by timing events: `wait` = how long the compute stream stood
+  // still for it (a halo: from the wait on the exchange's completion event
+  // to its release; an all-gather, which runs on the compute stream: its
+  // whole duration), `comm` = the transport's own time (a halo: the grouped
+  // send/recv on the comm stream, including the wait for the peers).  Per
+  // category; AMG halos per level.
+  enum CommCat {
+    kCommKrylovHalo = 0,   // V_j / p_sol / Z_j / x halos of the FGMRES iteration
+    kCommStateHalo = 1,    // FluidState, prepare / assemble outputs, check_evolution records
+    kCommReduceGather = 2, // segment values of the reductions (CGS dots, norms), max-diff
+    kCommRepGather = 3,    // rhs of the first replicated AMG level
+    kCommAmgHalo = 4,      // + level: x / residual / coarse-x halos of AMG level l
+  };
+  static constexpr int kCommAmgLevels = 28;
+  static constexpr int kCommCats = kCommAmgHalo + kCommAmgLevels;
+  struct CommTimes {
+    uint64_t calls = 0;
+    double wait_ms = 0.0, comm_ms = 0.0;
+    uint64_t bytes = 0;
+  };
+  CommTimes comm_times[kCommCats];
+  bool comm_prof = false;
+  void comm_prof_reset();
+  static int amg_cat(int level) { return kCommAmgHalo + std::min(level, kCommAmgLevels - 1); }
+  void comm_drain();  // synchronise both streams, fold the pending records into comm_times
+  struct CommScope {  // category of the halos / all-gathers issued inside the scope
+    Solver* s;
+    int prev;
+    CommScope(Solver* s_, int c) : s(s_), prev(s_->comm_cat) { s->comm_cat = c; }
+    ~CommScope() { s->comm_cat = prev; }
+  };
+
+ private:
+  int comm_cat = kCommStateHalo;
+  int halo_cat = kCommStateHalo;  // category of the exchange in flight (halo_begin -> halo_end)
+  struct CommRec {
+    int cat, kind;  // kind 0: compute-stream wait, 1: comm time
+    hipEvent_t a, b;
+  };
+  std::vector<CommRec> comm_recs;
+  std::vector<hipEvent_t> comm_ev_pool;
+  size_t comm_ev_used = 0;
+  hipEvent_t comm_event();
+  // an all-gather on the compute stream, timed when comm_prof is on
+  template <class F>
+  void timed_gather(int cat, size_t bytes, F&& f) {
+    if (!comm_prof) {
+      f();
+      return;
+    }
+    hipEvent_t a = comm_event(), b = comm_event();
+    CFD_HIP(hipEventRecord(a, stream));
+    f();
+    CFD_HIP(hipEventRecord(b, stream));
+    comm_recs.push_back({cat, 2, a, b});  // kind 2: counts as both wait and comm
+    comm_times[cat].calls++;
+    comm_times[cat].bytes += bytes;
+  }
+
+ private:
   void halo_state(bool all);
   // the source the finishing kernels read for nvec reductions of chunk
   // partials part[v * nchunks + k]: the partials themselves on one GPU; on a

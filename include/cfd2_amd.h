@@ -333,6 +333,13 @@ cfd_status cfd_solver_create_dist_host(const cfd_mesh_view* mesh, const cfd_conf
 cfd_status cfd_group_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t nranks,
                             const int32_t* devices, cfd_solver** out /* [nranks] */);
 cfd_status cfd_group_step(cfd_solver* const* handles, int32_t nranks);
+/* A cfd_group_step that failed on any rank leaves the ranks at different
+ * points of the step, so the group is marked "needs restore": further
+ * cfd_group_step calls return CFD_ERR_INVALID until every rank has loaded a
+ * consistent state (cfd_state_load, per rank) or the caller accepts the state
+ * as is (cfd_group_reset).  cfd_group_needs_restore: 1 while marked.       */
+cfd_status cfd_group_reset(cfd_solver* const* handles, int32_t nranks);
+int32_t cfd_group_needs_restore(cfd_solver* const* handles, int32_t nranks);
 /* RCCL plumbing check on one GPU: 1-rank communicator, grouped send/recv to
  * self and an all-gather through the solver's transport; CFD_OK if the data
  * arrived intact.                                                           */
@@ -350,10 +357,37 @@ typedef struct {
   uint64_t bytes_gathered;  /* all-gather payload bytes this rank contributed */
 } cfd_comm_stats;
 cfd_status cfd_dist_comm_stats(cfd_solver* s, cfd_comm_stats* out, int32_t reset);
+/* Timing of the distributed communication by category (measurement aid for
+ * the multi-GPU runs; no reference counterpart).  While enabled, every halo
+ * exchange and all-gather is bracketed by timing events (a small cost:
+ * bench.py times its headline steps with it off, then one extra step with it
+ * on).  category: 0 Krylov halos (V_j, p_sol, Z_j, x), 1 state / assembly
+ * halos, 2 reduction all-gathers (dots, norms, max-diff), 3 the all-gather of
+ * the first replicated AMG level's rhs, 4 AMG level halos (`level` = the AMG
+ * level).  wait_us: time the compute stream stood still for the operation
+ * (halos: from reaching the wait on the exchange to its release; all-gathers
+ * run on the compute stream: their whole duration); comm_us: the
+ * transport's own time (halos: the grouped send/recv on the comm stream,
+ * peer waits included).  enable resets the totals.                         */
+typedef struct {
+  int32_t category;
+  int32_t level;    /* AMG level (category 4), else -1 */
+  uint64_t calls;
+  uint64_t bytes;   /* payload this rank sent / contributed */
+  double wait_us;
+  double comm_us;
+} cfd_comm_timing_entry;
+cfd_status cfd_comm_timing_enable(cfd_solver* s, int32_t enable);
+/* the non-empty categories, at most `cap`; *count = how many were written  */
+cfd_status cfd_comm_timing(cfd_solver* s, cfd_comm_timing_entry* out, int32_t cap, int32_t* count);
 /* In-process group failure path (test hook): every rank enters a collective
  * except `fail_rank`, which fails first; the others must return an error
  * instead of waiting forever, and the group must stay usable afterwards.     */
 cfd_status cfd_debug_group_fault(cfd_solver* const* handles, int32_t nranks, int32_t fail_rank);
+/* ... and a failure in the middle of a step: `fail_rank` throws right after
+ * the step's first prepare() while the other ranks continue until their next
+ * collective; the group is then marked needs-restore (see cfd_group_reset). */
+cfd_status cfd_debug_group_fault_midstep(cfd_solver* const* handles, int32_t nranks, int32_t fail_rank);
 /* rank, rank count, owned global range [c0, c1), global cell count         */
 cfd_status cfd_dist_info(const cfd_solver* s, int32_t* rank, int32_t* nranks, uint32_t* c0,
                          uint32_t* c1, uint32_t* num_global_cells);

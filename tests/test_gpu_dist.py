@@ -228,3 +228,37 @@ def test_group_device_setup_equals_host_setup(nranks, rep, which, replicate_rows
     _assert_same_info(d, h, f"{which} R={nranks} device vs host setup")
     h.close()
     d.close()
+
+
+def test_comm_timing_categories_and_bits(replicate_rows):
+    """cfd_comm_timing (the multi-GPU line's exposed-communication fields):
+    with timing on, every category of the distributed step shows up with its
+    calls and non-negative times, AMG halos per level, and the bracketing
+    events change no result bit (group == one GPU == oracle)."""
+    replicate_rows(64)  # distributed coarse levels + the replicated-level all-gather
+    mesh = backwards_step()
+    grp = GpuGroup(mesh, 3)
+    one = GpuSolver(mesh)
+    orc = OracleSolver(mesh)
+    for s in (grp, one, orc):
+        _setup_amg_test(s, mesh, 1)
+    for r in grp.ranks:
+        r.comm_timing_enable(True)
+    for step in range(2):
+        grp.step()
+        one.step()
+        orc.step()
+        _assert_same_fields(grp, one, f"timed group step {step}")
+        _assert_same_fields(one, orc, f"one GPU step {step}")
+    for r in grp.ranks:
+        t = r.comm_timing()
+        cats = {(e["category"], e["level"]) for e in t}
+        for need in [("krylov_halo", -1), ("state_halo", -1), ("reduction_allgather", -1),
+                     ("replicated_level_allgather", -1), ("amg_halo", 0)]:
+            assert need in cats, (need, cats)
+        for e in t:
+            assert e["calls"] > 0 and e["wait_us"] >= 0.0 and e["comm_us"] >= 0.0, e
+        r.comm_timing_enable(False)
+        assert r.comm_timing() == []
+    grp.close()
+    one.close()

@@ -91,3 +91,41 @@ def test_group_rank_failure_then_reuse():
     assert st["exchanges"] > 0 and st["allgathers"] > 0
     grp.close()
     one.close()
+
+
+def test_group_midstep_failure_needs_restore(tmp_path):
+    """A rank that fails in the middle of a group step (after its first
+    prepare(), while the others run on to their next collective) leaves the
+    ranks at different points of the step: the group refuses to step again
+    until every rank loads a consistent state, and after the load it steps
+    bit-exactly like one GPU from the same checkpoint."""
+    mesh = backwards_step()
+    grp = GpuGroup(mesh, 3)
+    one = GpuSolver(mesh)
+    for s in (grp, one):
+        _setup_amg_test(s, mesh, 1)
+    for _ in range(2):
+        grp.step()
+        one.step()
+    path = str(tmp_path / "ckpt.bin")
+    grp.save_state(path)
+    assert not grp.needs_restore
+    with pytest.raises(RuntimeError, match="rank 1: injected fault after prepare"):
+        grp.debug_fault_midstep(1)
+    assert grp.needs_restore
+    with pytest.raises(RuntimeError, match="needs restore"):
+        grp.step()
+    grp.load_state(path)
+    assert not grp.needs_restore
+    for step in range(2):
+        grp.step()
+        one.step()
+        _assert_same_fields(grp, one, f"group after restore, step {step}")
+        _assert_same_info(grp, one, f"group after restore, step {step}")
+    with pytest.raises(RuntimeError, match="rank 0: injected fault after prepare"):
+        grp.debug_fault_midstep(0)
+    assert grp.needs_restore
+    grp.reset()  # the caller accepts the state as is
+    assert not grp.needs_restore
+    grp.close()
+    one.close()
