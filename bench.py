@@ -31,7 +31,9 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: (h, target cells per GPU, BASELINE.json configs[] index)
-    "c0": (0.0172, 1.0e4, 0),  # the reference-test scale (CPU-runnable); launch-bound on a GPU
+    # the reference-test scale (CPU-runnable; launch-bound on a GPU): the seeded
+    # Voronoi channel (BASELINE configs[0] names Voronoi cells), h of the Voronoi mesher
+    "c0": (0.0138, 1.0e4, 0),
     "c1": (0.001723, 1.0e6, 1),
     "c2": (5.449e-4, 1.0e7, 2),
 }
@@ -336,7 +338,11 @@ def main():
         if args.mesh_cache and os.path.exists(args.mesh_cache):
             from cfd2_amd.mesh import Mesh
             return Mesh.load(args.mesh_cache)
-        m = bench_channel(h_run, 100)
+        if args.config == "c0":
+            from cfd2_amd.mesh import bench_voronoi_channel
+            m = bench_voronoi_channel(h_run)
+        else:
+            m = bench_channel(h_run, 100)
         if args.mesh_cache and rank == 0:
             m.save(args.mesh_cache)
         return m
@@ -551,7 +557,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: deterministic cut-cell channel+obstacle mesh (reference generator restated)",
+        "data": ("synthetic: seeded Voronoi channel+obstacle mesh (voronoi.rs restated, seed 12345)"
+                 if args.config == "c0" else
+                 "synthetic: deterministic cut-cell channel+obstacle mesh (reference generator restated)"),
         "config": {
             "workload": (f"BASELINE {cfg_label}: channel+obstacle {n_global} cells on {world} GPU(s) (~{n_cells} per rank), "
                          f"fixed schedule {args.outer} Picard x {args.inner} FGMRES/AMG per step"

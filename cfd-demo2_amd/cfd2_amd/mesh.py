@@ -200,6 +200,19 @@ def channel_obstacle_h(target_cells: float) -> float:
     return float(np.sqrt(2.9686 / target_cells))
 
 
+C0_VORONOI_H = 0.0138  # ~10.1 k cells (BASELINE configs[0]: "~10k Voronoi cells")
+
+
+def bench_voronoi_channel(h: float = C0_VORONOI_H, seed: int = 12345) -> Mesh:
+    """BASELINE configs[0]: the same ChannelWithObstacle{3x1, (1.0,0.51), r 0.1}
+    meshed by the seeded Voronoi generator (voronoi.rs:23-721 restated,
+    cfd_mesh_generate_voronoi) with min = max = h: 10,106 polygonal cells at
+    the default h."""
+    geo = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.51),
+                              obstacle_radius=0.1)
+    return generate_voronoi_mesh(geo, h, h, 1.2, (3.0, 1.0), seed=seed)
+
+
 def bench_channel(h: float, smooth_iters: int = 100) -> Mesh:
     """SURVEY §8(d) synthetic input: ChannelWithObstacle{3x1, (1.0,0.51), r 0.1},
     cut-cell with min=max=h, growth 1.2, then smooth(0.3, 100)."""

@@ -1086,8 +1086,14 @@ void ensure_fgmres(oracle_solver* s) {
   if (s->fgmres_init) return;
   const size_t n = 3 * (size_t)s->N;
   const int m = s->m;
-  s->basis.assign((size_t)(m + 1) * n, 0.0f);
-  s->zvec.assign((size_t)m * n, 0.0f);
+  // under a fixed schedule a solve is one cycle of min(fixed_inner, m)
+  // iterations (solve(): inner_max, outer_max = 1), so only that many basis /
+  // Z vectors are ever touched: allocate those (the 40 M / 80 M-cell parity
+  // legs of tests/test_gpu_configs.py would otherwise need 100+ GB for the
+  // basis alone); the algorithm and its bits are unchanged
+  const int kb = s->cfg.fixed_inner > 0 ? std::min(s->cfg.fixed_inner, m) : m;
+  s->basis.assign((size_t)(kb + 1) * n, 0.0f);
+  s->zvec.assign((size_t)kb * n, 0.0f);
   s->w.assign(n, 0.0f);
   s->temp.assign(n, 0.0f);
   s->temp_p.assign(s->N, 0.0f);

@@ -1,14 +1,23 @@
-"""Every BASELINE.json config under parity on the HIP path.
+"""Every BASELINE.json config under parity on the HIP path (VERDICT r02 item 1,
+r03 item 1).
 
 - C2 (configs[2], 10 M cells): the bench's exact fixed schedule, 5 Picard x
   30 FGMRES iterations, the t = 0 step and the first real step (the bench's
   two warm-up steps), GPU == oracle bit-exact after each.
-- C3 (configs[3], 40 M cells, 4 ranks): GpuGroup(4) == GpuSolver bit-exact on
-  one GPU (the distributed algorithm the RCCL path runs; the oracle's
-  equality with GpuSolver is established at C2 and on every smaller case).
-- C4 (configs[4], 80 M cells, 8 ranks): the same with 8 in-process ranks; the
-  single-GPU run goes first and is freed before the group is built (two
-  80 M-cell solvers do not both fit).  ~4 min: CFD_C4_PARITY=1 enables it.
+- C3 (configs[3], 40 M cells, 4 ranks): GpuGroup(4) == GpuSolver bit-exact
+  under the bench's 5 x 30 schedule (one step at t = 0.05), and
+  GpuGroup(4) == OracleSolver bit-exact under a short fixed schedule
+  (1 Picard x 6 FGMRES iterations): 40 M-cell HIP output tied to the oracle.
+- C4 (configs[4], 80 M cells, 8 ranks): GpuSolver, GpuGroup(8) and the
+  oracle, all under the 1 x 6 schedule, bit-identical; each solver is freed
+  before the next is built (two 80 M-cell solvers do not both fit).
+
+At 40 M / 80 M rows the coupled matrices hold more than 2^31 entries and the
+AMG hierarchy is deeper than at C2, so these legs check the single-GPU path
+(coupled_solver.rs:33-499, coupled_solver_fgmres.rs:1728-2448, amg.rs:374-595)
+where nothing smaller does.  The oracle's Krylov basis is sized to the fixed
+schedule (oracle.cpp ensure_fgmres: 7 vectors for 6 iterations; 64 GB of
+host memory at 80 M cells instead of ~160 GB).
 
 Each phase prints a progress line straight to the terminal (pytest's capture
 disabled for that line) so a long test is never mistaken for a hung one.
@@ -85,62 +94,106 @@ def test_c2_headline_schedule_bitexact(progress):
     g.close()
 
 
-def _group_vs_one(config, nranks, progress, cfg=None, t0=0.05):
-    """One GPU first (its fields kept on the host, the solver freed), then the
-    in-process group of `nranks` ranks on the same GPU: bit-identical fields,
-    step statistics and AMG hierarchy."""
-    cfg = cfg or dict(fixed_outer=2, fixed_inner=10)
-    mesh = bench_channel(BENCH_H[config], 100)
-    n = mesh.num_cells()
-    progress(f"{config} mesh {n} cells")
-    one = GpuSolver(mesh, config=default_config(**cfg))
-    _bench_setup(one, t0)
-    progress(f"{config} GpuSolver created")
-    one.step()
-    progress(f"{config} GpuSolver step done")
-    want = (one.get_u(), one.get_p(), one.get_d_p())
-    info1 = one.step_info()
-    levels1 = one.amg_levels()
-    one.close()
-    del one
+def _leg(make, mesh, cfg, t0, progress, label):
+    """Build one solver of the leg, run one step, keep the fields / statistics /
+    hierarchy on the host, free the solver."""
+    s = make(mesh, cfg)
+    _bench_setup(s, t0)
+    progress(f"{label} created")
+    s.step()
+    progress(f"{label} step done")
+    out = {"fields": (s.get_u(), s.get_p(), s.get_d_p()), "info": s.step_info(), "levels": s.amg_levels(),
+           "ranks": [r.amg_levels() for r in s.ranks] if hasattr(s, "ranks") else None,
+           "comm": [r.comm_stats() for r in s.ranks] if hasattr(s, "ranks") else None}
+    if hasattr(s, "close"):
+        s.close()
+    del s  # the oracle frees its state when collected
     gc.collect()
-    grp = GpuGroup(mesh, nranks, config=default_config(**cfg))
-    del mesh
-    gc.collect()
-    _bench_setup(grp, t0)
-    progress(f"{config} GpuGroup({nranks}) created")
-    grp.step()
-    progress(f"{config} GpuGroup({nranks}) step done")
-    got = (grp.get_u(), grp.get_p(), grp.get_d_p())
-    for a, b, name in zip(got, want, ("u", "p", "d_p")):
-        assert np.all(np.isfinite(a)), name
-        assert np.array_equal(a, b), f"{config} R={nranks} {name} differs (max {np.abs(a - b).max()})"
-    ig = grp.step_info()
+    return out
+
+
+def _same(a, b, label):
+    for x, y, name in zip(a["fields"], b["fields"], ("u", "p", "d_p")):
+        assert np.all(np.isfinite(x)), f"{label} {name} not finite"
+        assert np.array_equal(x, y), f"{label}: {name} differs (max {np.abs(x - y).max()})"
+    ia, ib = a["info"], b["info"]
     for f in ("outer_iterations", "total_linear_iterations", "outer_residual_u", "outer_residual_p"):
-        assert getattr(ig, f) == getattr(info1, f), f
-    assert ig.stats_p.residual == info1.stats_p.residual
-    # the same hierarchy: row-partitioned levels sum to the one-GPU level,
-    # replicated levels are the one-GPU level on every rank
-    per_rank = [r.amg_levels() for r in grp.ranks]
+        assert getattr(ia, f) == getattr(ib, f), f"{label}: {f}"
+    assert ia.stats_p.residual == ib.stats_p.residual, label
+    assert np.abs(a["fields"][0]).max() > 0.01, label
+
+
+def _global_levels(per_rank):
+    """The global hierarchy from every rank's levels: a replicated level is the
+    same on every rank, a row-partitioned one sums over the ranks."""
+    out = []
+    for i in range(len(per_rank[0])):
+        lv = [p[i] for p in per_rank]
+        out.append(lv[0] if all(x == lv[0] for x in lv) else (sum(x[0] for x in lv), sum(x[1] for x in lv)))
+    return out
+
+
+def _group_hierarchy(g, one, nranks):
+    """Row-partitioned levels sum to the one-GPU level; replicated levels are
+    the one-GPU level on every rank; the transport reports every rank."""
+    levels1 = one["levels"]
+    per_rank = g["ranks"]
     assert all(len(lv) == len(levels1) for lv in per_rank)
     for i, (rows1, nnz1) in enumerate(levels1):
         lv = [p[i] for p in per_rank]
         if all(x == lv[0] for x in lv) and lv[0] == (rows1, nnz1):
             continue
         assert sum(x[0] for x in lv) == rows1 and sum(x[1] for x in lv) == nnz1, (i, lv, rows1, nnz1)
-    assert np.abs(got[0]).max() > 0.01
-    for r in range(nranks):
-        st = grp.ranks[r].comm_stats()
+    for r, st in enumerate(g["comm"]):
         assert st["comm_count"] == nranks and st["comm_rank"] == r
-    grp.close()
 
 
-def test_c3_group4_equals_one_gpu(progress):
-    """configs[3] (40 M cells, 4 ranks): GpuGroup(4) == GpuSolver bit-exact."""
-    _group_vs_one("c3", 4, progress)
+def _gpu(mesh, cfg):
+    return GpuSolver(mesh, config=default_config(**cfg))
 
 
-@pytest.mark.skipif(os.environ.get("CFD_C4_PARITY") != "1", reason="~4 min: CFD_C4_PARITY=1")
-def test_c4_group8_equals_one_gpu(progress):
-    """configs[4] (80 M cells, 8 ranks): GpuGroup(8) == GpuSolver bit-exact."""
-    _group_vs_one("c4", 8, progress)
+def _group(nranks):
+    return lambda mesh, cfg: GpuGroup(mesh, nranks, config=default_config(**cfg))
+
+
+def _oracle(mesh, cfg):
+    olib().oracle_set_threads(min(16, os.cpu_count() or 1))
+    return OracleSolver(mesh, config=default_config(**cfg))
+
+
+SHORT = dict(fixed_outer=1, fixed_inner=6)
+BENCH = dict(fixed_outer=5, fixed_inner=30)
+
+
+def test_c3_group4_bench_schedule_and_oracle(progress):
+    """configs[3] (40 M cells, 4 ranks): GpuGroup(4) == GpuSolver under the
+    bench's 5 x 30 schedule, and GpuGroup(4) == OracleSolver under 1 x 6."""
+    mesh = bench_channel(BENCH_H["c3"], 100)
+    assert mesh.num_cells() > 39_000_000
+    progress(f"C3 mesh {mesh.num_cells()} cells")
+    one = _leg(_gpu, mesh, BENCH, 0.05, progress, "C3 GpuSolver 5x30")
+    grp = _leg(_group(4), mesh, BENCH, 0.05, progress, "C3 GpuGroup(4) 5x30")
+    _same(grp, one, "C3 5x30 group vs one GPU")
+    assert grp["info"].total_linear_iterations == 150
+    _group_hierarchy(grp, one, 4)
+    del one, grp
+    gs = _leg(_group(4), mesh, SHORT, 0.05, progress, "C3 GpuGroup(4) 1x6")
+    orc = _leg(_oracle, mesh, SHORT, 0.05, progress, "C3 oracle 1x6")
+    _same(gs, orc, "C3 1x6 group vs oracle")
+    assert _global_levels(gs["ranks"]) == orc["levels"]
+
+
+def test_c4_group8_one_gpu_and_oracle(progress):
+    """configs[4] (80 M cells, 8 ranks): GpuSolver == GpuGroup(8) ==
+    OracleSolver under 1 x 6 at t = 0.05."""
+    mesh = bench_channel(BENCH_H["c4"], 100)
+    assert mesh.num_cells() > 79_000_000
+    progress(f"C4 mesh {mesh.num_cells()} cells")
+    one = _leg(_gpu, mesh, SHORT, 0.05, progress, "C4 GpuSolver 1x6")
+    grp = _leg(_group(8), mesh, SHORT, 0.05, progress, "C4 GpuGroup(8) 1x6")
+    _same(grp, one, "C4 group vs one GPU")
+    _group_hierarchy(grp, one, 8)
+    del grp
+    orc = _leg(_oracle, mesh, SHORT, 0.05, progress, "C4 oracle 1x6")
+    _same(one, orc, "C4 one GPU vs oracle")
+    assert one["levels"] == orc["levels"]

@@ -132,10 +132,16 @@ def test_coupled_schemes_steps(scheme, time_scheme):
     assert np.all(np.isfinite(r.get_u())) and np.all(np.isfinite(r.get_p()))
 
 
-def test_c0_channel_fixed_schedule():
-    """BASELINE configs[0] (~10 k-cell channel + obstacle, bench physics), AMG:
-    two steps of 2 Picard x 8 FGMRES, inlet on."""
-    mesh = bench_mesh(0.0172, 100)
+@pytest.mark.parametrize("kind", ["voronoi", "cutcell"])
+def test_c0_channel_fixed_schedule(kind):
+    """BASELINE configs[0] (~10 k Voronoi cells, channel + obstacle, bench
+    physics; also its cut-cell counterpart), AMG: two steps of 2 Picard x 8
+    FGMRES, inlet on."""
+    if kind == "voronoi":
+        from cfd2_amd.mesh import bench_voronoi_channel
+        mesh = bench_voronoi_channel()
+    else:
+        mesh = bench_mesh(0.0172, 100)
     assert 9000 < mesh.num_cells() < 11000
     cfg = dict(convergence_lag=0, fixed_outer=2, fixed_inner=8)
     o = OracleSolver(mesh, config=default_config(**cfg))

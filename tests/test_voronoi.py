@@ -86,3 +86,31 @@ def test_voronoi_group_parity(nranks):
         g.close()
     finally:
         os.environ.pop("CFD_AMG_REPLICATE_ROWS", None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precond", [1, 0])
+def test_c0_voronoi_bench_mesh_gpu_parity(precond):
+    """BASELINE configs[0] as named: the ~10 k-cell seeded Voronoi channel +
+    obstacle (bench.py --config c0), bench physics from t = 0.05; AMG under
+    the bench's 5 x 30 schedule, Jacobi under the reference's natural
+    schedule; two steps each, GPU == oracle bit-exact."""
+    from cfd2_amd import GpuSolver
+    from cfd2_amd.mesh import bench_voronoi_channel
+    from tests.test_gpu_configs import _bench_setup
+    from tests.test_gpu_parity import _assert_same_fields, _assert_same_info
+    m = bench_voronoi_channel()
+    assert 9000 < m.num_cells() < 11000
+    cfg = dict(fixed_outer=5, fixed_inner=30) if precond == 1 else {}
+    g = GpuSolver(m, config=default_config(**cfg))
+    o = OracleSolver(m, config=default_config(**cfg))
+    for s in (g, o):
+        _bench_setup(s, 0.05)
+        s.set_precond_type(precond)
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"C0 voronoi precond {precond} step {k}")
+        _assert_same_info(g, o, f"C0 voronoi precond {precond} step {k}")
+    assert np.abs(g.get_u()).max() > 0.01
+    g.close()
