@@ -1874,11 +1874,12 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const
 }
 
 // coarse value I of the restriction: sum_{f in R row I, ascending} 1.0 * r[f]
+template <bool NT = false>
 __device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float* __restrict__ r, uint32_t I) {
   float sum = 0.0f;
   if (L.r_m4) {
     // the first 4 members in one 16-byte load, then their values
-    const int4 m = L.r_m4[I];
+    const int4 m = ldx<NT>(L.r_m4 + I);
     const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
     const int f[4] = {m.x, m.y, m.z, over ? -2 - m.w : m.w};
     float v[4];
@@ -1912,6 +1913,7 @@ __device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float*
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
 // also clears the coarse solution (amg.rs:721-725 `clear`, fused), including
 // its ghost entries [-glo, 0) and [stride_c, stride_c + ghi) on a distributed level
+template <bool NT>
 __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
                                                          float* __restrict__ cb,
                                                          float* __restrict__ cx, uint32_t stride_c,
@@ -1923,7 +1925,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
   if (I < I1) {
     // the coarse diagonal loaded with the members (no round trip after the sum)
     const float dec = sm_out ? sm_de[I] : 1.0f;
-    const float sum = restrict_sum(L, r, I);
+    const float sum = restrict_sum<NT>(L, r, I);
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
       sm_out[I] = wmix(0.0f, (sum - 0.0f) / dec, 0.8f);
@@ -2012,12 +2014,13 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
 // prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread.
 // agg is a signed local index on a distributed level (aggregates seeded on a
 // lower rank are ghosts of xc below 0).
+template <bool NT>
 __global__ void __launch_bounds__(kBlock) k_amg_prolong(AmgLevelDev L, float* __restrict__ x,
                                                         const float* __restrict__ xc, uint32_t f0, uint32_t f1) {
   const uint32_t i0 = f0 + 4 * row_id();
   if (i0 >= f1) return;
   float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
+  const int4 ag = ldv<NT, int4>(L.agg + i0);
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;  // padding rows (>= n) get 0
   c0 += 1.0f * xc[ag.x];
   if (i0 + 1 < L.n) c1 += 1.0f * xc[ag.y];
@@ -2656,11 +2659,11 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
                          uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de, uint32_t I0,
-                         uint32_t I1, bool ghosts) {
+                         uint32_t I1, bool ghosts, bool nt) {
   if (I1 == 0) I1 = L.nc;
   const size_t n = (size_t)(I1 - I0) + (sm_out || !ghosts ? 0 : (size_t)glo + ghi);
   if (n)
-    hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
+    hipLaunchKernelGGL(nt ? k_amg_restrict<true> : k_amg_restrict<false>, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
                        sm_out, sm_de, I0, I1);
 }
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* cb, float* cx,
@@ -2672,10 +2675,10 @@ void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b
   else
     hipLaunchKernelGGL(k_amg_resrestrict<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
 }
-void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1) {
+void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1, bool nt) {
   if (f1 == 0) f1 = L.n;
   if (f1 > f0)
-    hipLaunchKernelGGL(k_amg_prolong, dim3(grid_for((f1 - f0 + 3) / 4)), dim3(kBlock), 0, s, L, x, xc, f0, f1);
+    hipLaunchKernelGGL(nt ? k_amg_prolong<true> : k_amg_prolong<false>, dim3(grid_for((f1 - f0 + 3) / 4)), dim3(kBlock), 0, s, L, x, xc, f0, f1);
 }
 void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_bytes, hipStream_t s) {
   if (lds_bytes == 0) {

@@ -353,7 +353,7 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
                          uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s,
                          float* sm_out = nullptr, const float* sm_de = nullptr, uint32_t I0 = 0,
-                         uint32_t I1 = 0, bool ghosts = true);
+                         uint32_t I1 = 0, bool ghosts = true, bool nt = false);
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).
@@ -373,7 +373,7 @@ void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, c
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* coarse_b, float* coarse_x,
                             float* sm_out, const float* sm_de, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,
-                        uint32_t f1 = 0);
+                        uint32_t f1 = 0, bool nt = false);
 // Sets the tail kernels' dynamic-LDS attribute on `device` (once per device,
 // thread-safe; throws on failure) and returns their LDS budget there:
 // min(kTailLdsMax, the device's opt-in per-block LDS).  Call with `device` current.

@@ -316,7 +316,8 @@ struct Solver {
   // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
   // 1 post-smoother of the split levels, 2 level-0 AMG residual, 4 Schur
   // prediction, 8 SpMV, 16 pre-smoother, 32 Schur correction, 64 the face-slot
-  // geometry of prepare / assemble.  Same bits either way.
+  // geometry of prepare / assemble, 128 the restriction / prolongation maps of
+  // the split levels.  Same bits either way.
   unsigned nt_mask = 0;
   // an in-process group step failed on some rank: the ranks stopped at
   // different points of the step (ring rotation, time, FGMRES state), so the
