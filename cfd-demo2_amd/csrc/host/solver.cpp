@@ -1354,7 +1354,7 @@ void Solver::v_cycle() {
     if (Lv.dist && !C.dist) {  // into the first replicated level: own slice, all-gather
       std::vector<size_t> off(R + 1);
       for (int q = 0; q <= R; ++q) off[q] = C.part[q] * sizeof(float);
-      timed_gather(kCommRepGather, off[R] - off[rk + 1] + off[rk], [&] { comm->allgatherv_inplace(C.b, off, stream); });
+      timed_gather(kCommRepGather, off[rk + 1] - off[rk], [&] { comm->allgatherv_inplace(C.b, off, stream); });
     }
   }
   if (tf < L && tf == tail_blob_first) {

@@ -318,7 +318,7 @@ struct Solver {
   // prediction, 8 SpMV, 16 pre-smoother, 32 Schur correction, 64 the face-slot
   // geometry of prepare / assemble, 128 the restriction / prolongation maps of
   // the split levels.  Same bits either way.
-  unsigned nt_mask = 0;
+  unsigned nt_mask = 15;  // same-box A/B, profiles/r04/ab_nt_c2.txt
   // an in-process group step failed on some rank: the ranks stopped at
   // different points of the step (ring rotation, time, FGMRES state), so the
   // group refuses to step until its state is restored on every rank
