@@ -329,14 +329,13 @@ constexpr int kRedFinalThreads = CFD_RED_FINAL_THREADS;
 // ---------------------------------------------------------------------------
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
 // Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
-template <bool NT>
 __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
   const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
   const FaceSlots fs = a.fs;
-  const float vol = ldx<NT>(a.vol + i);
+  const float vol = a.vol[i];
   float diag_coeff = 0.0f;
   float time_coeff = vol * c.density / c.dt;
   if (c.time_scheme == 1u) {
@@ -349,15 +348,15 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
   const float dpc = a.st.dp[i];
   const float2 gpc = a.st.gp[i];
   float gpx = 0.0f, gpy = 0.0f, gux = 0.0f, guy = 0.0f, gvx = 0.0f, gvy = 0.0f;
-  const uint32_t nf = ldx<NT>(fs.nface + i);
+  const uint32_t nf = fs.nface[i];
   for (uint32_t k = 0; k < nf; ++k) {
     const size_t e = (size_t)k * N + i;
-    const uint32_t meta = ldx<NT>(fs.meta + e);
-    const int32_t other = ldx<NT>(fs.other + e);
+    const uint32_t meta = fs.meta[e];
+    const int32_t other = fs.other[e];
     const uint32_t bt = meta & kMetaBtypeMask;
     const bool own = (meta & kMetaOwner) != 0;
-    const float area = ldx<NT>(fs.area + e);
-    const float nx = ldx<NT>(fs.nx + e), ny = ldx<NT>(fs.ny + e);  // oriented out of this cell
+    const float area = fs.area[e];
+    const float nx = fs.nx[e], ny = fs.ny[e];  // oriented out of this cell
     // stored face normal, then prepare's geometric re-orientation (wgsl:122-130)
     const float Nx = own ? nx : -nx, Ny = own ? ny : -ny;
     const bool flip = (meta & kMetaFluxFlip) != 0;
@@ -376,13 +375,13 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
       const float pow_ = own ? pc : p_oth, png = own ? p_oth : pc;
       const float dpow = own ? dpc : dp_oth, dpng = own ? dp_oth : dpc;
       const float2 gpow = own ? gpc : gp_oth, gpng = own ? gp_oth : gpc;
-      const float lambda = ldx<NT>(fs.lam_f + e);
+      const float lambda = fs.lam_f[e];
       const float ufx = lambda * uow.x + (1.0f - lambda) * ung.x;
       const float ufy = lambda * uow.y + (1.0f - lambda) * ung.y;
       const float dp_face = lambda * dpow + (1.0f - lambda) * dpng;
       const float gfx = lambda * gpow.x + (1.0f - lambda) * gpng.x;
       const float gfy = lambda * gpow.y + (1.0f - lambda) * gpng.y;
-      const float dist = ldx<NT>(fs.dist_a + e);
+      const float dist = fs.dist_a[e];
       const float grad_p_n = gfx * nfx + gfy * nfy;
       const float p_grad_f = (png - pow_) / dist;
       const float rc_term = dp_face * area * (grad_p_n - p_grad_f);
@@ -399,7 +398,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
     }
     const float flux_out = own ? flux : -flux;
     a.flux_s[e] = flux_out;
-    const float diff_coeff = c.viscosity * area / ldx<NT>(fs.dist_e + e);
+    const float diff_coeff = c.viscosity * area / fs.dist_e[e];
     const float conv_diag = flux_out > 0.0f ? flux_out : 0.0f;
     if (other != kNoCell) {
       diag_coeff += diff_coeff + conv_diag;
@@ -411,7 +410,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
     }
     float vfp, vfu, vfv;
     if (other != kNoCell) {
-      const float lp = ldx<NT>(fs.lam_s + e);
+      const float lp = fs.lam_s[e];
       vfp = lp * pc + (1.0f - lp) * po_other;
       if ((meta & kMetaDegen) == 0) {
         vfu = lp * uc.x + (1.0f - lp) * uo.x;
@@ -448,14 +447,13 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
 }
 
 // coupled_assembly_merged.wgsl:70-463
-template <bool NT>
 __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
   const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
   const FaceSlots fs = a.fs;
-  const float vol = ldx<NT>(a.vol + i);
+  const float vol = a.vol[i];
   float diag_uv = 0.0f;  // diag_u == diag_v (identical update sequence)
   float sdup = 0.0f, sdvp = 0.0f, sdpu = 0.0f, sdpv = 0.0f, sdpp = 0.0f;
   float rhs_u = 0.0f, rhs_v = 0.0f, rhs_p = 0.0f, sdiag = 0.0f;
@@ -477,16 +475,16 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
   rhs_v += rtv;
   const float dpc = a.st.dp[i];
   const float2 uc = a.st.u[i];
-  const uint32_t nf = ldx<NT>(fs.nface + i);
+  const uint32_t nf = fs.nface[i];
   for (uint32_t k = 0; k < nf; ++k) {
     const size_t e = (size_t)k * N + i;
-    const uint32_t meta = ldx<NT>(fs.meta + e);
-    const int32_t other = ldx<NT>(fs.other + e);
+    const uint32_t meta = fs.meta[e];
+    const int32_t other = fs.other[e];
     const uint32_t bt = meta & kMetaBtypeMask;
-    const float area = ldx<NT>(fs.area + e);
-    const float nx = ldx<NT>(fs.nx + e), ny = ldx<NT>(fs.ny + e);
+    const float area = fs.area[e];
+    const float nx = fs.nx[e], ny = fs.ny[e];
     const float flux = a.flux_s[e];
-    const float dist = ldx<NT>(fs.dist_a + e);
+    const float dist = fs.dist_a[e];
     const float diff_coeff = c.viscosity * area / dist;
     const float conv_diag = flux > 0.0f ? flux : 0.0f;
     const float conv_off = flux > 0.0f ? 0.0f : flux;
@@ -506,25 +504,25 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
         if (c.scheme == 1u) {
           if (flux > 0.0f) {
             const float2 gu = a.grad_u[i], gv = a.grad_v[i];
-            const float rx = ldx<NT>(fs.rx + e), ry = ldx<NT>(fs.ry + e);
+            const float rx = fs.rx[e], ry = fs.ry[e];
             ph_u = uc.x + (gu.x * rx + gu.y * ry);
             ph_v = uc.y + (gv.x * rx + gv.y * ry);
           } else {
             const float2 gu = a.grad_u[other], gv = a.grad_v[other];
-            const float rx = ldx<NT>(fs.rox + e), ry = ldx<NT>(fs.roy + e);
+            const float rx = fs.rox[e], ry = fs.roy[e];
             ph_u = uo.x + (gu.x * rx + gu.y * ry);
             ph_v = uo.y + (gv.x * rx + gv.y * ry);
           }
         } else if (c.scheme == 2u) {
           if (flux > 0.0f) {
             const float2 gu = a.grad_u[i], gv = a.grad_v[i];
-            const float dx = ldx<NT>(fs.dvx + e), dy = ldx<NT>(fs.dvy + e);
+            const float dx = fs.dvx[e], dy = fs.dvy[e];
             const float gtu = gu.x * dx + gu.y * dy, gtv = gv.x * dx + gv.y * dy;
             ph_u = 0.625f * uc.x + 0.375f * uo.x + 0.125f * gtu;
             ph_v = 0.625f * uc.y + 0.375f * uo.y + 0.125f * gtv;
           } else {
             const float2 gu = a.grad_u[other], gv = a.grad_v[other];
-            const float dx = -ldx<NT>(fs.dvx + e), dy = -ldx<NT>(fs.dvy + e);  // center - other_center
+            const float dx = -fs.dvx[e], dy = -fs.dvy[e];  // center - other_center
             const float gtu = gu.x * dx + gu.y * dy, gtv = gv.x * dx + gv.y * dy;
             ph_u = 0.625f * uo.x + 0.375f * uc.x + 0.125f * gtu;
             ph_v = 0.625f * uo.y + 0.375f * uc.y + 0.125f * gtv;
@@ -533,7 +531,7 @@ __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
         rhs_u -= flux * (ph_u - pu_u);
         rhs_v -= flux * (ph_v - pu_v);
       }
-      const float lambda = ldx<NT>(fs.lam_s + e);
+      const float lambda = fs.lam_s[e];
       const float oml = 1.0f - lambda;
       const float pgx = area * nx, pgy = area * ny;
       sdup += lambda * pgx;
@@ -1429,7 +1427,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
   if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
 }
-template <bool D16, int U, bool REG = false, bool NT = false>  // REG: see spmv2_group
+template <bool D16, int U, bool REG = false>  // REG: see spmv2_group
 __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const float* __restrict__ p_sol, uint32_t i0,
                                                uint32_t r0, uint32_t rmax, const uint32_t lw[2], float cu[2],
                                                float cv[2]) {
@@ -1439,12 +1437,12 @@ __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const flo
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    g[u] = ldv<NT, float4>(A.cval_g + off);
+    g[u] = *reinterpret_cast<const float4*>(A.cval_g + off);
     if constexpr (REG) {
       c[u][0] = (int)i0 + A.tmode[u];
       c[u][1] = c[u][0] + 1;
     } else {
-      ccols2<D16, NT>(A, off, i0, c[u]);
+      ccols2<D16>(A, off, i0, c[u]);
     }
   }
 #pragma unroll
@@ -1465,7 +1463,7 @@ __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const flo
       cv[k] += (k ? g[u].w : g[u].y) * pj[u][k];
     }
 }
-template <bool D16, bool NT>
+template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, const float* __restrict__ w_in,
                                                              const float* __restrict__ binv, int jv,
                                                              const float* __restrict__ p_sol,
@@ -1474,22 +1472,22 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
   constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
   uint32_t i0;
   if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
-  const ushort2 lg = ldv<NT, ushort2>(A.lg + i0);
+  const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
   // the row pair's own operands issued with the header (no round trip after the slots)
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;
   const f4u wa = ld4u(wb);
   const f2u wc = ld2u(wb + 4);
-  const float2 du = ldv<NT, float2>(dinv_uv + i0);
+  const float2 du = *reinterpret_cast<const float2*>(dinv_uv + i0);
   const float2 ps = *reinterpret_cast<const float2*>(p_sol + i0);
   const uint32_t lw[2] = {lg.x, lg.y};
   const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
   float cu[2] = {0.0f, 0.0f}, cv[2] = {0.0f, 0.0f};
   if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))  // ws <= U1: the only group
-    correct2_group<D16, U1, true, NT>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
+    correct2_group<D16, U1, true>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
   else
-    correct2_group<D16, U1, false, NT>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
-  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U, false, NT>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
+    correct2_group<D16, U1>(A, p_sol, i0, 0, (uint32_t)A.ws - 1u, lw, cu, cv);
+  for (uint32_t r0 = U1; r0 < maxlen; r0 += U) correct2_group<D16, U>(A, p_sol, i0, r0, maxlen - 1u, lw, cu, cv);
   const float wo[6] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y};
   const float dk[2] = {du.x, du.y}, pk[2] = {ps.x, ps.y};
   float o[6];
@@ -1874,12 +1872,11 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const
 }
 
 // coarse value I of the restriction: sum_{f in R row I, ascending} 1.0 * r[f]
-template <bool NT = false>
 __device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float* __restrict__ r, uint32_t I) {
   float sum = 0.0f;
   if (L.r_m4) {
     // the first 4 members in one 16-byte load, then their values
-    const int4 m = ldx<NT>(L.r_m4 + I);
+    const int4 m = L.r_m4[I];
     const bool over = m.w < -1;  // more than 4 members: member 3 stored as -2 - f
     const int f[4] = {m.x, m.y, m.z, over ? -2 - m.w : m.w};
     float v[4];
@@ -1913,7 +1910,6 @@ __device__ __forceinline__ float restrict_sum(const AmgLevelDev& L, const float*
 // restriction part: coarse_b[I] = sum_{f in R row I, ascending} 1.0 * r[f];
 // also clears the coarse solution (amg.rs:721-725 `clear`, fused), including
 // its ghost entries [-glo, 0) and [stride_c, stride_c + ghi) on a distributed level
-template <bool NT>
 __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const float* __restrict__ r,
                                                          float* __restrict__ cb,
                                                          float* __restrict__ cx, uint32_t stride_c,
@@ -1925,7 +1921,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_restrict(AmgLevelDev L, const fl
   if (I < I1) {
     // the coarse diagonal loaded with the members (no round trip after the sum)
     const float dec = sm_out ? sm_de[I] : 1.0f;
-    const float sum = restrict_sum<NT>(L, r, I);
+    const float sum = restrict_sum(L, r, I);
     cb[I] = sum;
     if (sm_out)  // the coarse level's zero-x pre-smoother fused (k_amg_smooth_zero)
       sm_out[I] = wmix(0.0f, (sum - 0.0f) / dec, 0.8f);
@@ -2499,11 +2495,11 @@ __global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint
 }  // namespace
 
 // ------------------------------- launchers ----------------------------------
-void launch_prepare(const PrepareArgs& a, hipStream_t s, bool nt) {
-  if (a.N) hipLaunchKernelGGL(nt ? k_prepare<true> : k_prepare<false>, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
+void launch_prepare(const PrepareArgs& a, hipStream_t s) {
+  if (a.N) hipLaunchKernelGGL(k_prepare, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
 }
-void launch_assemble(const AssembleArgs& a, hipStream_t s, bool nt) {
-  if (a.N) hipLaunchKernelGGL(nt ? k_assemble<true> : k_assemble<false>, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
+void launch_assemble(const AssembleArgs& a, hipStream_t s) {
+  if (a.N) hipLaunchKernelGGL(k_assemble, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
 }
 void launch_update_fields(uint32_t N, float au, float ap, const float* x, float2* u, float* p,
                           uint32_t* blockmax, uint32_t* maxbits, uint32_t* host_out, hipStream_t s) {
@@ -2605,12 +2601,13 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
   return false;
 }
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
-                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s, bool nt) {
+                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
   const unsigned nb = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
-  auto fn = A.use16 ? (nt ? k_precond_correct2<true, true> : k_precond_correct2<true, false>)
-                    : (nt ? k_precond_correct2<false, true> : k_precond_correct2<false, false>);
-  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+  if (A.use16)
+    hipLaunchKernelGGL(k_precond_correct2<true>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
+  else
+    hipLaunchKernelGGL(k_precond_correct2<false>, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, p_sol, dinv_uv, z);
 }
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1, hipStream_t s) {
   if (k > 64 || m1 > 64) throw std::invalid_argument("solve_triangular: basis larger than 64");
@@ -2659,11 +2656,11 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,
                          uint32_t glo, uint32_t ghi, hipStream_t s, float* sm_out, const float* sm_de, uint32_t I0,
-                         uint32_t I1, bool ghosts, bool nt) {
+                         uint32_t I1, bool ghosts) {
   if (I1 == 0) I1 = L.nc;
   const size_t n = (size_t)(I1 - I0) + (sm_out || !ghosts ? 0 : (size_t)glo + ghi);
   if (n)
-    hipLaunchKernelGGL(nt ? k_amg_restrict<true> : k_amg_restrict<false>, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
+    hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
                        sm_out, sm_de, I0, I1);
 }
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* cb, float* cx,

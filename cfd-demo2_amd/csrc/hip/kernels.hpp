@@ -275,9 +275,8 @@ struct TailBlobLevel {
 };
 
 // ---------------- launch wrappers (kernels.hip) ----------------
-// nt: the static face-slot geometry read with the nontemporal policy
-void launch_prepare(const PrepareArgs& a, hipStream_t s, bool nt = false);
-void launch_assemble(const AssembleArgs& a, hipStream_t s, bool nt = false);
+void launch_prepare(const PrepareArgs& a, hipStream_t s);
+void launch_assemble(const AssembleArgs& a, hipStream_t s);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 // (and to host_out[0..1], a device view of pinned host memory, when non-null)
 void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float* x, float2* u,
@@ -326,7 +325,7 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
                                  const float* sval, const float* dinv_p, const float* temp_p, float* p_sol,
                                  float* temp, uint32_t iters, hipStream_t s);
 void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
-                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s, bool nt = false);
+                            const float* p_sol, const float* dinv_uv, float* z, hipStream_t s);
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,
                              hipStream_t s);
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
@@ -353,7 +352,7 @@ void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, f
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* coarse_b, float* coarse_x,
                          uint32_t stride_c, uint32_t glo, uint32_t ghi, hipStream_t s,
                          float* sm_out = nullptr, const float* sm_de = nullptr, uint32_t I0 = 0,
-                         uint32_t I1 = 0, bool ghosts = true, bool nt = false);
+                         uint32_t I1 = 0, bool ghosts = true);
 // V-cycle restricted to levels [first, nlev) of `tail` (device array), one workgroup:
 // pre-smooth / residual / restrict+clear down, 10 coarsest sweeps, prolong / post-smooth up.
 // Every level's x ends in tail[l].x (even sweep counts).

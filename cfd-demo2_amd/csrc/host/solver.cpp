@@ -505,7 +505,7 @@ void Solver::prepare() {
   a.flux_s = flux_s;
   a.grad_u = grad_u;
   a.grad_v = grad_v;
-  launch_prepare(a, stream, nt(64));
+  launch_prepare(a, stream);
   check_launch("prepare");
   // commit d_p / grad_p (snapshot semantics): swap the scratch into the slot
   std::swap(S().dp, dp_scratch);
@@ -536,7 +536,7 @@ void Solver::assemble() {
   a.rhs = rhs;
   a.dinv_uv = dinv_uv;
   a.dinv_p = dinv_p;
-  launch_assemble(a, stream, nt(64));
+  launch_assemble(a, stream);
   check_launch("assemble");
   if (dist()) halo(cell_plan, {{dinv_uv, 1}});  // the Schur prediction reads neighbours' D_u^-1
 }
@@ -1330,7 +1330,7 @@ void Solver::v_cycle() {
       launch_amg_resrestrict(Lv.dev, Lv.x, Lv.b, C.b, C.x, smo, C.dev.de, stream);
     } else if (!Lv.dist) {
       res(i);
-      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream, smo, C.dev.de, 0, 0, true, nt(128));
+      launch_amg_restrict(Lv.dev, Lv.r, C.b, C.x, 0, 0, 0, stream, smo, C.dev.de);
     } else {
       res(i);
       // the restriction sums members owned by the next ranks too (their residuals
@@ -1345,11 +1345,9 @@ void Solver::v_cycle() {
       const uint32_t split = Lv.dev.n >= overlap_min_rows ? Lv.rc_hi : 0u;  // as overlapped()
       const CommScope cs(this, amg_cat(i));
       halo_begin(Lv.plan, {{Lv.r, 1}});
-      if (split > 0)
-        launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false, nt(128));
+      if (split > 0) launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false);
       halo_end();
-      launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, split, Lv.dev.nc, true,
-                          nt(128));
+      launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, split, Lv.dev.nc, true);
     }
     if (Lv.dist && !C.dist) {  // into the first replicated level: own slice, all-gather
       std::vector<size_t> off(R + 1);
@@ -1375,9 +1373,9 @@ void Solver::v_cycle() {
       const uint32_t split = F.dev.n >= overlap_min_rows ? F.pf_lo : F.dev.n;  // as overlapped()
       const CommScope cs(this, amg_cat(ii + 1));
       halo_begin(levels[ii + 1].plan, {{levels[ii + 1].x, 1}});
-      if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n, nt(128));
+      if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n, nt(32));
       halo_end();
-      if (split > 0) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, split, nt(128));
+      if (split > 0) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, split, nt(32));
     } else if (fused_prolong(ii)) {
       // the prolongation applied inside the post-smoother's reads (x stays un-prolonged)
       AmgGpuLevel& F = levels[ii];
@@ -1385,7 +1383,7 @@ void Solver::v_cycle() {
       std::swap(F.x, F.xt);
       continue;
     } else {
-      launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream, 0, 0, nt(128));
+      launch_amg_prolong(levels[ii].dev, levels[ii].x, levels[ii + 1].x, stream, 0, 0, nt(32));
     }
     sm(ii, false, true);
   }
@@ -1453,7 +1451,7 @@ void Solver::precondition(int j, float* z) {
     Ar.r1 = b;
     Ar.r2 = a2;
     Ar.r3 = b2;
-    launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream, nt(32));
+    launch_precond_correct(Ar, v, binv, j, ps, dinv_uv, z, stream);
   });
 }
 

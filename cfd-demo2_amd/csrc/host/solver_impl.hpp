@@ -315,10 +315,12 @@ struct Solver {
   // nontemporal loads of the matrix streams (kernels.hip ldx), per kernel, for
   // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
   // 1 post-smoother of the split levels, 2 level-0 AMG residual, 4 Schur
-  // prediction, 8 SpMV, 16 pre-smoother, 32 Schur correction, 64 the face-slot
-  // geometry of prepare / assemble, 128 the restriction / prolongation maps of
-  // the split levels.  Same bits either way.
-  unsigned nt_mask = 15;  // same-box A/B, profiles/r04/ab_nt_c2.txt
+  // prediction, 8 SpMV, 16 pre-smoother, 32 the prolongation map of the split
+  // levels.  Same bits either way.  Tried and not kept:
+  // the Schur correction (its lines are the SpMV's Infinity-Cache hits),
+  // prepare / assemble (assemble re-reads prepare's face slots), the
+  // restriction maps.
+  unsigned nt_mask = 47;  // same-box A/B, profiles/r04/ab_nt_c2.txt, ab_nt2_c2.txt
   // an in-process group step failed on some rank: the ranks stopped at
   // different points of the step (ring rotation, time, FGMRES state), so the
   // group refuses to step until its state is restored on every rank

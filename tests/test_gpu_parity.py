@@ -511,8 +511,8 @@ VARIANTS = [
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
     {"CFD_AMG_FUSED_PROLONG": "off"},                 # separate prolongation + post-smoother launches
     {"CFD_AMG_FUSED_PROLONG": "0", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused, every level, predicated loads
-    {"CFD_NT": "255", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG": "off"},  # nontemporal loads everywhere
-    {"CFD_NT": "255", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR": "0"},             # ... with predicated slot loads
+    {"CFD_NT": "63", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG": "off"},  # nontemporal loads everywhere
+    {"CFD_NT": "63", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR": "0"},             # ... with predicated slot loads
 ]
 
 
