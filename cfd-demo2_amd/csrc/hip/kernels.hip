@@ -714,13 +714,7 @@ __device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const 
     const size_t c = cell_q(q);
     if (FULL || c < N) {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) {
-#if CFD_AB_CGS_ST  // temporary A/B (round 4): default-policy stores of the new basis vector
-        p[3 * c + e] = v[q][e];
-#else
-        __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
-#endif
-      }
+      for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
     }
   }
 }
