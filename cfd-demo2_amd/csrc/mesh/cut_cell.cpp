@@ -76,10 +76,15 @@ namespace {
 // ---------------------------------------------------------------------------
 // Open-addressing hash maps (the reference uses AHashMap; only lookups/inserts
 // are observable, never iteration order, so any exact map is equivalent).
+// Open-addressing hash map (u64, u64) -> u32 with linear probing.  One
+// 24-byte slot per entry (key pair, value, in-use flag) so a probe touches one
+// cache line, not four separate arrays.
 struct PairMap {
-  std::vector<uint64_t> k0, k1;
-  std::vector<uint32_t> val;
-  std::vector<uint8_t> used;
+  struct Slot {
+    uint64_t a, b;
+    uint32_t v, used;
+  };
+  std::vector<Slot> slots;
   size_t mask = 0, count = 0;
   explicit PairMap(size_t expect) { rehash(std::max<size_t>(64, expect * 2)); }
   static uint64_t mix(uint64_t a, uint64_t b) {
@@ -92,23 +97,18 @@ struct PairMap {
   void rehash(size_t cap) {
     size_t c = 1;
     while (c < cap) c <<= 1;
-    std::vector<uint64_t> o0 = std::move(k0), o1 = std::move(k1);
-    std::vector<uint32_t> ov = std::move(val);
-    std::vector<uint8_t> ou = std::move(used);
-    k0.assign(c, 0);
-    k1.assign(c, 0);
-    val.assign(c, 0);
-    used.assign(c, 0);
+    std::vector<Slot> old = std::move(slots);
+    slots.assign(c, Slot{0, 0, 0, 0});
     mask = c - 1;
     count = 0;
-    for (size_t i = 0; i < ou.size(); ++i)
-      if (ou[i]) insert(o0[i], o1[i], ov[i]);
+    for (const Slot& o : old)
+      if (o.used) insert(o.a, o.b, o.v);
   }
   // Returns pointer to the value slot for key, or nullptr if absent.
   uint32_t* find(uint64_t a, uint64_t b) {
     size_t h = mix(a, b) & mask;
-    while (used[h]) {
-      if (k0[h] == a && k1[h] == b) return &val[h];
+    while (slots[h].used) {
+      if (slots[h].a == a && slots[h].b == b) return &slots[h].v;
       h = (h + 1) & mask;
     }
     return nullptr;
@@ -116,18 +116,51 @@ struct PairMap {
   void insert(uint64_t a, uint64_t b, uint32_t v) {
     if ((count + 1) * 2 > mask + 1) rehash((mask + 1) * 2);
     size_t h = mix(a, b) & mask;
-    while (used[h]) {
-      if (k0[h] == a && k1[h] == b) {
-        val[h] = v;
+    while (slots[h].used) {
+      if (slots[h].a == a && slots[h].b == b) {
+        slots[h].v = v;
         return;
       }
       h = (h + 1) & mask;
     }
-    used[h] = 1;
-    k0[h] = a;
-    k1[h] = b;
-    val[h] = v;
+    slots[h] = Slot{a, b, v, 1};
     ++count;
+  }
+};
+
+// Faces by their vertex pair (kmin, kmax), for the finalize pass: the first
+// two faces of each kmin live in a per-vertex array (vertices of a cell are
+// numbered close together, so these accesses stay in cache), further ones in
+// a PairMap.  Same answers as one PairMap over all pairs.
+struct EdgeMap {
+  std::vector<uint64_t> inl;  // [2 v + s] = kmax << 32 | face, or kEmpty
+  PairMap extra;
+  static constexpr uint64_t kEmpty = ~0ull;
+  explicit EdgeMap(size_t nverts) : inl(2 * nverts, kEmpty), extra(64) {}
+  bool find(uint32_t kmin, uint32_t kmax, uint32_t* face) {
+    for (int q = 0; q < 2; ++q) {
+      const uint64_t e = inl[2 * (size_t)kmin + q];
+      if (e == kEmpty) return false;  // slots fill in order: no later entry
+      if ((uint32_t)(e >> 32) == kmax) {
+        *face = (uint32_t)e;
+        return true;
+      }
+    }
+    if (uint32_t* f = extra.find(kmin, kmax)) {
+      *face = *f;
+      return true;
+    }
+    return false;
+  }
+  void insert(uint32_t kmin, uint32_t kmax, uint32_t face) {
+    for (int q = 0; q < 2; ++q) {
+      uint64_t& e = inl[2 * (size_t)kmin + q];
+      if (e == kEmpty) {
+        e = ((uint64_t)kmax << 32) | face;
+        return;
+      }
+    }
+    extra.insert(kmin, kmax, face);
   }
 };
 
@@ -215,15 +248,26 @@ Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double ma
     return idx;
   };
 
-  // 1. Base mesh (cut_cell.rs:47-207).  Serial: vertex numbering is order-dependent.
+  // 1. Base mesh (cut_cell.rs:47-207).  The vertex numbering is
+  // order-dependent, so it stays serial; the polygons themselves (quadtree
+  // refinement, SDF bisection, corner reconstruction: the bulk of the work)
+  // are built in parallel over a band of base columns, then inserted in the
+  // serial (column, row, leaf) order -- the same vertices, numbers and cells.
   cells.reserve(nx * ny);
-  std::vector<std::pair<Pt, Pt>> leaves;
   struct PV {
     Pt p;
     bool inter;
   };
-  std::vector<PV> poly, recon;
-  for (size_t i = 0; i < nx; ++i) {
+  // one base column: its cells' polygons, concatenated (sizes in `len`)
+  struct Column {
+    std::vector<PV> verts;
+    std::vector<uint32_t> len;
+  };
+  auto build_column = [&](size_t i, Column& col) {
+    col.verts.clear();
+    col.len.clear();
+    std::vector<std::pair<Pt, Pt>> leaves;
+    std::vector<PV> poly, recon;
     for (size_t j = 0; j < ny; ++j) {
       const double x0 = (double)i * max_cell_size;
       const double y0 = (double)j * max_cell_size;
@@ -297,11 +341,26 @@ Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double ma
               }
             }
           }
-          std::vector<uint32_t> idxs;
-          idxs.reserve(recon.size());
-          for (const auto& pv : recon) idxs.push_back(add_vertex(pv.p, pv.inter));
-          cells.push_back(std::move(idxs));
+          col.verts.insert(col.verts.end(), recon.begin(), recon.end());
+          col.len.push_back((uint32_t)recon.size());
         }
+      }
+    }
+  };
+  constexpr size_t kBand = 64;  // base columns built in parallel per band
+  std::vector<Column> band(kBand);
+  for (size_t i0 = 0; i0 < nx; i0 += kBand) {
+    const size_t nb = std::min(kBand, nx - i0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (long q = 0; q < (long)nb; ++q) build_column(i0 + (size_t)q, band[q]);
+    for (size_t q = 0; q < nb; ++q) {
+      const Column& col = band[q];
+      size_t at = 0;
+      for (const uint32_t n : col.len) {
+        std::vector<uint32_t> idxs;
+        idxs.reserve(n);
+        for (uint32_t k = 0; k < n; ++k, ++at) idxs.push_back(add_vertex(col.verts[at].p, col.verts[at].inter));
+        cells.push_back(std::move(idxs));
       }
     }
   }
@@ -403,7 +462,20 @@ Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double ma
   mesh.v_fixed = std::move(v_fixed);
   mesh.cell_face_offsets.push_back(0);
   mesh.cell_vertex_offsets.push_back(0);
-  PairMap face_map(cells.size() * 2 + 16);
+  {
+    size_t nvs = 0;
+    for (const auto& cv : cells) nvs += cv.size();
+    const size_t nfe = nvs / 2 + cells.size() + 16;  // ~2 faces per quad cell, boundary extra
+    for (auto* v : {&mesh.face_v1, &mesh.face_v2, &mesh.face_owner, &mesh.face_neighbor, &mesh.face_boundary})
+      v->reserve(nfe);
+    for (auto* v : {&mesh.face_nx, &mesh.face_ny, &mesh.face_area, &mesh.face_cx, &mesh.face_cy}) v->reserve(nfe);
+    for (auto* v : {&mesh.cell_cx, &mesh.cell_cy, &mesh.cell_vol}) v->reserve(cells.size());
+    mesh.cell_face_offsets.reserve(cells.size() + 1);
+    mesh.cell_vertex_offsets.reserve(cells.size() + 1);
+    mesh.cell_faces.reserve(nvs);
+    mesh.cell_vertices.reserve(nvs);
+  }
+  EdgeMap face_map(mesh.vx.size());
   for (const auto& cv : cells) {
     double ccx = 0.0, ccy = 0.0, area = 0.0;
     const size_t n = cv.size();
@@ -429,10 +501,11 @@ Mesh generate_cut_cell_mesh(const Geometry& geo, double min_cell_size, double ma
       const double elen = norm2(ex, ey);
       if (elen < 1e-9) continue;
       const uint32_t kmin = std::min(v1, v2), kmax = std::max(v1, v2);
-      if (uint32_t* fidx = face_map.find(kmin, kmax)) {
-        mesh.face_neighbor[*fidx] = cell_idx;
-        mesh.face_boundary[*fidx] = kNone;
-        mesh.cell_faces.push_back(*fidx);
+      uint32_t fidx;
+      if (face_map.find(kmin, kmax, &fidx)) {
+        mesh.face_neighbor[fidx] = cell_idx;
+        mesh.face_boundary[fidx] = kNone;
+        mesh.cell_faces.push_back(fidx);
       } else {
         const double fcx = (p1x + p2x) * 0.5, fcy = (p1y + p2y) * 0.5;
         // Vector2::new(edge.y, -edge.x).normalize()
