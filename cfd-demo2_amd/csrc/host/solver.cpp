@@ -88,6 +88,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
   if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
+  if (const char* re = std::getenv("CFD_AMG_REG")) amg_reg = std::atoi(re);
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -695,6 +696,43 @@ void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
   const double offd = ((double)G.nnz - n) / n;  // mean off-diagonals per row
   const bool regular = G.dev.w > 0 && offd >= 0.75 * G.dev.w;
   G.dev.full = fe ? (fe[0] == '1') : (li == 0 || regular || G.dev.n <= (1u << 19));
+  set_amg_regular(G, li);
+}
+
+// Level 0 of a face-stencil mesh: the row kernels derive lengths, diagonal
+// ranks and columns of regular waves (kernels.hip wave_regular).  The slot
+// pattern is the coupled matrix's modal one (Topology::tmode, the scalar
+// pattern with the diagonal in its slot) without the diagonal; the mask marks
+// the quads whose rows match it, so any pattern stays correct -- a mesh with
+// few regular rows only gains less.  CFD_AMG_REG=0 (at solver creation) disables it.
+void Solver::set_amg_regular(AmgGpuLevel& G, int li) {
+  G.dev.qmask = nullptr;
+  if (li != 0 || !amg_reg || !G.dev.full || !G.dev.use16 || G.dev.w < 1 || G.dev.w > kAmgRegMaxW)
+    return;
+  const std::vector<int32_t>& tm = topo.tmode;
+  if ((int)tm.size() != G.dev.w + 1 || std::count(tm.begin(), tm.end(), 0) != 1) return;
+  int r = 0;
+  for (int s = 0; s < (int)tm.size(); ++s) {
+    if (tm[s] == 0)
+      G.dev.tdr = s;
+    else
+      G.dev.tdelta[r++] = tm[s];
+  }
+  const uint32_t nwords = (G.dev.stride / 4 + 31) / 32;
+  uint32_t* m = arena.alloc<uint32_t>(nwords);
+  launch_amg_qmask(G.dev, m, stream);
+  CFD_HIP(hipGetLastError());
+  G.dev.qmask = m;
+  // regular waves of a one-range launch over [0, n) (the layout-true byte count)
+  std::vector<uint32_t> h(nwords);
+  CFD_HIP(hipMemcpyAsync(h.data(), m, nwords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  sync();
+  G.dev.qlane = amg_reg == 2 ? 1 : 0;
+  uint64_t rows = 0;
+  for (uint32_t w = 0; w < nwords; ++w)
+    rows += G.dev.qlane ? 4u * (uint32_t)__builtin_popcount(h[w])
+                        : ((w % 2 == 0 && w + 1 < nwords && h[w] == ~0u && h[w + 1] == ~0u) ? 256u : 0u);
+  G.reg_rows = rows;
 }
 
 // Host AMG setup (amg_setup.cpp): the assembled scalar matrix is downloaded,
@@ -1983,7 +2021,16 @@ double Solver::smoother_layout_bytes() const {
   if (levels.empty()) return 0.0;
   const AmgLevelDev& d = levels[0].dev;
   const double st = d.stride, n = d.n;
-  return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n;
+  return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n - reg_saving(0, false);
+}
+
+// Bytes the regular waves of level li do not move in one smoother (or, with
+// residual, residual) sweep: the length (and rank) byte and the column deltas
+// of each of their rows, less the mask words every wave reads (8 B per wave).
+double Solver::reg_saving(size_t li, bool residual) const {
+  const AmgLevelDev& d = levels[li].dev;
+  if (!d.qmask) return 0.0;
+  return (double)levels[li].reg_rows * ((residual ? 2.0 : 1.0) + 2.0 * d.w) - d.stride / 32.0;
 }
 
 // Layout-true bytes of one step under the fixed schedule: per kernel, the
@@ -2016,7 +2063,7 @@ double Solver::layout_step_bytes() const {
   for (int i = 0; i < L; ++i) {
     const AmgLevelDev& d = levels[i].dev;
     const double n = d.n, st = d.stride, img = row_image(d);
-    const double smooth = st + img + 16 * n;
+    const double smooth = st + img + 16 * n - reg_saving(i, false);
     if (i < down) {
       const double nc = levels[i + 1].dev.n;
       // pre-smoother (coarse: zero-x, elementwise; not launched when fused into
@@ -2026,7 +2073,7 @@ double Solver::layout_step_bytes() const {
       if (d.rr_agg && !levels[i].dist)
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
       else
-        vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
+        vc += (2 * st + img + 16 * n - reg_saving(i, true)) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
       if (fused_prolong(i))
         vc += smooth + 4 * n + 4 * nc;                                 // post-smoother reading x + P xc
       else
