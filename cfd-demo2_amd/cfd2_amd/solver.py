@@ -66,7 +66,6 @@ def _bind():
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
     L.cfd_debug_prepare_assemble.argtypes = [_vp, C.c_int32]
     L.cfd_debug_amg_info.argtypes = [_vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
-    L.cfd_debug_amg_regular.argtypes = [_vp, C.c_int32, C.POINTER(C.c_uint64)]
     u8p = C.POINTER(C.c_uint8)
     u32p = C.POINTER(C.c_uint32)
     L.cfd_dist_unique_id.argtypes = [u8p]
@@ -305,13 +304,6 @@ class GpuSolver:
             self._call("cfd_debug_amg_info", li, C.byref(path), C.byref(d))
             dig.append(int(d.value))
         return int(path.value), dig
-
-    def amg_regular_rows(self, level: int = 0) -> int:
-        """Rows of `level` in regular waves (lengths, ranks and columns derived
-        by the row kernels, not loaded); 0 when the level has none."""
-        n = C.c_uint64()
-        self._call("cfd_debug_amg_regular", level, C.byref(n))
-        return int(n.value)
 
     def step_algorithmic_bytes(self) -> float:
         return float(_ffi.lib().cfd_step_algorithmic_bytes(self._h))

@@ -116,20 +116,20 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // same data starts on the rows whose lines that kernel touched last, which may
 // still sit in the memory-side Infinity Cache (MALL, 256 MB, shared by all
 // XCDs).  Order only: every row's arithmetic is unchanged.
+// remap = false (kernel-uniform): blocks keep dispatch order (REV: reversed),
+// each XCD's blocks interleaved over the whole range -- faster for the Schur
+// kernels and the face sweeps on big meshes (see CoupledMatrix::schur_flat).
 template <bool REV = false>
-__device__ __forceinline__ uint32_t xcd_block() {
+__device__ __forceinline__ uint32_t xcd_block(bool remap = true) {
   const uint32_t b = blockIdx.x, nb = gridDim.x;
-#if defined(CFD_DBG_NOXCD)
-  if constexpr (REV) return nb - 1u - b;
-  return b;
-#endif
+  if (!remap) return REV ? nb - 1u - b : b;
   const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
   const uint32_t base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   if constexpr (REV) return base + ((xcd < r) ? q : q - 1u) - (b >> 3);
   return base + (b >> 3);
 }
 template <bool REV = false>
-__device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock + threadIdx.x; }
+__device__ __forceinline__ uint32_t row_id(bool remap = true) { return xcd_block<REV>(remap) * kBlock + threadIdx.x; }
 
 // Kernels that run top-down (xcd_block<true>) to reuse the Infinity Cache lines
 // of the kernel before them (build-time tunables, tools/ab_variants.py).  Same-box
@@ -153,8 +153,9 @@ constexpr bool kRevSmooth = true;     // k_amg_smooth: top-down
 // second range lets a distributed rank process both boundary strips of a
 // halo'd kernel in one launch); false: no rows for this thread.
 template <bool REV = false>
-__device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
-  const uint32_t t = row_id<REV>(), na = (r1 - r0 + 3) / 4;
+__device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0,
+                                          bool remap = true) {
+  const uint32_t t = row_id<REV>(remap), na = (r1 - r0 + 3) / 4;
   if (t < na) {
     i0 = r0 + 4 * t;
     return i0 < r1;
@@ -334,7 +335,7 @@ constexpr int kRedFinalThreads = CFD_RED_FINAL_THREADS;
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
 // Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
 __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
-  const uint32_t i = row_id();
+  const uint32_t i = row_id(!a.flat);
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -452,7 +453,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
 
 // coupled_assembly_merged.wgsl:70-463
 __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
-  const uint32_t i = row_id();
+  const uint32_t i = row_id(!a.flat);
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -885,8 +886,9 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
 // (102 instead of 196 VGPRs: 4 wavefronts per SIMD instead of 2), one 16-byte
 // load per slot array; same-box A/B at C2 (round 2): SpMV 225.8 -> 218.0 us.
 template <bool REV = false>
-__device__ __forceinline__ bool row_range2(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
-  const uint32_t t = row_id<REV>(), na = (r1 - r0 + 1) / 2;
+__device__ __forceinline__ bool row_range2(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0,
+                                           bool remap = true) {
+  const uint32_t t = row_id<REV>(remap), na = (r1 - r0 + 1) / 2;
   if (t < na) {
     i0 = r0 + 2 * t;
     return i0 < r1;
@@ -1409,7 +1411,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
                                                              float* p_sol, float* p_prev) {
   constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
   uint32_t i0;
-  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0, !A.schur_flat)) return;
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;
   const f4u wa = ld4u(wb);
@@ -1475,7 +1477,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
                                                              float* __restrict__ z) {
   constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
   uint32_t i0;
-  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0, !A.schur_flat)) return;
   const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
   // the row pair's own operands issued with the header (no round trip after the slots)
   const float sc = binv[jv];
@@ -1701,67 +1703,43 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
   }
 }
 
-// Regular waves (L.qmask, level 0 of a face-stencil mesh): every row of the
-// wave has len = w, drank = tdr and the columns row + tdelta[slot], so the
-// row lengths, diagonal ranks and column deltas (9 of the 41 bytes per row of
-// a quad-mesh smoother sweep) are not loaded, and since the columns are known
-// up front the slot values, the x gathers (one 16-byte load per slot: the 4
-// rows' columns are consecutive) and the row operands all issue at once --
-// one memory round trip instead of the chain lengths -> slots -> gathers.
-// The accumulation is the general path's, slot by slot.
-__device__ __forceinline__ bool wave_regular(const AmgLevelDev& L, uint32_t i0) {
-  const uint32_t q = i0 >> 2;
-  const bool on = (L.qmask[q >> 5] >> (q & 31u)) & 1u;
-  return L.qlane ? on : __all(on);
-}
-template <bool NT, bool PRO>
-__device__ __forceinline__ void regular_slots(const AmgLevelDev& L, const float* __restrict__ x, uint32_t i0,
-                                              float4 v[kAmgRegMaxW], float xg[kAmgRegMaxW][4],
-                                              const float* __restrict__ xc) {
-  [[maybe_unused]] i4u ag[kAmgRegMaxW];
+// smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8).
+// PRO (post-smoother of a single-GPU / replicated level): the prolongation
+// from the coarse level xc that precedes it (k_amg_prolong) is applied to
+// every x value as it is read, so x' = x + P xc is never stored -- the same
+// f32 operations per value, one launch and one pass over x / agg fewer.
+// smooth4: the 4 rows i0..i0+3
+// The row operands (b, x, diagonal) are loaded after the slot loop (loading
+// them with the row lengths was inside the noise, round 3); in the fused
+// post-smoother the row's own prolongation term (agg -> x_c) comes after the
+// slots as well (before them: +0.1 ... +0.5 us on every C1 level).
+template <bool D16, int MODE, bool PRO = false, bool NT = false>
+__device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __restrict__ x,
+                                          const float* __restrict__ b, uint32_t i0,
+                                          const float* __restrict__ xc = nullptr) {
+  const uchar4 ln = ldv<NT, uchar4>(L.len + i0);
+  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
+  float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  auto step = [&](uint32_t r0, uint32_t rmax) {
+    float4 v[kU];
+    float xg[kU][4];
+    gather_group<D16, MODE, true, PRO, NT>(L, x, i0, r0, rmax, ln, v, xg, xc);
 #pragma unroll
-  for (int r = 0; r < kAmgRegMaxW; ++r)
-    if (r < L.w) {
-#if defined(CFD_DBG_ALIGNED)
-      const float* c = x + (ptrdiff_t)i0 + (L.tdelta[r] & ~3);
-#else
-      const float* c = x + (ptrdiff_t)i0 + L.tdelta[r];
-#endif
-      v[r] = ldv<NT, float4>(L.val + (size_t)r * L.stride + i0);
-#if defined(CFD_DBG_NOGATHER)
-      const f4u q = f4u{1.0f, 1.0f, 1.0f, 1.0f};
-      (void)c;
-#else
-      const f4u q = ld4u(c);
-#endif
-      xg[r][0] = q.x;
-      xg[r][1] = q.y;
-      xg[r][2] = q.z;
-      xg[r][3] = q.w;
-      if constexpr (PRO) ag[r] = *reinterpret_cast<const i4u*>(L.agg + (ptrdiff_t)i0 + L.tdelta[r]);
-    }
-  if constexpr (PRO) {
-    float cv[kAmgRegMaxW][4];
+    for (int u = 0; u < kU; ++u)
 #pragma unroll
-    for (int r = 0; r < kAmgRegMaxW; ++r)
-      if (r < L.w) {
-        cv[r][0] = xc[ag[r].x];
-        cv[r][1] = xc[ag[r].y];
-        cv[r][2] = xc[ag[r].z];
-        cv[r][3] = xc[ag[r].w];
-      }
-#pragma unroll
-    for (int r = 0; r < kAmgRegMaxW; ++r)
-      if (r < L.w)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) xg[r][k] = prolonged(xg[r][k], cv[r][k]);
+      for (int k = 0; k < 4; ++k)
+        if (r0 + u < u4(ln, k)) sg[k] += f4(v[u], k) * xg[u][k];
+  };
+  if constexpr (MODE != 0) {
+    // first slot group peeled: its loads (clamped to the ELL width) do not wait for the lengths
+    step(0, (uint32_t)max(L.w, 1) - 1u);
+    for (uint32_t r0 = kU; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
+  } else {
+    for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
   }
-}
-
-// the smoother's row update from sigma (PRO: the row's own prolongation term first)
-template <bool PRO>
-__device__ __forceinline__ float4 smooth_rows(const AmgLevelDev& L, float4 xx, const float4 bb, const float4 dd,
-                                              const float sg[4], uint32_t i0, const float* __restrict__ xc) {
+  const float4 bb = ldv<NT, float4>(b + i0);
+  float4 xx = *reinterpret_cast<const float4*>(x + i0);
+  const float4 dd = ldv<NT, float4>(L.de + i0);
   if constexpr (PRO) {  // the row's own value, as k_amg_prolong (padding rows get + 0)
     float pc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const int4 ag = *reinterpret_cast<const int4*>(L.agg + i0);
@@ -1781,69 +1759,13 @@ __device__ __forceinline__ float4 smooth_rows(const AmgLevelDev& L, float4 xx, c
   o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
   return o;
 }
-
-// smooth_op (amg.wgsl:24-50) restated out-of-place: x_out = mix(x, (b - sigma)/diag, 0.8).
-// PRO (post-smoother of a single-GPU / replicated level): the prolongation
-// from the coarse level xc that precedes it (k_amg_prolong) is applied to
-// every x value as it is read, so x' = x + P xc is never stored -- the same
-// f32 operations per value, one launch and one pass over x / agg fewer.
-// smooth4: the 4 rows i0..i0+3
-// The row operands (b, x, diagonal) are loaded after the slot loop (loading
-// them with the row lengths was inside the noise, round 3); in the fused
-// post-smoother the row's own prolongation term (agg -> x_c) comes after the
-// slots as well (before them: +0.1 ... +0.5 us on every C1 level).
-template <bool D16, int MODE, bool PRO = false, bool NT = false, bool RW = false>
-__device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __restrict__ x,
-                                          const float* __restrict__ b, uint32_t i0,
-                                          const float* __restrict__ xc = nullptr) {
-  float sg[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if constexpr (RW) {  // (launched only for a level with L.qmask: D16, MODE 1)
-    if (wave_regular(L, i0)) {
-      float4 v[kAmgRegMaxW];
-      float xg[kAmgRegMaxW][4];
-      regular_slots<NT, PRO>(L, x, i0, v, xg, xc);
-      const float4 bb = ldv<NT, float4>(b + i0);
-      const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-      const float4 dd = ldv<NT, float4>(L.de + i0);
-#pragma unroll
-      for (int r = 0; r < kAmgRegMaxW; ++r)
-        if (r < L.w)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) sg[k] += f4(v[r], k) * xg[r][k];
-      return smooth_rows<PRO>(L, xx, bb, dd, sg, i0, xc);
-    }
-  }
-  const uchar4 ln = ldv<NT, uchar4>(L.len + i0);
-  const uint32_t maxlen = max(max(ln.x, ln.y), max(ln.z, ln.w));
-  auto step = [&](uint32_t r0, uint32_t rmax) {
-    float4 v[kU];
-    float xg[kU][4];
-    gather_group<D16, MODE, true, PRO, NT>(L, x, i0, r0, rmax, ln, v, xg, xc);
-#pragma unroll
-    for (int u = 0; u < kU; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (r0 + u < u4(ln, k)) sg[k] += f4(v[u], k) * xg[u][k];
-  };
-  if constexpr (MODE != 0) {
-    // first slot group peeled: its loads (clamped to the ELL width) do not wait for the lengths
-    step(0, (uint32_t)max(L.w, 1) - 1u);
-    for (uint32_t r0 = kU; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
-  } else {
-    for (uint32_t r0 = 0; r0 < maxlen; r0 += kU) step(r0, maxlen - 1u);
-  }
-  const float4 bb = ldv<NT, float4>(b + i0);
-  const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-  const float4 dd = ldv<NT, float4>(L.de + i0);
-  return smooth_rows<PRO>(L, xx, bb, dd, sg, i0, xc);
-}
-template <bool D16, int MODE, bool PRO = false, bool NT = false, bool RW = false>
+template <bool D16, int MODE, bool PRO = false, bool NT = false>
 __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
                                                        const float* __restrict__ b, float* __restrict__ x_out,
                                                        const float* __restrict__ xc) {
   uint32_t i0;
-  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0)) return;
-  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT, RW>(L, x, b, i0, xc);
+  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0, !L.flat)) return;
+  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(L, x, b, i0, xc);
 }
 
 // smooth_op on a level whose x is identically +0 (every coarse level's
@@ -1866,32 +1788,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth_zero(AmgLevelDev L, const
 
 // residual part of restrict_residual (amg.wgsl:80-111): r = b - A x over the full
 // row in column order, the diagonal inserted at its rank.
-template <bool D16, int MODE, bool NT = false, bool RW = false>
+template <bool D16, int MODE, bool NT = false>
 __device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* __restrict__ x,
                                             const float* __restrict__ b, uint32_t i0) {
-  if constexpr (RW) {
-    if (wave_regular(L, i0)) {  // the general path's order: the diagonal at its rank tdr
-      float4 v[kAmgRegMaxW];
-      float xg[kAmgRegMaxW][4];
-      regular_slots<NT, false>(L, x, i0, v, xg, nullptr);
-      const float4 xx = *reinterpret_cast<const float4*>(x + i0);
-      const float4 dv = ldv<NT, float4>(L.dv + i0);
-      const float4 bb = ldv<NT, float4>(b + i0);
-      float ax[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int r = 0; r < kAmgRegMaxW; ++r)
-        if (r < L.w)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (r == L.tdr) ax[k] += f4(dv, k) * f4(xx, k);
-            ax[k] += f4(v[r], k) * xg[r][k];
-          }
-      if (L.tdr >= L.w)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ax[k] += f4(dv, k) * f4(xx, k);
-      return make_float4(bb.x - ax[0], bb.y - ax[1], bb.z - ax[2], bb.w - ax[3]);
-    }
-  }
   const uchar4 ln = ldv<NT, uchar4>(L.len + i0);
   const uchar4 dr = ldv<NT, uchar4>(L.drank + i0);
   const float4 xx = *reinterpret_cast<const float4*>(x + i0);
@@ -1929,12 +1828,12 @@ __device__ __forceinline__ float4 residual4(const AmgLevelDev& L, const float* _
   o.w = bb.w - ax[3];
   return o;
 }
-template <bool D16, int MODE, bool NT = false, bool RW = false>
+template <bool D16, int MODE, bool NT = false>
 __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const float* __restrict__ x,
                                                          const float* __restrict__ b, float* __restrict__ rr) {
   uint32_t i0;
   if (!row_range<kRevResidual>(L.r0, L.r1, L.r2, L.r3, i0)) return;
-  *reinterpret_cast<float4*>(rr + i0) = residual4<D16, MODE, NT, RW>(L, x, b, i0);
+  *reinterpret_cast<float4*>(rr + i0) = residual4<D16, MODE, NT>(L, x, b, i0);
 }
 
 // relax_pressure (schur_precond.wgsl:52-90) on large meshes, 4 rows per thread
@@ -2737,46 +2636,19 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
                        hipEvent_t ev0, hipEvent_t ev1, bool nt) {
   if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
-  auto fn = L.qmask ? (nt ? k_amg_smooth<true, 1, false, true, true> : k_amg_smooth<true, 1, false, false, true>)
-           : nt     ? CFD_AMG_INSTANCE(k_amg_smooth, L, false, true)
-                    : CFD_AMG_INSTANCE(k_amg_smooth, L, false, false);
+  auto fn = nt ? CFD_AMG_INSTANCE(k_amg_smooth, L, false, true) : CFD_AMG_INSTANCE(k_amg_smooth, L, false, false);
   if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
     hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out, nullptr);
   else
     hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, nullptr);
-}
-// one thread per qmask word (32 quads): bit b set iff the 4 rows of quad
-// 32 w + b are real rows with len = w, drank = tdr and col16 = tdelta slot by
-// slot (setup, once per hierarchy)
-__global__ void __launch_bounds__(kBlock) k_amg_qmask(AmgLevelDev L, uint32_t* __restrict__ qmask, uint32_t nwords) {
-  const uint32_t wd = blockIdx.x * kBlock + threadIdx.x;
-  if (wd >= nwords) return;
-  uint32_t m = 0;
-  for (uint32_t bq = 0; bq < 32; ++bq) {
-    bool reg = true;
-    for (uint32_t k = 0; k < 4 && reg; ++k) {
-      const uint32_t i = (wd * 32 + bq) * 4 + k;
-      reg = i < L.n && L.len[i] == (uint32_t)L.w && L.drank[i] == (uint32_t)L.tdr;
-      for (int r = 0; r < kAmgRegMaxW && reg; ++r)
-        if (r < L.w) reg = L.col16[(size_t)r * L.stride + i] == L.tdelta[r];
-    }
-    if (reg) m |= 1u << bq;
-  }
-  qmask[wd] = m;
-}
-void launch_amg_qmask(const AmgLevelDev& L, uint32_t* qmask, hipStream_t s) {
-  if (!L.use16 || L.w < 1 || L.w > kAmgRegMaxW) throw std::invalid_argument("amg_qmask: level not eligible");
-  const uint32_t nwords = (L.stride / 4 + 31) / 32;
-  hipLaunchKernelGGL(k_amg_qmask, dim3(grid_for(nwords)), dim3(kBlock), 0, s, L, qmask, nwords);
 }
 void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b, float* x_out,
                                hipStream_t s) {
   if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
   if (!L.agg || !xc) throw std::invalid_argument("amg_smooth_prolong: level without a coarse level");
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
-  auto fn = L.qmask   ? k_amg_smooth<true, 1, true, false, true>
-           : L.use16 ? (L.full ? k_amg_smooth<true, 1, true> : k_amg_smooth<true, 0, true>)
-                     : (L.full ? k_amg_smooth<false, 1, true> : k_amg_smooth<false, 0, true>);
+  auto fn = L.use16 ? (L.full ? k_amg_smooth<true, 1, true> : k_amg_smooth<true, 0, true>)
+                    : (L.full ? k_amg_smooth<false, 1, true> : k_amg_smooth<false, 0, true>);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, xc);
 }
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
@@ -2785,9 +2657,7 @@ void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, 
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r, hipStream_t s, bool nt) {
   if (L.r1 <= L.r0 && L.r3 <= L.r2) return;
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
-  auto fn = L.qmask ? (nt ? k_amg_residual<true, 1, true, true> : k_amg_residual<true, 1, false, true>)
-           : nt     ? CFD_AMG_INSTANCE(k_amg_residual, L, true)
-                    : CFD_AMG_INSTANCE(k_amg_residual, L, false);
+  auto fn = nt ? CFD_AMG_INSTANCE(k_amg_residual, L, true) : CFD_AMG_INSTANCE(k_amg_residual, L, false);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, r);
 }
 void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float* cx, uint32_t stride_c,

@@ -129,6 +129,7 @@ struct StateView {
 
 struct PrepareArgs {
   uint32_t N;
+  int flat;               // rows in dispatch order (big meshes, see CoupledMatrix::schur_flat)
   cfd_constants c;
   FaceSlots fs;
   const float* vol;
@@ -142,6 +143,7 @@ struct PrepareArgs {
 
 struct AssembleArgs {
   uint32_t N;
+  int flat;               // rows in dispatch order (big meshes, see CoupledMatrix::schur_flat)
   uint32_t ld;             // scalar-row ELL slot stride
   cfd_constants c;
   FaceSlots fs;
@@ -187,6 +189,12 @@ struct CoupledMatrix {
   // loading them; set when ws <= kCoupledRegMaxWs (one peeled slot group)
   int reg;
   int tmode[8];
+  // 1: the Schur prediction / correction take their row pairs in block
+  // dispatch order instead of the XCD-contiguous remap (kernels.hip
+  // xcd_block): on big meshes their streams then run closer together in
+  // memory (C2 A/B, profiles/r04/ab_noxcd_c2.txt: predict 157.4 -> 146.1 us,
+  // correct 131.3 -> 123.9); at C1 the remap's L2 locality wins (15.7 vs 18.7)
+  int schur_flat;
 };
 constexpr uint32_t kLgUsedMask = 0x7Fu, kLgRegular = 0x80u;
 constexpr int kCoupledRegMaxWs = 5;
@@ -231,16 +239,10 @@ struct AmgLevelDev {
   // k_amg_resrestrict: aggregates per block (0: the level keeps the separate
   // residual + restriction kernels); every block's members fit kRRCap
   uint32_t rr_agg;
-  // regular quads (level 0 of a face-stencil mesh, kernels.hip k_amg_qmask):
-  // bit q of qmask[q / 32] = rows 4q..4q+3 all have len = w, drank = tdr and
-  // the columns row + tdelta[slot].  A wave whose 64 quads are all regular
-  // derives lengths, ranks and columns instead of loading them (null: none)
-  const uint32_t* qmask = nullptr;
-  int qlane = 0;  // 1: per quad instead (the wave's other quads take the general path)
-  int tdr = 0;
-  int tdelta[4] = {0, 0, 0, 0};
+  // k_amg_smooth: rows in block dispatch order (the level-0 pre-smoother after
+  // a dispatch-order Schur prediction, CoupledMatrix::schur_flat)
+  int flat = 0;
 };
-constexpr int kAmgRegMaxW = 4;     // widest level the regular-wave path handles
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
 // zeroed entries after every level's agg array: the fused prolongation reads
 // agg with 16-byte loads from any column (as the x gathers, whose vectors
@@ -343,8 +345,6 @@ void launch_update_x(float* x, const float* z, size_t stride, const float* y, in
 // nt: the level matrix, b and the diagonal read with the nontemporal policy
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,
                        hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, bool nt = false);
-// L.qmask (ceil(stride / 128) words) from L's len / drank / col16 and L.tdr / tdelta
-void launch_amg_qmask(const AmgLevelDev& L, uint32_t* qmask, hipStream_t s);
 // post-smoother with the prolongation fused: x_out = smooth(x + P xc), bit-identical
 // to launch_amg_prolong(L, x, xc) then launch_amg_smooth(L, x, b, x_out), but x is
 // only read (single-GPU / replicated levels: every column an owned row)

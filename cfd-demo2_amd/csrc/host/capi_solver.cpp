@@ -245,14 +245,6 @@ cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path,
     if (digest) *digest = s->s->amg_level_digest(level);
   });
 }
-cfd_status cfd_debug_amg_regular(const cfd_solver* s, int32_t level, uint64_t* regular_rows) {
-  CHECK_S(s);
-  if (!regular_rows) return set_error(CFD_ERR_INVALID, "null output");
-  return guard([&] {
-    const auto& L = s->s->levels;
-    *regular_rows = (level >= 0 && level < (int32_t)L.size() && L[level].dev.qmask) ? L[level].reg_rows : 0;
-  });
-}
 double cfd_smoother_layout_bytes(const cfd_solver* s) { return (s && s->s) ? s->s->smoother_layout_bytes() : 0.0; }
 double cfd_step_layout_bytes(const cfd_solver* s) { return (s && s->s) ? s->s->layout_step_bytes() : 0.0; }
 double cfd_step_algorithmic_bytes(const cfd_solver* s) {

@@ -87,8 +87,9 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
+  if (const char* fr = std::getenv("CFD_FLAT_ROWS")) flat_rows = (uint32_t)std::strtoul(fr, nullptr, 0);
+  if (const char* fp = std::getenv("CFD_FLAT_PRE")) pre_flat = fp[0] != '0';
   if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
-  if (const char* re = std::getenv("CFD_AMG_REG")) amg_reg = std::atoi(re);
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -249,6 +250,7 @@ CoupledMatrix Solver::cmat() const {
   A.cdiag2 = cdiag2;
   A.reg = coupled_reg && !topo.tmode.empty() && topo.ws <= kCoupledRegMaxWs ? 1 : 0;
   for (int r = 0; r < 8; ++r) A.tmode[r] = r < (int)topo.tmode.size() ? topo.tmode[r] : 0;
+  A.schur_flat = flat_order() ? 1 : 0;
   return A;
 }
 
@@ -497,6 +499,7 @@ void Solver::rotate() {  // coupled_solver.rs:43-71
 void Solver::prepare() {
   PrepareArgs a;
   a.N = N;
+  a.flat = flat_order() ? 1 : 0;
   a.c = constants;
   a.fs = fs;
   a.vol = d_vol;
@@ -518,6 +521,7 @@ void Solver::prepare() {
 void Solver::assemble() {
   AssembleArgs a;
   a.N = N;
+  a.flat = flat_order() ? 1 : 0;
   a.ld = topo.ld;
   a.c = constants;
   a.fs = fs;
@@ -696,43 +700,6 @@ void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
   const double offd = ((double)G.nnz - n) / n;  // mean off-diagonals per row
   const bool regular = G.dev.w > 0 && offd >= 0.75 * G.dev.w;
   G.dev.full = fe ? (fe[0] == '1') : (li == 0 || regular || G.dev.n <= (1u << 19));
-  set_amg_regular(G, li);
-}
-
-// Level 0 of a face-stencil mesh: the row kernels derive lengths, diagonal
-// ranks and columns of regular waves (kernels.hip wave_regular).  The slot
-// pattern is the coupled matrix's modal one (Topology::tmode, the scalar
-// pattern with the diagonal in its slot) without the diagonal; the mask marks
-// the quads whose rows match it, so any pattern stays correct -- a mesh with
-// few regular rows only gains less.  CFD_AMG_REG=0 (at solver creation) disables it.
-void Solver::set_amg_regular(AmgGpuLevel& G, int li) {
-  G.dev.qmask = nullptr;
-  if (li != 0 || !amg_reg || !G.dev.full || !G.dev.use16 || G.dev.w < 1 || G.dev.w > kAmgRegMaxW)
-    return;
-  const std::vector<int32_t>& tm = topo.tmode;
-  if ((int)tm.size() != G.dev.w + 1 || std::count(tm.begin(), tm.end(), 0) != 1) return;
-  int r = 0;
-  for (int s = 0; s < (int)tm.size(); ++s) {
-    if (tm[s] == 0)
-      G.dev.tdr = s;
-    else
-      G.dev.tdelta[r++] = tm[s];
-  }
-  const uint32_t nwords = (G.dev.stride / 4 + 31) / 32;
-  uint32_t* m = arena.alloc<uint32_t>(nwords);
-  launch_amg_qmask(G.dev, m, stream);
-  CFD_HIP(hipGetLastError());
-  G.dev.qmask = m;
-  // regular waves of a one-range launch over [0, n) (the layout-true byte count)
-  std::vector<uint32_t> h(nwords);
-  CFD_HIP(hipMemcpyAsync(h.data(), m, nwords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  sync();
-  G.dev.qlane = amg_reg == 2 ? 1 : 0;
-  uint64_t rows = 0;
-  for (uint32_t w = 0; w < nwords; ++w)
-    rows += G.dev.qlane ? 4u * (uint32_t)__builtin_popcount(h[w])
-                        : ((w % 2 == 0 && w + 1 < nwords && h[w] == ~0u && h[w + 1] == ~0u) ? 256u : 0u);
-  G.reg_rows = rows;
 }
 
 // Host AMG setup (amg_setup.cpp): the assembled scalar matrix is downloaded,
@@ -1281,16 +1248,18 @@ void Solver::prof_grow(size_t n) {
   }
 }
 
-void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bool nt) {
+void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bool nt, bool pre) {
   AmgGpuLevel& L = levels[li];
+  AmgLevelDev d = L.dev;
+  d.flat = (li == 0 && pre && flat_order() && pre_flat) ? 1 : 0;
   if (x_zero) {
-    launch_amg_smooth_zero(L.dev, b, L.xt, stream);
+    launch_amg_smooth_zero(d, b, L.xt, stream);
   } else if (li == 0 && prof_take()) {
     const auto ev = prof_pair();
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second, nt);
+    launch_amg_smooth(d, xcur, b, L.xt, stream, ev.first, ev.second, nt);
     prof_launches++;
   } else {
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, nullptr, nullptr, nt);
+    launch_amg_smooth(d, xcur, b, L.xt, stream, nullptr, nullptr, nt);
   }
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
@@ -1315,7 +1284,7 @@ void Solver::v_cycle() {
     AmgGpuLevel& Lv = levels[i];
     const bool ntl = nt(post ? 1u : 16u);
     if (!Lv.dist || x_zero) {
-      amg_smooth(i, Lv.x, Lv.b, x_zero, ntl);
+      amg_smooth(i, Lv.x, Lv.b, x_zero, ntl, !post);
       return;
     }
     const bool timed = i == 0 && prof_take();  // kernel time only: each part timed separately
@@ -1326,6 +1295,7 @@ void Solver::v_cycle() {
       d.r1 = b;
       d.r2 = a2;
       d.r3 = b2;
+      d.flat = (i == 0 && !post && flat_order() && pre_flat) ? 1 : 0;
       if (timed) {
         const auto ev = prof_pair();
         launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second, ntl);
@@ -2021,16 +1991,7 @@ double Solver::smoother_layout_bytes() const {
   if (levels.empty()) return 0.0;
   const AmgLevelDev& d = levels[0].dev;
   const double st = d.stride, n = d.n;
-  return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n - reg_saving(0, false);
-}
-
-// Bytes the regular waves of level li do not move in one smoother (or, with
-// residual, residual) sweep: the length (and rank) byte and the column deltas
-// of each of their rows, less the mask words every wave reads (8 B per wave).
-double Solver::reg_saving(size_t li, bool residual) const {
-  const AmgLevelDev& d = levels[li].dev;
-  if (!d.qmask) return 0.0;
-  return (double)levels[li].reg_rows * ((residual ? 2.0 : 1.0) + 2.0 * d.w) - d.stride / 32.0;
+  return st + std::max(d.w, 1) * st * (4.0 + (d.use16 ? 2.0 : 4.0)) + 16.0 * n;
 }
 
 // Layout-true bytes of one step under the fixed schedule: per kernel, the
@@ -2063,7 +2024,7 @@ double Solver::layout_step_bytes() const {
   for (int i = 0; i < L; ++i) {
     const AmgLevelDev& d = levels[i].dev;
     const double n = d.n, st = d.stride, img = row_image(d);
-    const double smooth = st + img + 16 * n - reg_saving(i, false);
+    const double smooth = st + img + 16 * n;
     if (i < down) {
       const double nc = levels[i + 1].dev.n;
       // pre-smoother (coarse: zero-x, elementwise; not launched when fused into
@@ -2073,7 +2034,7 @@ double Solver::layout_step_bytes() const {
       if (d.rr_agg && !levels[i].dist)
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
       else
-        vc += (2 * st + img + 16 * n - reg_saving(i, true)) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
+        vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
       if (fused_prolong(i))
         vc += smooth + 4 * n + 4 * nc;                                 // post-smoother reading x + P xc
       else

@@ -172,7 +172,6 @@ struct AmgGpuLevel {
   float* b = nullptr;   // level rhs (level 0: external temp_p)
   float* r = nullptr;   // residual scratch
   uint64_t nnz = 0;     // including diagonal (rows this rank stores)
-  uint64_t reg_rows = 0;  // rows in regular waves (dev.qmask) of a one-range launch
   uint64_t nglob = 0;   // rows of the whole level
   // distributed level: owned rows [C0, C1) of the global level, ghosts around
   bool dist = false;
@@ -310,6 +309,12 @@ struct Solver {
   int amg_wide_limit = 255;
   size_t lds_budget = 0;           // dynamic LDS of the tail kernels on this device (init_kernel_attributes)
   bool coupled_reg = true;         // regular coupled rows: derived columns (CFD_COUPLED_REG=0: always load)
+  // from this many rows on, the Schur kernels and the face sweeps (prepare,
+  // assemble) take their rows in block dispatch order instead of the
+  // XCD-contiguous remap (kernels.hpp CoupledMatrix::schur_flat; CFD_FLAT_ROWS)
+  uint32_t flat_rows = 1u << 22;
+  bool flat_order() const { return N >= flat_rows; }
+  bool pre_flat = true;  // the level-0 pre-smoother too (CFD_FLAT_PRE=0: remap)
   bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
   bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
@@ -331,7 +336,6 @@ struct Solver {
   // first prepare() when this rank's index matches
   int debug_fault_after_prepare = -1;
   bool nt(unsigned bit) const { return (nt_mask & bit) != 0; }
-  int amg_reg = 1;  // level-0 regular waves (set_amg_regular; CFD_AMG_REG=0: off, 2: per quad)
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {
@@ -428,7 +432,6 @@ struct Solver {
   double algorithmic_step_bytes() const;
   double layout_step_bytes() const;
   double smoother_bytes() const;
-  double reg_saving(size_t li, bool residual) const;
   double smoother_layout_bytes() const;
   // checkpoint / resume (checkpoint.cpp, cfd_state_file_header)
   void save_state(const char* path);  // collective on a distributed solver
@@ -450,10 +453,9 @@ struct Solver {
   bool device_levels(AmgSetupLevel& cur, int li0, const std::vector<uint64_t>& part0);
   std::vector<std::vector<uint32_t>> allgatherv_u32(const std::vector<uint32_t>& mine);  // collective
   void set_amg_full_policy(AmgGpuLevel& G, int li);
-  void set_amg_regular(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
   void v_cycle();
-  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false);
+  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false, bool pre = false);
   std::pair<hipEvent_t, hipEvent_t> prof_pair();
  public:
   static constexpr size_t kProfPoolMax = 1u << 15;

@@ -268,11 +268,6 @@ cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* ro
  * (matrix, diagonal, P, R) -- host and device setups must agree bit-for-bit.
  * Debug/parity only; not part of the reference surface.                     */
 cfd_status cfd_debug_amg_info(cfd_solver* s, int32_t level, int32_t* setup_path, uint64_t* digest);
-/* Rows of AMG level `level` in regular waves (level 0 of a face-stencil mesh:
- * every row of the wave has the modal slot pattern, so the smoother and
- * residual derive its lengths, diagonal ranks and columns instead of loading
- * them; CFD_AMG_REG=0 at solver creation disables it); 0: none.  Debug only. */
-cfd_status cfd_debug_amg_regular(const cfd_solver* s, int32_t level, uint64_t* regular_rows);
 /* Layout-true bytes of one level-0 smoother sweep: the minimum the kernel
  * moves in this library's level image (u8 lengths, ELL values + 16/32-bit
  * columns, b, x, diagonal, x_out); the roofline of record divides this by

@@ -506,6 +506,7 @@ VARIANTS = [
     {"CFD_AMG_TAIL_ROWS": "0"},       # no tail kernel: every level launched
     {"CFD_AMG_FUSE_PRESMOOTH": "0"},  # coarse pre-smoother as its own sweep
     {"CFD_COUPLED_REG": "0"},         # coupled-matrix kernels always load their columns
+    {"CFD_FLAT_ROWS": "0"},           # Schur kernels / face sweeps in dispatch order (production: >= 2^22 rows)
     {"CFD_AMG_FUSED_RR": "0"},        # separate residual + restriction kernels on every level
     {"CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused residual-restriction on every level, predicated loads
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
@@ -537,38 +538,6 @@ def test_amg_kernel_variants_parity(env, mesh_name, monkeypatch):
         o.step()
         _assert_same_fields(g, o, f"{env} {mesh_name} step {k}")
         _assert_same_info(g, o, f"{env} {mesh_name} step {k}")
-
-
-@pytest.mark.parametrize("env", [{}, {"CFD_NT": "63"}, {"CFD_AMG_FUSED_PROLONG": "off", "CFD_AMG_TAIL_ROWS": "0"},
-                                 {"CFD_AMG_REG": "2"}],
-                         ids=["default", "nt63", "separate-prolong", "per-quad"])
-def test_amg_regular_waves_parity(env, monkeypatch):
-    """Level 0 of a tall cut-cell channel + obstacle (600-cell columns, 28 %
-    of its 256-row waves regular: kernels.hip wave_regular derives their
-    lengths, diagonal ranks and columns) next to irregular waves in the same
-    launches: GPU == oracle bit-exact, and == the GPU with the regular path
-    off (CFD_AMG_REG=0)."""
-    from cfd2_amd.mesh import ChannelWithObstacle, generate_cut_cell_mesh
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    geo = ChannelWithObstacle(length=0.2, height=1.5, obstacle_center=(0.1, 0.75), obstacle_radius=0.05)
-    mesh = generate_cut_cell_mesh(geo, 0.0025, 0.0025, 1.2, (0.2, 1.5))
-    g, o = _pair(mesh, fixed_outer=3, fixed_inner=10)
-    monkeypatch.setenv("CFD_AMG_REG", "0")
-    off = GpuSolver(mesh, config=default_config(fixed_outer=3, fixed_inner=10))
-    for s in (g, o, off):
-        _setup_amg_test(s, mesh, 1)
-    for k in range(3):
-        for s in (g, o, off):
-            s.step()
-        if k == 0:
-            rows = g.amg_levels()[0][0]
-            hi = 0.7 if env.get("CFD_AMG_REG") == "2" else 0.5  # per quad: every regular quad counts
-            assert 0.2 * rows < g.amg_regular_rows(0) < hi * rows
-            assert off.amg_regular_rows(0) == 0
-        _assert_same_fields(g, o, f"{env} step {k}")
-        _assert_same_info(g, o, f"{env} step {k}")
-        _assert_same_fields(g, off, f"{env} regular off, step {k}")
 
 
 def test_midrun_api_changes_parity():
