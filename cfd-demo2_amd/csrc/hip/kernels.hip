@@ -116,20 +116,16 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // same data starts on the rows whose lines that kernel touched last, which may
 // still sit in the memory-side Infinity Cache (MALL, 256 MB, shared by all
 // XCDs).  Order only: every row's arithmetic is unchanged.
-// remap = false (kernel-uniform): blocks keep dispatch order (REV: reversed),
-// each XCD's blocks interleaved over the whole range -- faster for the Schur
-// kernels and the face sweeps on big meshes (see CoupledMatrix::schur_flat).
 template <bool REV = false>
-__device__ __forceinline__ uint32_t xcd_block(bool remap = true) {
+__device__ __forceinline__ uint32_t xcd_block() {
   const uint32_t b = blockIdx.x, nb = gridDim.x;
-  if (!remap) return REV ? nb - 1u - b : b;
   const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
   const uint32_t base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   if constexpr (REV) return base + ((xcd < r) ? q : q - 1u) - (b >> 3);
   return base + (b >> 3);
 }
 template <bool REV = false>
-__device__ __forceinline__ uint32_t row_id(bool remap = true) { return xcd_block<REV>(remap) * kBlock + threadIdx.x; }
+__device__ __forceinline__ uint32_t row_id() { return xcd_block<REV>() * kBlock + threadIdx.x; }
 
 // Kernels that run top-down (xcd_block<true>) to reuse the Infinity Cache lines
 // of the kernel before them (build-time tunables, tools/ab_variants.py).  Same-box
@@ -153,9 +149,8 @@ constexpr bool kRevSmooth = true;     // k_amg_smooth: top-down
 // second range lets a distributed rank process both boundary strips of a
 // halo'd kernel in one launch); false: no rows for this thread.
 template <bool REV = false>
-__device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0,
-                                          bool remap = true) {
-  const uint32_t t = row_id<REV>(remap), na = (r1 - r0 + 3) / 4;
+__device__ __forceinline__ bool row_range(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
+  const uint32_t t = row_id<REV>(), na = (r1 - r0 + 3) / 4;
   if (t < na) {
     i0 = r0 + 4 * t;
     return i0 < r1;
@@ -335,7 +330,7 @@ constexpr int kRedFinalThreads = CFD_RED_FINAL_THREADS;
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
 // Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
 __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
-  const uint32_t i = row_id(!a.flat);
+  const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -453,7 +448,7 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
 
 // coupled_assembly_merged.wgsl:70-463
 __global__ void __launch_bounds__(kBlock) k_assemble(AssembleArgs a) {
-  const uint32_t i = row_id(!a.flat);
+  const uint32_t i = row_id();
   const uint32_t N = a.N;
   if (i >= N) return;
   const cfd_constants c = a.c;
@@ -886,9 +881,8 @@ __device__ __forceinline__ bool consec4(const int c[4]) {
 // (102 instead of 196 VGPRs: 4 wavefronts per SIMD instead of 2), one 16-byte
 // load per slot array; same-box A/B at C2 (round 2): SpMV 225.8 -> 218.0 us.
 template <bool REV = false>
-__device__ __forceinline__ bool row_range2(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0,
-                                           bool remap = true) {
-  const uint32_t t = row_id<REV>(remap), na = (r1 - r0 + 1) / 2;
+__device__ __forceinline__ bool row_range2(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t& i0) {
+  const uint32_t t = row_id<REV>(), na = (r1 - r0 + 1) / 2;
   if (t < na) {
     i0 = r0 + 2 * t;
     return i0 < r1;
@@ -1411,7 +1405,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
                                                              float* p_sol, float* p_prev) {
   constexpr int U = CFD_PREDICT_U, U1 = CFD_PREDICT_U1;
   uint32_t i0;
-  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0, !A.schur_flat)) return;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const float sc = binv[jv];
   const float* wb = w_in + 3 * (size_t)i0;
   const f4u wa = ld4u(wb);
@@ -1477,7 +1471,7 @@ __global__ void __launch_bounds__(kBlock) k_precond_correct2(CoupledMatrix A, co
                                                              float* __restrict__ z) {
   constexpr int U = CFD_CORRECT_U, U1 = CFD_CORRECT_U1;
   uint32_t i0;
-  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0, !A.schur_flat)) return;
+  if (!row_range2(A.r0, A.r1, A.r2, A.r3, i0)) return;
   const ushort2 lg = *reinterpret_cast<const ushort2*>(A.lg + i0);
   // the row pair's own operands issued with the header (no round trip after the slots)
   const float sc = binv[jv];
@@ -1764,7 +1758,7 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const floa
                                                        const float* __restrict__ b, float* __restrict__ x_out,
                                                        const float* __restrict__ xc) {
   uint32_t i0;
-  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0, !L.flat)) return;
+  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0)) return;
   *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(L, x, b, i0, xc);
 }
 

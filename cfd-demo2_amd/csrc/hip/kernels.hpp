@@ -129,7 +129,6 @@ struct StateView {
 
 struct PrepareArgs {
   uint32_t N;
-  int flat;               // rows in dispatch order (big meshes, see CoupledMatrix::schur_flat)
   cfd_constants c;
   FaceSlots fs;
   const float* vol;
@@ -143,7 +142,6 @@ struct PrepareArgs {
 
 struct AssembleArgs {
   uint32_t N;
-  int flat;               // rows in dispatch order (big meshes, see CoupledMatrix::schur_flat)
   uint32_t ld;             // scalar-row ELL slot stride
   cfd_constants c;
   FaceSlots fs;
@@ -189,12 +187,6 @@ struct CoupledMatrix {
   // loading them; set when ws <= kCoupledRegMaxWs (one peeled slot group)
   int reg;
   int tmode[8];
-  // 1: the Schur prediction / correction take their row pairs in block
-  // dispatch order instead of the XCD-contiguous remap (kernels.hip
-  // xcd_block): on big meshes their streams then run closer together in
-  // memory (C2 A/B, profiles/r04/ab_noxcd_c2.txt: predict 157.4 -> 146.1 us,
-  // correct 131.3 -> 123.9); at C1 the remap's L2 locality wins (15.7 vs 18.7)
-  int schur_flat;
 };
 constexpr uint32_t kLgUsedMask = 0x7Fu, kLgRegular = 0x80u;
 constexpr int kCoupledRegMaxWs = 5;
@@ -239,9 +231,6 @@ struct AmgLevelDev {
   // k_amg_resrestrict: aggregates per block (0: the level keeps the separate
   // residual + restriction kernels); every block's members fit kRRCap
   uint32_t rr_agg;
-  // k_amg_smooth: rows in block dispatch order (the level-0 pre-smoother after
-  // a dispatch-order Schur prediction, CoupledMatrix::schur_flat)
-  int flat = 0;
 };
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
 // zeroed entries after every level's agg array: the fused prolongation reads

@@ -87,8 +87,6 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
-  if (const char* fr = std::getenv("CFD_FLAT_ROWS")) flat_rows = (uint32_t)std::strtoul(fr, nullptr, 0);
-  if (const char* fp = std::getenv("CFD_FLAT_PRE")) pre_flat = fp[0] != '0';
   if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
@@ -250,7 +248,6 @@ CoupledMatrix Solver::cmat() const {
   A.cdiag2 = cdiag2;
   A.reg = coupled_reg && !topo.tmode.empty() && topo.ws <= kCoupledRegMaxWs ? 1 : 0;
   for (int r = 0; r < 8; ++r) A.tmode[r] = r < (int)topo.tmode.size() ? topo.tmode[r] : 0;
-  A.schur_flat = flat_order() ? 1 : 0;
   return A;
 }
 
@@ -499,7 +496,6 @@ void Solver::rotate() {  // coupled_solver.rs:43-71
 void Solver::prepare() {
   PrepareArgs a;
   a.N = N;
-  a.flat = flat_order() ? 1 : 0;
   a.c = constants;
   a.fs = fs;
   a.vol = d_vol;
@@ -521,7 +517,6 @@ void Solver::prepare() {
 void Solver::assemble() {
   AssembleArgs a;
   a.N = N;
-  a.flat = flat_order() ? 1 : 0;
   a.ld = topo.ld;
   a.c = constants;
   a.fs = fs;
@@ -1248,18 +1243,16 @@ void Solver::prof_grow(size_t n) {
   }
 }
 
-void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bool nt, bool pre) {
+void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bool nt) {
   AmgGpuLevel& L = levels[li];
-  AmgLevelDev d = L.dev;
-  d.flat = (li == 0 && pre && flat_order() && pre_flat) ? 1 : 0;
   if (x_zero) {
-    launch_amg_smooth_zero(d, b, L.xt, stream);
+    launch_amg_smooth_zero(L.dev, b, L.xt, stream);
   } else if (li == 0 && prof_take()) {
     const auto ev = prof_pair();
-    launch_amg_smooth(d, xcur, b, L.xt, stream, ev.first, ev.second, nt);
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second, nt);
     prof_launches++;
   } else {
-    launch_amg_smooth(d, xcur, b, L.xt, stream, nullptr, nullptr, nt);
+    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, nullptr, nullptr, nt);
   }
   std::swap(xcur, L.xt);  // out-of-place Jacobi: the partner buffer becomes current
 }
@@ -1284,7 +1277,7 @@ void Solver::v_cycle() {
     AmgGpuLevel& Lv = levels[i];
     const bool ntl = nt(post ? 1u : 16u);
     if (!Lv.dist || x_zero) {
-      amg_smooth(i, Lv.x, Lv.b, x_zero, ntl, !post);
+      amg_smooth(i, Lv.x, Lv.b, x_zero, ntl);
       return;
     }
     const bool timed = i == 0 && prof_take();  // kernel time only: each part timed separately
@@ -1295,7 +1288,6 @@ void Solver::v_cycle() {
       d.r1 = b;
       d.r2 = a2;
       d.r3 = b2;
-      d.flat = (i == 0 && !post && flat_order() && pre_flat) ? 1 : 0;
       if (timed) {
         const auto ev = prof_pair();
         launch_amg_smooth(d, Lv.x, Lv.b, Lv.xt, stream, ev.first, ev.second, ntl);

@@ -309,12 +309,6 @@ struct Solver {
   int amg_wide_limit = 255;
   size_t lds_budget = 0;           // dynamic LDS of the tail kernels on this device (init_kernel_attributes)
   bool coupled_reg = true;         // regular coupled rows: derived columns (CFD_COUPLED_REG=0: always load)
-  // from this many rows on, the Schur kernels and the face sweeps (prepare,
-  // assemble) take their rows in block dispatch order instead of the
-  // XCD-contiguous remap (kernels.hpp CoupledMatrix::schur_flat; CFD_FLAT_ROWS)
-  uint32_t flat_rows = 1u << 22;
-  bool flat_order() const { return N >= flat_rows; }
-  bool pre_flat = true;  // the level-0 pre-smoother too (CFD_FLAT_PRE=0: remap)
   bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
   bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
   bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
@@ -455,7 +449,7 @@ struct Solver {
   void set_amg_full_policy(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
   void v_cycle();
-  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false, bool pre = false);
+  void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false);
   std::pair<hipEvent_t, hipEvent_t> prof_pair();
  public:
   static constexpr size_t kProfPoolMax = 1u << 15;
