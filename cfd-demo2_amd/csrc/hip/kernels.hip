@@ -685,14 +685,15 @@ __device__ __forceinline__ void store12(float* p, const float v[12]) {
 // before the next issues -- for these kernels, which stream up to 51 vectors
 // at once, measured faster than keeping a wavefront's loads in flight
 // together (same-box A/B at C2: CGS update 349 -> 294 us, dots 300 -> 289).
-__device__ __forceinline__ size_t cell_q(uint32_t q) {
-  return (size_t)blockIdx.x * 1024u + 256u * q + (threadIdx.x & ~63u) + red_lane();
+__device__ __forceinline__ size_t cell_qb(uint32_t b, uint32_t q) {
+  return (size_t)b * 1024u + 256u * q + (threadIdx.x & ~63u) + red_lane();
 }
+__device__ __forceinline__ size_t cell_q(uint32_t q) { return cell_qb(blockIdx.x, q); }
 template <bool FULL, bool NT = false, bool SER = false>
-__device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[4][3]) {
+__device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[4][3], uint32_t b = ~0u) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const size_t c = cell_q(q);
+    const size_t c = cell_qb(b == ~0u ? blockIdx.x : b, q);
     if (FULL || c < N) {
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
@@ -708,10 +709,10 @@ __device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[
   }
 }
 template <bool FULL>
-__device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const float v[4][3]) {
+__device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const float v[4][3], uint32_t b = ~0u) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const size_t c = cell_q(q);
+    const size_t c = cell_qb(b == ~0u ? blockIdx.x : b, q);
     if (FULL || c < N) {
 #pragma unroll
       for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
@@ -769,8 +770,8 @@ __device__ __forceinline__ float unit_value_q(const float* ql, uint32_t U, uint3
   return unit_value(l, U, u);
 }
 // the block's chunks are all inside the mesh
-__device__ __forceinline__ bool block_full(uint32_t N) {
-  return (size_t)(blockIdx.x + 1) * 4u * kRedChunkCells <= N;
+__device__ __forceinline__ bool block_full(uint32_t N, uint32_t b = ~0u) {
+  return (size_t)((b == ~0u ? blockIdx.x : b) + 1) * 4u * kRedChunkCells <= N;
 }
 
 // unit partials of dot(x, y) over 3-component cells
@@ -1044,7 +1045,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv2(CoupledMatrix A, const float* 
 // calc_dots_cgs (gmres_cgs.wgsl:28-82): partial[ii * np + unit] = <w, V_ii>, ii = 0..j,
 // V_ii = binv[ii] * W_ii, in the cell layout of load_cells3; quarter values
 // ql[16 ii + 4 q + w] in LDS, units at the end.
-template <bool FULL, bool SER>
+template <bool FULL, bool SER, bool NTB = true>
 __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, const float* __restrict__ basis,
                                                const float* __restrict__ binv, size_t stride, int j, uint32_t N,
                                                float* ql) {
@@ -1053,7 +1054,7 @@ __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, cons
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[4][3], t[4];
-    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, NTB, SER>(basis + (size_t)ii * stride, N, v);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
@@ -1067,12 +1068,22 @@ template <bool SER>
 __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w,
                                                      const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride,
-                                                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np) {
+                                                     int j, uint32_t N, uint32_t U, float* partial, uint32_t np,
+                                                     uint32_t tb) {
   __shared__ float ql[16 * 64];
-  if (block_full(N))
-    cgs_dots_cells<true, SER>(w, basis, binv, stride, j, N, ql);
-  else
-    cgs_dots_cells<false, SER>(w, basis, binv, stride, j, N, ql);
+  // blocks from tb on read the basis with the default policy: their lines stay
+  // in the Infinity Cache for the update, which walks the blocks top-down
+  if (blockIdx.x < tb) {
+    if (block_full(N))
+      cgs_dots_cells<true, SER>(w, basis, binv, stride, j, N, ql);
+    else
+      cgs_dots_cells<false, SER>(w, basis, binv, stride, j, N, ql);
+  } else {
+    if (block_full(N))
+      cgs_dots_cells<true, SER, false>(w, basis, binv, stride, j, N, ql);
+    else
+      cgs_dots_cells<false, SER, false>(w, basis, binv, stride, j, N, ql);
+  }
   __syncthreads();
   const uint32_t UB = 4 / U;
   for (uint32_t idx = threadIdx.x; idx < (uint32_t)(j + 1) * UB; idx += kBlock) {
@@ -1093,26 +1104,27 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 // updated w is written straight into basis slot j+1 (unnormalised, see binv).
 template <bool FULL, bool SER>
 __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
-                                                 const float* hcol, const float* scol, uint32_t N, float t[4]) {
+                                                 const float* hcol, const float* scol, uint32_t N, float t[4],
+                                                 uint32_t b) {
   float corr[4][3] = {};
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
-    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v);
+    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v, b);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int e = 0; e < 3; ++e) corr[q][e] += h * (sc * v[q][e]);
   }
   float wn[4][3];
-  load_cells3<FULL>(w, N, wn);
+  load_cells3<FULL>(w, N, wn, b);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #pragma unroll
     for (int e = 0; e < 3; ++e) wn[q][e] = wn[q][e] - corr[q][e];
     t[q] = cell_dot3(wn[q], wn[q]);
   }
-  store_cells3_stream<FULL>(basis + (size_t)(j + 1) * stride, N, wn);
+  store_cells3_stream<FULL>(basis + (size_t)(j + 1) * stride, N, wn, b);
 }
 template <bool SER>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
@@ -1120,21 +1132,22 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
                                                             const float* __restrict__ binv,
                                                             size_t stride, int j,
                                                             const float* __restrict__ H, int m1,
-                                                            uint32_t N, uint32_t U, float* partial) {
+                                                            uint32_t N, uint32_t U, float* partial, int rev) {
   __shared__ float hcol[64], scol[64], ql[16];
+  const uint32_t b = rev ? gridDim.x - 1u - blockIdx.x : blockIdx.x;  // rev: top-down (after the dots)
   if (threadIdx.x <= (unsigned)j) {
     hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
     scol[threadIdx.x] = binv[threadIdx.x];
   }
   __syncthreads();
   float t[4];
-  if (block_full(N))
-    cgs_update_cells<true, SER>(w, basis, stride, j, hcol, scol, N, t);
+  if (block_full(N, b))
+    cgs_update_cells<true, SER>(w, basis, stride, j, hcol, scol, N, t, b);
   else
-    cgs_update_cells<false, SER>(w, basis, stride, j, hcol, scol, N, t);
+    cgs_update_cells<false, SER>(w, basis, stride, j, hcol, scol, N, t, b);
   quarter_trees(t, ql);
   __syncthreads();
-  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
+  const uint32_t UB = 4 / U, unit = b * UB + threadIdx.x;
   if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, threadIdx.x);
 }
 
@@ -2528,27 +2541,32 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, x, y, b);
 }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
-                     uint32_t U, float* partial, uint32_t np, hipStream_t s) {
+                     uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes) {
   if (!N) return;
+  const uint32_t nb = red_blocks(N);
+  // the last blocks whose basis lines (j + 1 vectors + w, 12 B per cell each) fit keep_bytes
+  const size_t keep_blocks = keep_bytes / ((size_t)(j + 2) * 12u * 1024u);
+  const uint32_t tb = keep_blocks >= nb ? 0u : nb - (uint32_t)keep_blocks;
   if (N >= CFD_CGS_SER_MIN_CELLS)
-    hipLaunchKernelGGL(k_cgs_dots<true>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
-                       partial, np);
+    hipLaunchKernelGGL(k_cgs_dots<true>, dim3(nb), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
+                       partial, np, tb);
   else
-    hipLaunchKernelGGL(k_cgs_dots<false>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
-                       partial, np);
+    hipLaunchKernelGGL(k_cgs_dots<false>, dim3(nb), dim3(kBlock), 0, s, w, basis, binv, stride, j, N, U,
+                       partial, np, tb);
 }
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s,
+                            bool rev) {
   if (!N) return;
   if (N >= CFD_CGS_SER_MIN_CELLS)
     hipLaunchKernelGGL(k_cgs_update_norm<true>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
-                       m1, N, U, partial);
+                       m1, N, U, partial, rev ? 1 : 0);
   else
     hipLaunchKernelGGL(k_cgs_update_norm<false>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
-                       m1, N, U, partial);
+                       m1, N, U, partial, rev ? 1 : 0);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, float* host_resid, hipStream_t s) {

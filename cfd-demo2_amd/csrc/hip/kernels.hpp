@@ -294,13 +294,16 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
                  bool nt = false);
 // basis: unnormalised W_i at basis + i*stride, scales binv[i]; unit partials
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
+// keep_bytes > 0: the last blocks (their j + 2 vectors within keep_bytes) read
+// the basis with the default policy, for a top-down update (rev) after it
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
-                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s);
+                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes = 0);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
 // W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s);
+                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s,
+                            bool rev = false);
 // ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|,
 // also into host_resid[j] (device view of pinned host memory) when non-null
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,

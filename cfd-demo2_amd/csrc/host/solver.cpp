@@ -88,6 +88,12 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
   if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
+  // C1-size meshes: 64 MB of the dots pass kept in the Infinity Cache for a
+  // top-down update (profiles/r04/ab_cgskeep2_c1.txt: update 36.5-36.9 ->
+  // 32.3 us, dots +0.3 us per iteration); from 2^22 cells on the kept lines
+  // cost more than they return (ab_cgskeep_c2.txt: dots 284 -> 293 us)
+  cgs_keep_bytes = N < (1u << 22) ? (size_t)64 << 20 : 0;  // (kernels.hip CFD_CGS_SER_MIN_CELLS)
+  if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
@@ -1556,9 +1562,9 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
         A.r3 = b2;
         launch_spmv(A, zj, w, stream, nullptr, nt(8));
       });
-      launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream);
+      launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
       launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream);
+      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0);
       // the residual estimate goes to one of two pinned slots, never the slot
       // of a lagged read still pending (which may carry over from the previous
       // iteration, restart or solve: the reader is never reset)

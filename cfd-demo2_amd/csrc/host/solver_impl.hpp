@@ -330,6 +330,11 @@ struct Solver {
   // first prepare() when this rank's index matches
   int debug_fault_after_prepare = -1;
   bool nt(unsigned bit) const { return (nt_mask & bit) != 0; }
+  // CGS: bytes of the dots pass's last blocks read with the default policy
+  // (kept in the Infinity Cache for the top-down update after it); 0: every
+  // basis read nontemporal, both passes bottom-up (CFD_CGS_KEEP_MB; default
+  // set in the constructor: 64 MB below 2^22 cells, else 0)
+  size_t cgs_keep_bytes = 0;
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {

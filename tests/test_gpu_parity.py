@@ -506,6 +506,7 @@ VARIANTS = [
     {"CFD_AMG_TAIL_ROWS": "0"},       # no tail kernel: every level launched
     {"CFD_AMG_FUSE_PRESMOOTH": "0"},  # coarse pre-smoother as its own sweep
     {"CFD_COUPLED_REG": "0"},         # coupled-matrix kernels always load their columns
+    {"CFD_CGS_KEEP_MB": "1"},         # CGS dots' last blocks default-policy, update top-down
     {"CFD_AMG_FUSED_RR": "0"},        # separate residual + restriction kernels on every level
     {"CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused residual-restriction on every level, predicated loads
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
