@@ -2331,29 +2331,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
         X[i] = xp;   // sweep 9
       }
       __syncthreads();
-#if !defined(CFD_DBG_TAIL_BARRIERS)
-    } else if (D.n <= 64) {
-      // coarsest level within one wavefront (C1: 64 rows, C2: 51): its 10
-      // sweeps run in wave 0, ordered by wavefront-scope LDS fences instead of
-      // 10 block barriers -- the same row operations in the same order
-      if (t < 64) {
-        for (int s = 0; s < 10; ++s) {
-          if (t < D.n) {
-            if (s == 0) {
-              XT[t] = wmix(0.0f, (B[t] - 0.0f) / de[t], 0.8f);
-            } else {
-              const float* xin = (s & 1) ? XT : X;
-              float* xout = (s & 1) ? X : XT;
-              xout[t] = smooth(D, xin, B, t);
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-      }
-      __syncthreads();
-#endif
     } else {
       for (int s = 0; s < 10; ++s) {
         if (s == 0) {
