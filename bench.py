@@ -597,8 +597,10 @@ def main():
             "frac_counter": (counter_gbs / HBM_PEAK_GBS) if counter_gbs else None,
             "bytes_per_launch": layout_bytes,
             "bytes_model": "layout-true (cfd_smoother_layout_bytes)",
-            "reference_format_bytes_per_launch": sm_bytes,
-            "reference_format_rate_gbs": achieved_ref,
+            # counts, not HBM rates: bytes in the reference's CSR format that
+            # this layout does not move, and that count / the launch time
+            "reference_format_bytes_count": sm_bytes,
+            "reference_format_effective_gbs": achieved_ref,
             "avg_launch_us": sm_avg_s * 1e6,
             "launches": sm_n,  # timed sweeps: every sample_stride-th level-0 sweep of the timed steps
             "sample_stride": max(1, int(os.environ.get("CFD_PROF_STRIDE", "1"))),
@@ -607,7 +609,7 @@ def main():
         # whole-step byte COUNT in the reference's CSR format (SURVEY §8(d)
         # sum): this layout moves ~45 % less (step_counter_traffic below is the
         # measured traffic), so count / step time is not an HBM rate
-        "step_reference_format_bytes": step_bytes,
+        "step_reference_format_bytes_count": step_bytes,
         # layout-true bytes of one step (this rank): each kernel's minimum
         # traffic at kernel level in this library's layouts x its launches (not
         # a bound on HBM traffic: some lines come from the Infinity Cache)

@@ -62,12 +62,22 @@ __device__ __forceinline__ V ldx(const V* p) {
   } else {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    // f4u / f2u sources are only 4-byte aligned: their loads keep that
+    // alignment instead of the vector types' natural 16 / 8 bytes
+    typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    typedef unsigned int u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
     V r;
-    if constexpr (sizeof(V) == 16) {
+    if constexpr (sizeof(V) == 16 && alignof(V) >= 16) {
       const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
       __builtin_memcpy(&r, &t, 16);
-    } else if constexpr (sizeof(V) == 8) {
+    } else if constexpr (sizeof(V) == 16) {
+      const u32x4a4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4a4*>(p));
+      __builtin_memcpy(&r, &t, 16);
+    } else if constexpr (sizeof(V) == 8 && alignof(V) >= 8) {
       const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+      __builtin_memcpy(&r, &t, 8);
+    } else if constexpr (sizeof(V) == 8) {
+      const u32x2a4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2a4*>(p));
       __builtin_memcpy(&r, &t, 8);
     } else if constexpr (sizeof(V) == 4) {
       const uint32_t t = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));

@@ -180,6 +180,10 @@ cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out) {
 cfd_status cfd_state_save(cfd_solver* s, const char* path) {
   CHECK_S(s);
   if (!path) return set_error(CFD_ERR_INVALID, "null path");
+  // a rank of a group whose step failed holds a state from the middle of that
+  // step: a checkpoint of it would later load as a consistent one
+  if (s->s->needs_restore)
+    return set_error(CFD_ERR_INVALID, "state save refused: the group needs restore after a failed step");
   return guard([&] { s->s->save_state(path); });
 }
 cfd_status cfd_state_load(cfd_solver* s, const char* path) {
@@ -423,6 +427,12 @@ int32_t cfd_group_needs_restore(cfd_solver* const* h, int32_t n) {
 
 cfd_status cfd_group_state_save(cfd_solver* const* h, int32_t n, const char* path) {
   if (!path) return set_error(CFD_ERR_INVALID, "null path");
+  // the ranks of a failed group step stopped at different points of it: a file
+  // of that state would clear needs_restore on load (cfd_state_load) and the
+  // group would continue from an inconsistent state
+  if (cfd_group_needs_restore(h, n))
+    return set_error(CFD_ERR_INVALID, "group state save refused: the group needs restore after a failed step "
+                                      "(cfd_state_load on every rank, or cfd_group_reset)");
   return group_run(h, n, [path](cfd2::Solver& s) { s.save_state(path); });
 }
 

@@ -357,16 +357,16 @@ void Solver::halo_end() {
   comm_recs.push_back({halo_cat, 0, a, b});
 }
 
+// The pool grows for as long as comm_prof is on: a drain (both streams
+// synchronised) inside the timed step would stall it and shift the waits
+// measured after it (a C4 step records ~18 k events).  The pool
+// is folded and reused only by comm_drain() (cfd_comm_timing, enable/disable).
 hipEvent_t Solver::comm_event() {
   if (comm_ev_used == comm_ev_pool.size()) {
-    if (comm_ev_pool.size() >= (1u << 14)) {  // fold what is pending, reuse the pool
-      comm_drain();
-    } else {
-      for (int k = 0; k < 256; ++k) {
-        hipEvent_t e;
-        CFD_HIP(hipEventCreate(&e));
-        comm_ev_pool.push_back(e);
-      }
+    for (int k = 0; k < 1024; ++k) {
+      hipEvent_t e;
+      CFD_HIP(hipEventCreate(&e));
+      comm_ev_pool.push_back(e);
     }
   }
   return comm_ev_pool[comm_ev_used++];
@@ -1061,8 +1061,9 @@ void Solver::ensure_amg() {
   amg_built = true;
   if (!from_checkpoint) amg_age = 0;
   if (timing)
-    std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s\n", how, L,
-                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+    std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s, tail from level %d (LDS image from level %d)\n",
+                 how, L, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
+                 tail_first, tail_blob_first);
 }
 
 // Aggregates per block of k_amg_resrestrict for the single-GPU / replicated
@@ -1508,6 +1509,10 @@ void Solver::flush_inner() {
 
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   const Range range("fgmres solve");
+  // LinearSolverStats.time = start_time.elapsed() on every exit
+  // (coupled_solver_fgmres.rs:1729,1840,1867,2446): host wall time of the solve
+  const auto t_start = std::chrono::steady_clock::now();
+  auto elapsed = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
   cfd_linear_stats st{};
   const size_t n = 3 * (size_t)N;
   const float tol = cfg.fgmres_rtol, abstol = cfg.fgmres_atol;
@@ -1527,6 +1532,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     st.residual = rhs_norm;
     st.converged = rhs_norm < abstol;
     st.diverged = !std::isfinite(rhs_norm);
+    st.time_s = elapsed();
     return st;
   }
   float residual_norm = h_pin[1];
@@ -1535,6 +1541,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
     log("FGMRES: Initial guess already converged (||r|| = %s < %s)\n", e2(residual_norm).c_str(), e2(target).c_str());
     st.residual = residual_norm;
     st.converged = 1;
+    st.time_s = elapsed();
     return st;
   }
   log("FGMRES: Initial residual = %s\n", e2(residual_norm).c_str());
@@ -1642,6 +1649,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   st.residual = final_resid;
   st.converged = converged;
   st.diverged = std::isnan(final_resid);
+  st.time_s = elapsed();
   return st;
 }
 

@@ -49,14 +49,19 @@ int main(int argc, char** argv) {
   }
   cfd_step_info info;
   CHECK(cfd_get_step_info(s, &info));
+  /* LinearSolverStats.time (coupled_solver_fgmres.rs:2446): the last solve's wall time */
+  if (!(info.stats_p.time_s > 0.0) || !(info.stats_p.time_s < 60.0)) {
+    fprintf(stderr, "stats_p.time_s not filled: %g\n", info.stats_p.time_s);
+    return 1;
+  }
   CHECK(cfd_state_save(s, state_path));
   /* a bad call reports a status and a message instead of aborting */
   if (cfd_set_u(NULL, uv) != CFD_ERR_INVALID || cfd_last_error()[0] == '\0') {
     fprintf(stderr, "null handle not rejected\n");
     return 1;
   }
-  printf("abi_smoke: %u cells, max|u| = %.6f, outer iterations %u, linear %u: ok\n", n, umax,
-         info.outer_iterations, info.total_linear_iterations);
+  printf("abi_smoke: %u cells, max|u| = %.6f, outer iterations %u, linear %u, last solve %.3f ms: ok\n", n, umax,
+         info.outer_iterations, info.total_linear_iterations, 1e3 * info.stats_p.time_s);
   free(uv);
   cfd_solver_destroy(s);
   cfd_mesh_destroy(mesh);

@@ -184,7 +184,10 @@ def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"CFD_HALO_PACK": "1"}, {"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"},
-                                 {"CFD_AMG_FUSED_PROLONG": "off"}],
+                                 {"CFD_AMG_FUSED_PROLONG": "off"},
+                                 # every level split around its exchanges, but the restriction /
+                                 # prolongation of straddling aggregates all after them
+                                 {"CFD_OVERLAP_MIN_ROWS": "64", "CFD_AMG_HALO_OVERLAP": "0"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_group_variants_parity(env, replicate_rows, monkeypatch):
     """Distributed runs through the packed halo path and the alternative AMG

@@ -115,6 +115,13 @@ def test_group_midstep_failure_needs_restore(tmp_path):
     assert grp.needs_restore
     with pytest.raises(RuntimeError, match="needs restore"):
         grp.step()
+    # nor can the mid-step state be checkpointed (its load would clear the mark,
+    # ADVICE r04): whole group and single rank alike
+    with pytest.raises(RuntimeError, match="needs restore"):
+        grp.save_state(str(tmp_path / "bad.bin"))
+    with pytest.raises(RuntimeError, match="needs restore"):
+        grp.ranks[1].save_state(str(tmp_path / "bad1.bin"))
+    assert not (tmp_path / "bad.bin").exists() and not (tmp_path / "bad1.bin").exists()
     grp.load_state(path)
     assert not grp.needs_restore
     for step in range(2):

@@ -540,6 +540,39 @@ def test_amg_kernel_variants_parity(env, mesh_name, monkeypatch):
         _assert_same_info(g, o, f"{env} {mesh_name} step {k}")
 
 
+@pytest.mark.parametrize("shift", ["0", "1", "4"])
+def test_amg_blob_shift_parity(shift, monkeypatch, capfd):
+    """CFD_AMG_BLOB_SHIFT: how many levels the LDS-image tail may start below
+    the first tail level when that level's image does not fit one CU's LDS
+    (production: C1's 3.9 k-row level).  Forced here by a tail from level 1
+    (CFD_AMG_TAIL_ROWS) on a mesh whose level 1 is too large for the image:
+    shift 0 runs the vectors-only LDS tail, larger shifts the image tail from a
+    lower level -- GPU == oracle bit-exact either way."""
+    monkeypatch.setenv("CFD_AMG_TAIL_ROWS", "1000000")
+    monkeypatch.setenv("CFD_AMG_BLOB_SHIFT", shift)
+    monkeypatch.setenv("CFD_AMG_SETUP_TIMING", "1")
+    mesh = channel_obstacle(h=0.012)
+    g, o = _pair(mesh, fixed_outer=2, fixed_inner=8)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    capfd.readouterr()
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"blob shift {shift} step {k}")
+        _assert_same_info(g, o, f"blob shift {shift} step {k}")
+    import re
+    m = re.search(r"tail from level (-?\d+) \(LDS image from level (-?\d+)\)", capfd.readouterr().err)
+    assert m, "no AMG setup line"
+    tail, blob = int(m.group(1)), int(m.group(2))
+    if shift == "0":
+        assert blob == -1 and tail == 1, (tail, blob)  # level 1's image does not fit: no image tail
+    elif blob >= 0:
+        assert blob == tail and 1 < tail <= 1 + int(shift), (tail, blob)
+    else:
+        assert tail == 1 and shift != "4", (tail, blob)  # four levels down the image fits
+
+
 def test_midrun_api_changes_parity():
     """The reference API used mid-run the way the GUI does (src/ui/app.rs):
     dt / viscosity / scheme / time-scheme / preconditioner switches, a direct
