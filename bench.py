@@ -439,14 +439,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    # timing on from the warm-up steps: the FGMRES iteration graphs (one GPU,
+    # small meshes) are captured there with the smoother's timing nodes, not
+    # inside the timed region (profile_reset below drops the warm-up times)
+    solver.profile_enable(True)
     for k in range(args.warmup):
         t0 = time.perf_counter()
         solver.step()
         setup_s.setdefault("first_step", time.perf_counter() - t0)  # t = 0 step: includes the AMG setup
         log(f"[rank {rank}] warmup step {k}: {time.perf_counter() - t0:.3f}s")
     barrier_sync()
-    solver.profile_enable(True)
     solver.profile_reset()
+    graph0 = solver.graph_stats() if hasattr(solver, "graph_stats") else None
     handles = solver.ranks if args.inproc_ranks > 1 else [solver]
     for hnd in handles:
         hnd.comm_stats(reset=True)
@@ -458,6 +462,7 @@ def main():
     elapsed = time.perf_counter() - t0
     sm_ms, sm_n, sm_bytes = solver.profile_smoother()
     solver.profile_enable(False)
+    graph1 = solver.graph_stats() if graph0 is not None else None
     info = solver.step_info()
     if dist is not None:
         import torch
@@ -606,6 +611,9 @@ def main():
             "sample_stride": max(1, int(os.environ.get("CFD_PROF_STRIDE", "1"))),
         },
         "comm": comm_line,
+        # hipGraph replay of the FGMRES iteration: captures / replays inside the timed steps
+        "graph": ({"enabled": graph1[0], "captures_timed": graph1[1] - graph0[1],
+                   "replays_timed": graph1[2] - graph0[2]} if graph1 else None),
         # whole-step byte COUNT in the reference's CSR format (SURVEY §8(d)
         # sum): this layout moves ~45 % less (step_counter_traffic below is the
         # measured traffic), so count / step time is not an HBM rate

@@ -53,6 +53,8 @@ def _bind():
     L.cfd_profile_enable.argtypes = [_vp, C.c_int32]
     L.cfd_profile_reset.argtypes = [_vp]
     L.cfd_profile_smoother.argtypes = [_vp, dp, C.POINTER(C.c_uint64), dp]
+    L.cfd_graph_enable.argtypes = [_vp, C.c_int32]
+    L.cfd_graph_stats.argtypes = [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.cfd_amg_levels.argtypes = [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint64)]
     L.cfd_step_algorithmic_bytes.argtypes = [_vp]
@@ -282,6 +284,14 @@ class GpuSolver:
     # -- instrumentation --------------------------------------------------------
     def profile_enable(self, on=True): self._call("cfd_profile_enable", 1 if on else 0)
     def profile_reset(self): self._call("cfd_profile_reset")
+
+    def graph_enable(self, on=True): self._call("cfd_graph_enable", 1 if on else 0)
+
+    def graph_stats(self):
+        """(enabled, graphs captured, iterations replayed) of the FGMRES iteration graphs."""
+        e, c, r = C.c_int32(), C.c_uint64(), C.c_uint64()
+        self._call("cfd_graph_stats", C.byref(e), C.byref(c), C.byref(r))
+        return bool(e.value), c.value, r.value
 
     def profile_smoother(self):
         ms, n, b = C.c_double(), C.c_uint64(), C.c_double()

@@ -206,6 +206,7 @@ cfd_status cfd_profile_reset(cfd_solver* s) {
   CHECK_S(s);
   return guard([&] {
     CFD_HIP(hipStreamSynchronize(s->s->stream));
+    s->s->graph_harvest_all(true);  // replays before the reset do not count
     s->s->prof_used = 0;
     s->s->prof_ms = 0.0;
     s->s->prof_launches = 0;
@@ -215,12 +216,28 @@ cfd_status cfd_profile_reset(cfd_solver* s) {
     s->s->prof_grow(8192);  // 4096 timed launches without growing inside the timed steps
   });
 }
+cfd_status cfd_graph_enable(cfd_solver* s, int32_t enable) {
+  CHECK_S(s);
+  return guard([&] {
+    CFD_HIP(hipSetDevice(s->s->device));
+    s->s->drop_graphs();
+    s->s->graph_on = enable != 0;
+  });
+}
+cfd_status cfd_graph_stats(const cfd_solver* s, int32_t* enabled, uint64_t* captures, uint64_t* replays) {
+  CHECK_S(s);
+  if (enabled) *enabled = s->s->graph_on && s->s->R == 1 ? 1 : 0;
+  if (captures) *captures = s->s->graph_captures;
+  if (replays) *replays = s->s->graph_replays;
+  return CFD_OK;
+}
 cfd_status cfd_profile_smoother(const cfd_solver* cs, double* total_ms, uint64_t* launches,
                                 double* bytes_per_launch) {
   CHECK_S(cs);
   cfd2::Solver* s = cs->s;
   return guard([&] {
     CFD_HIP(hipStreamSynchronize(s->stream));
+    s->graph_harvest_all(false);
     for (size_t k = 0; k + 1 < s->prof_used; k += 2) {
       float ms = 0.0f;
       CFD_HIP(hipEventElapsedTime(&ms, s->prof_ev[k], s->prof_ev[k + 1]));

@@ -95,6 +95,14 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   cgs_keep_bytes = N < (1u << 22) ? (size_t)64 << 20 : 0;  // (kernels.hip CFD_CGS_SER_MIN_CELLS)
   if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  {
+    const char* ge = std::getenv("CFD_GRAPH");
+    // opt-in: replay measured no faster than eager launches on this pool
+    // (profiles/r05/ab_graph_c0_c1.txt: C0 13.36-13.47 vs 13.30-13.51 ms/step,
+    // C1 39.6-39.9 vs 38.8-39.1): the host runs ahead of the GPU either way
+    graph_on = ge && ge[0] == '1';
+    if (dist()) graph_on = false;  // halo exchanges and collectives stay eager
+  }
   if (dist()) {
     const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
     if (oe) overlap_min_rows = (uint32_t)std::strtoul(oe, nullptr, 10);
@@ -219,6 +227,10 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
 
 Solver::~Solver() {
   if (stream) (void)hipStreamSynchronize(stream);
+  for (IterGraph& G : graphs) {
+    if (G.exec) (void)hipGraphExecDestroy(G.exec);
+    for (auto e : G.ev) (void)hipEventDestroy(e);
+  }
   for (auto e : ev_iter) (void)hipEventDestroy(e);
   for (auto e : ev_outer)
     if (e) (void)hipEventDestroy(e);
@@ -935,6 +947,7 @@ void Solver::build_amg_host() {
 void Solver::drop_amg() {
   CFD_HIP(hipSetDevice(device));
   sync();
+  drop_graphs();  // they hold the hierarchy's pointers
   levels.clear();
   d_tail = nullptr;
   tail_blob_first = -1;
@@ -1255,9 +1268,20 @@ void Solver::amg_smooth(size_t li, float*& xcur, const float* b, bool x_zero, bo
   if (x_zero) {
     launch_amg_smooth_zero(L.dev, b, L.xt, stream);
   } else if (li == 0 && prof_take()) {
-    const auto ev = prof_pair();
-    launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second, nt);
-    prof_launches++;
+    if (capturing) {  // event nodes of the graph around the launch, read per replay (graph_harvest)
+      hipEvent_t e0, e1;
+      CFD_HIP(hipEventCreate(&e0));
+      capturing->ev.push_back(e0);
+      CFD_HIP(hipEventCreate(&e1));
+      capturing->ev.push_back(e1);
+      CFD_HIP(hipEventRecordWithFlags(e0, stream, hipEventRecordExternal));
+      launch_amg_smooth(L.dev, xcur, b, L.xt, stream, nullptr, nullptr, nt);
+      CFD_HIP(hipEventRecordWithFlags(e1, stream, hipEventRecordExternal));
+    } else {
+      const auto ev = prof_pair();
+      launch_amg_smooth(L.dev, xcur, b, L.xt, stream, ev.first, ev.second, nt);
+      prof_launches++;
+    }
   } else {
     launch_amg_smooth(L.dev, xcur, b, L.xt, stream, nullptr, nullptr, nt);
   }
@@ -1507,6 +1531,102 @@ void Solver::flush_inner() {
   inner.pending = -1;
 }
 
+// FGMRES iteration j (coupled_solver_fgmres.rs:1911-2283): Z_j = M^-1 V_j,
+// w = A Z_j, CGS against V_0..V_j, ||w||, Hessenberg column + Givens.  The
+// residual estimate also lands in pinned host memory at `pin` (natural
+// schedule) -- no host reads in between, so the sequence is graph-capturable.
+void Solver::iteration(int j, float* pin) {
+  float* zj = zvec + (size_t)j * stride;
+  precondition(j, zj);
+  const CommScope cs(this, kCommKrylovHalo);
+  overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
+    CoupledMatrix A = cmat();
+    A.r0 = a;
+    A.r1 = b;
+    A.r2 = a2;
+    A.r3 = b2;
+    launch_spmv(A, zj, w, stream, nullptr, nt(8));
+  });
+  launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
+  launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
+  launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0);
+  launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
+  check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
+}
+
+void Solver::drop_graphs() {
+  if (graphs.empty()) return;
+  sync();
+  for (IterGraph& G : graphs) {
+    graph_harvest(G, false);
+    if (G.exec) CFD_HIP(hipGraphExecDestroy(G.exec));
+    for (auto e : G.ev) CFD_HIP(hipEventDestroy(e));
+  }
+  graphs.clear();
+}
+
+void Solver::graph_harvest(IterGraph& G, bool discard) {
+  if (!G.pending) return;
+  G.pending = false;
+  if (G.ev.empty() || discard) return;
+  CFD_HIP(hipEventSynchronize(G.ev.back()));
+  for (size_t k = 0; k + 1 < G.ev.size(); k += 2) {
+    float ms = 0.0f;
+    CFD_HIP(hipEventElapsedTime(&ms, G.ev[k], G.ev[k + 1]));
+    prof_ms += ms;
+    prof_launches++;
+  }
+}
+
+void Solver::graph_harvest_all(bool discard) {
+  for (IterGraph& G : graphs) graph_harvest(G, discard);
+}
+
+void Solver::run_iteration(int j, float* pin, int variant) {
+  const bool use = graph_on && !dist() && !check_sync && !comm_prof;
+  if (!use) {
+    iteration(j, pin);
+    return;
+  }
+  if (graph_precond != (int)constants.precond_type) {
+    drop_graphs();
+    graph_precond = (int)constants.precond_type;
+  }
+  if (graphs.empty()) graphs.resize(3 * (size_t)m);
+  IterGraph& G = graphs[3 * (size_t)j + variant];
+  if (G.exec && G.prof != prof) {  // timing switched on / off: capture again
+    sync();
+    graph_harvest(G, false);
+    CFD_HIP(hipGraphExecDestroy(G.exec));
+    for (auto e : G.ev) CFD_HIP(hipEventDestroy(e));
+    G = IterGraph{};
+  }
+  if (!G.exec) {
+    hipGraph_t gr = nullptr;
+    CFD_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    capturing = &G;
+    try {
+      iteration(j, pin);
+    } catch (...) {
+      capturing = nullptr;
+      (void)hipStreamEndCapture(stream, &gr);
+      if (gr) (void)hipGraphDestroy(gr);
+      throw;
+    }
+    capturing = nullptr;
+    CFD_HIP(hipStreamEndCapture(stream, &gr));
+    const hipError_t e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    CFD_HIP(e);
+    G.prof = prof;
+    graph_captures++;
+  }
+  graph_harvest(G, false);  // the previous replay's smoother times (complete by now: a solve start synchronised)
+  CFD_HIP(hipGraphLaunch(G.exec, stream));
+  G.pending = true;
+  graph_replays++;
+}
+
 cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   const Range range("fgmres solve");
   // LinearSolverStats.time = start_time.elapsed() on every exit
@@ -1558,27 +1678,11 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       const Range it_range("fgmres iteration");
       basis_size = j + 1;
       ++total;
-      float* zj = zvec + (size_t)j * stride;
-      precondition(j, zj);
-      const CommScope cs(this, kCommKrylovHalo);
-      overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
-        CoupledMatrix A = cmat();
-        A.r0 = a;
-        A.r1 = b;
-        A.r2 = a2;
-        A.r3 = b2;
-        launch_spmv(A, zj, w, stream, nullptr, nt(8));
-      });
-      launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
-      launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-      launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0);
       // the residual estimate goes to one of two pinned slots, never the slot
       // of a lagged read still pending (which may carry over from the previous
       // iteration, restart or solve: the reader is never reset)
       const int wslot = inner.pending == 0 ? 1 : 0;
-      launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist,
-                         fixed ? nullptr : d_pin + 64 + wslot, stream);
-      check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
+      run_iteration(j, fixed ? nullptr : d_pin + 64 + wslot, fixed ? 0 : 1 + wslot);
       if (fixed) continue;
       // async residual read with the lag model (async_buffer.rs)
       flush_inner();

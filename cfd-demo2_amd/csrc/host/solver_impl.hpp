@@ -412,6 +412,36 @@ struct Solver {
   uint64_t prof_seq = 0;
   bool prof_take() { return prof && (prof_seq++ % prof_stride) == 0; }
 
+  // ---- hipGraph replay of the FGMRES iteration (Solver::run_iteration) ----
+  // One executable graph per (basis index j, residual-slot variant): the
+  // iteration's launches (Schur prediction, V-cycle or Jacobi sweeps, Schur
+  // correction, SpMV, CGS, Givens) depend on j only, every pointer they take is
+  // fixed once the Krylov space and the AMG hierarchy exist, so the graph is
+  // captured on first use and replayed by every later solve: one host call per
+  // iteration instead of ~14-20 launches.  Dropped with the hierarchy
+  // (drop_amg) and on a preconditioner switch.  While the level-0 smoother is
+  // being timed (prof) its launches in the graph are bracketed by event nodes
+  // owned by the graph; every replay's times are harvested before the next
+  // replay of that graph (graph_harvest) or when the profile is read.
+  // CFD_GRAPH=1 (or cfd_graph_enable) turns it on for one GPU (R = 1); off by
+  // default: the same-box A/B found replay no faster than eager launches at
+  // C0 and C1 -- the GPU's kernel boundaries, not the host's launch rate,
+  // bound the small-mesh iteration.
+  struct IterGraph {
+    hipGraphExec_t exec = nullptr;
+    std::vector<hipEvent_t> ev;  // timing pairs of the level-0 smoother (prof captures)
+    bool prof = false;           // captured with the timing pairs
+    bool pending = false;        // replayed since the last harvest
+  };
+  bool graph_on = false;
+  std::vector<IterGraph> graphs;   // [3 j + variant]; variant 0 fixed schedule, 1 + pinned residual slot
+  int graph_precond = -1;          // precond_type the graphs were captured for
+  IterGraph* capturing = nullptr;  // the graph being captured (amg_smooth's timing pairs)
+  uint64_t graph_captures = 0, graph_replays = 0;
+  void drop_graphs();
+  void graph_harvest(IterGraph& G, bool discard);
+  void graph_harvest_all(bool discard);  // the stream must be idle
+
   Solver(const cfd_mesh_view& mesh, const cfd_config& cfg, int device,
          std::unique_ptr<Comm> comm = nullptr);
   ~Solver();
@@ -453,6 +483,8 @@ struct Solver {
   std::vector<std::vector<uint32_t>> allgatherv_u32(const std::vector<uint32_t>& mine);  // collective
   void set_amg_full_policy(AmgGpuLevel& G, int li);
   void precondition(int j, float* z);
+  void iteration(int j, float* pin);  // one FGMRES iteration's launches (fixed order, no host reads)
+  void run_iteration(int j, float* pin, int variant);  // eager or graph replay
   void v_cycle();
   void amg_smooth(size_t li, float*& x, const float* b, bool x_zero = false, bool nt = false);
   std::pair<hipEvent_t, hipEvent_t> prof_pair();

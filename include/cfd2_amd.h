@@ -260,6 +260,14 @@ cfd_status cfd_profile_reset(cfd_solver* s);
  * algorithmic bytes per sweep (4(n+1) + 8 nnz + 12 n).       */
 cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t* launches,
                                 double* bytes_per_launch);
+/* hipGraph replay of the FGMRES iteration (one executable graph per basis
+ * index, captured on first use, replayed by every later solve; DESIGN.md
+ * section 5).  enable: 1 on, 0 off (the launches are issued one by one);
+ * default from CFD_GRAPH (1 on), else off: replay measured no faster than
+ * eager launches.  One GPU only.  Same bits either
+ * way.  Stats: graphs captured and iterations replayed so far.             */
+cfd_status cfd_graph_enable(cfd_solver* s, int32_t enable);
+cfd_status cfd_graph_stats(const cfd_solver* s, int32_t* enabled, uint64_t* captures, uint64_t* replays);
 /* AMG hierarchy summary: number of levels and rows/nnz per level.            */
 cfd_status cfd_amg_levels(const cfd_solver* s, int32_t* num_levels, uint32_t* rows /*[20]*/,
                           uint64_t* nnz /*[20]*/);
