@@ -303,6 +303,9 @@ def main():
     ap.add_argument("--amg-rebuild", type=int, default=0,
                     help="rebuild the AMG hierarchy every K steps (opt-in deviation from the reference's "
                          "frozen hierarchy; not the headline configuration)")
+    ap.add_argument("--amg-local", type=int, default=0,
+                    help="1: partition-aware AMG aggregation on the distributed levels (cfd_config."
+                         "amg_local_aggregation; opt-in, no restriction / prolongation halos)")
     ap.add_argument("--mesh-cache", default=None,
                     help="binary mesh file: loaded if present, else generated and saved (A/B runs)")
     args = ap.parse_args()
@@ -395,7 +398,8 @@ def main():
     setup_s = {"mesh": time.perf_counter() - t0}
     log(f"[rank {rank}] mesh {n_global} cells / {mesh.num_faces()} faces in {setup_s['mesh']:.1f}s")
 
-    cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner, amg_rebuild_interval=args.amg_rebuild)
+    cfg = default_config(fixed_outer=args.outer, fixed_inner=args.inner, amg_rebuild_interval=args.amg_rebuild,
+                         amg_local_aggregation=args.amg_local)
     t0 = time.perf_counter()
     # test / rehearsal mode: CFD_DIST_TRANSPORT=host stages every exchange through
     # the gloo process group (several ranks may then share one GPU: CFD_BENCH_DEVICE)
@@ -569,7 +573,8 @@ def main():
             "workload": (f"BASELINE {cfg_label}: channel+obstacle {n_global} cells on {world} GPU(s) (~{n_cells} per rank), "
                          f"fixed schedule {args.outer} Picard x {args.inner} FGMRES/AMG per step"
                          + (f", AMG hierarchy rebuilt every {args.amg_rebuild} step(s) (opt-in deviation)"
-                            if args.amg_rebuild else "")),
+                            if args.amg_rebuild else "")
+                         + (", partition-aware AMG aggregation (opt-in)" if args.amg_local and world > 1 else "")),
             "cells_total": n_global,
             "cells_per_gpu": n_cells if not inproc else n_global,
             "cells_per_rank": n_cells,

@@ -73,6 +73,7 @@ class Config(C.Structure):
         ("fgmres_atol", C.c_float),
         ("log_level", C.c_int32),
         ("amg_rebuild_interval", C.c_int32),
+        ("amg_local_aggregation", C.c_int32),
     ]
 
 
@@ -164,6 +165,7 @@ def default_config(**overrides) -> Config:
         fgmres_atol=1e-7,
         log_level=0,
         amg_rebuild_interval=0,
+        amg_local_aggregation=0,
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)

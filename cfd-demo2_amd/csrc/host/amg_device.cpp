@@ -456,7 +456,25 @@ bool Solver::build_amg_device_dist() {
     std::vector<std::vector<uint32_t>> exp_rows(R);  // own rows (local) that rank s < rk aggregates
     std::vector<uint32_t> imp;                       // upper rows this rank's aggregates took (global)
     std::vector<uint64_t> cpart(R + 1, 0);
-    for (int s = 0; s < R; ++s) {
+    if (amg_local) {
+      // partition-aware mode: the greedy pass over the own rows only (a seed
+      // takes no ghost row), local ids first, then every rank's count gives
+      // the global ids (seed order = rank order, as amg_setup.cpp)
+      uint32_t cnt = 0;
+      for (uint32_t i = 0; i < n; ++i) {
+        if (agg[i] != kNone) continue;
+        agg[i] = cnt;
+        for (uint32_t k = row[i]; k < row[i + 1]; ++k) {
+          const uint32_t c = col[k];
+          if (c >= C0 && c < C1 && agg[c - C0] == kNone) agg[c - C0] = cnt;
+        }
+        ++cnt;
+      }
+      const std::vector<uint64_t> counts = allgather_u64(cnt);
+      for (int q = 0; q < R; ++q) cpart[q + 1] = cpart[q] + counts[q];
+      for (uint32_t& a : agg) a += (uint32_t)cpart[rk];
+    }
+    for (int s = 0; s < R && !amg_local; ++s) {
       std::vector<uint32_t> msg;
       if (s == rk) {
         const uint32_t base = (uint32_t)cpart[s];

@@ -88,7 +88,7 @@ HostCsr spgemm(const HostCsr& a, const HostCsr& b) {
 }  // namespace
 
 uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, const std::vector<uint64_t>& part,
-                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart) {
+                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart, bool local) {
   const uint32_t NONE = std::numeric_limits<uint32_t>::max();
   agg.assign(n, NONE);
   cpart.assign(part.size(), 0);
@@ -96,14 +96,20 @@ uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, co
   // and takes every free neighbour.  Rows before a seed are all taken, so the
   // seed is its aggregate's smallest row and aggregates are numbered in seed
   // order: cpart[q] = first aggregate seeded at or after part[q].
+  // local (partition-aware mode, cfd_config.amg_local_aggregation): a seed
+  // takes only free neighbours of its own part, so no aggregate straddles two
+  // parts -- the same pass over the pattern without its cross-part entries.
   uint32_t nagg = 0;
   size_t q = 0;
   for (size_t i = 0; i < n; ++i) {
     while (q + 1 < part.size() && part[q] <= i) cpart[q++] = nagg;
     if (agg[i] != NONE) continue;
     agg[i] = nagg;
+    // part of row i: [part[q - 1], part[q])
+    const uint64_t lo = q > 0 ? part[q - 1] : 0, hi = q < part.size() ? part[q] : n;
     for (uint32_t k = row[i]; k < row[i + 1]; ++k) {
       const uint32_t j = col[k];
+      if (local && (j < lo || j >= hi)) continue;
       if (agg[j] == NONE) agg[j] = nagg;
     }
     ++nagg;
@@ -124,12 +130,16 @@ void transpose_aggregates(const std::vector<uint32_t>& agg, uint32_t nagg, std::
 }
 
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
-                                               const std::vector<uint64_t>& part0) {
+                                               const std::vector<uint64_t>& part0, bool local, uint64_t rep_rows) {
   std::vector<AmgHostLevel> levels;
   HostCsr cur = fine;
   // row partition of the current level (distributed solver): coarse rows
   // follow their seeds (seed order = rank order)
   std::vector<uint64_t> part = part0.empty() ? std::vector<uint64_t>{0, (uint64_t)fine.rows} : part0;
+  // partition-aware mode: the row-partitioned levels (level 0 and every next
+  // level of more than rep_rows rows) aggregate per part; from the first
+  // replicated level on, the global pass
+  bool local_level = local && part.size() > 2;
   for (size_t li = 0; li < max_levels; ++li) {
     AmgHostLevel L;
     L.part = part;
@@ -138,7 +148,7 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
     if (li < max_levels - 1 && n > 100) {
       std::vector<uint32_t> agg;
       std::vector<uint64_t> cpart;
-      const uint32_t nagg = aggregate_greedy(n, cur.row.data(), cur.col.data(), part, agg, cpart);
+      const uint32_t nagg = aggregate_greedy(n, cur.row.data(), cur.col.data(), part, agg, cpart, local_level);
       if (nagg < n) {
         // P (n x nagg) and R = P^T as CSR with unit values
         HostCsr P, R;
@@ -172,6 +182,7 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
         L.A = std::move(cur);
         cur = std::move(next);
         part = std::move(cpart);
+        local_level = local_level && nagg > rep_rows;
         coarsened = true;
       }
     }

@@ -69,6 +69,7 @@ void cfd_config_default(cfd_config* c) {
   c->fgmres_atol = 1e-7f;
   c->log_level = 0;
   c->amg_rebuild_interval = 0;
+  c->amg_local_aggregation = 0;
 }
 
 cfd_status cfd_solver_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,

@@ -95,6 +95,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   cgs_keep_bytes = N < (1u << 22) ? (size_t)64 << 20 : 0;  // (kernels.hip CFD_CGS_SER_MIN_CELLS)
   if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  amg_local = dist() && cfg.amg_local_aggregation != 0;
   {
     const char* ge = std::getenv("CFD_GRAPH");
     // opt-in: replay measured no faster than eager launches on this pool
@@ -765,7 +766,7 @@ void Solver::build_amg_host() {
     CFD_HIP(hipMemcpyAsync(A0.val.data(), d_vals, nnz_all * 4, hipMemcpyDeviceToHost, stream));
     sync();
     for (uint32_t i = 0; i < NG; ++i) A0.row[i + 1] = A0.row[i] + lens[i];
-    H = build_amg_hierarchy(A0, kMaxAmgLevels, starts);
+    H = build_amg_hierarchy(A0, kMaxAmgLevels, starts, amg_local, amg_replicate_rows());
   }
   const int L = (int)H.size();
   // distributed levels [0, amg_g): the rest are replicated (all of them on one GPU)
@@ -1373,12 +1374,17 @@ void Solver::v_cycle() {
       const uint32_t cg_lo = into_dist ? C.glo : (uint32_t)C.C0;
       const uint32_t cg_hi = into_dist ? C.ghi : (uint32_t)(C.nglob - C.C1);
       float* so = into_dist ? smo : nullptr;
-      const uint32_t split = Lv.dev.n >= overlap_min_rows ? Lv.rc_hi : 0u;  // as overlapped()
-      const CommScope cs(this, amg_cat(i));
-      halo_begin(Lv.plan, {{Lv.r, 1}});
-      if (split > 0) launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false);
-      halo_end();
-      launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, split, Lv.dev.nc, true);
+      if (amg_local) {  // partition-aware: every member is owned, no residual halo
+        launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, Lv.dev.nc, true);
+      } else {
+        const uint32_t split = Lv.dev.n >= overlap_min_rows ? Lv.rc_hi : 0u;  // as overlapped()
+        const CommScope cs(this, amg_cat(i));
+        halo_begin(Lv.plan, {{Lv.r, 1}});
+        if (split > 0)
+          launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, 0, split, false);
+        halo_end();
+        launch_amg_restrict(Lv.dev, Lv.r, cb, cx, sc, cg_lo, cg_hi, stream, so, C.dev.de, split, Lv.dev.nc, true);
+      }
     }
     if (Lv.dist && !C.dist) {  // into the first replicated level: own slice, all-gather
       std::vector<size_t> off(R + 1);
@@ -1399,7 +1405,10 @@ void Solver::v_cycle() {
   }
   for (int ii = down - 1; ii >= 0; --ii) {
     // the prolongation reads aggregates seeded on lower ranks (ghosts of the coarse x)
-    if (levels[ii + 1].dist) {  // the rows of owned aggregates overlap the coarse-x exchange
+    if (levels[ii + 1].dist && amg_local) {  // partition-aware: every fine row's aggregate is owned
+      AmgGpuLevel& F = levels[ii];
+      launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, F.dev.n, nt(32));
+    } else if (levels[ii + 1].dist) {  // the rows of owned aggregates overlap the coarse-x exchange
       AmgGpuLevel& F = levels[ii];
       const uint32_t split = F.dev.n >= overlap_min_rows ? F.pf_lo : F.dev.n;  // as overlapped()
       const CommScope cs(this, amg_cat(ii + 1));

@@ -152,14 +152,18 @@ struct AmgHostLevel {
   bool has_op = false;
   std::vector<uint64_t> part;  // row partition starts of this level (one entry per rank + 1)
 };
+// local: partition-aware aggregation of the row-partitioned levels (those of
+// more than rep_rows rows from level 0 on; cfd_config.amg_local_aggregation)
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
-                                               const std::vector<uint64_t>& part = {});
+                                               const std::vector<uint64_t>& part = {}, bool local = false,
+                                               uint64_t rep_rows = 0);
 // Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
 // n rows; returns the aggregate count, agg[i] = aggregate of row i, and
 // cpart = the aggregate partition induced by the row partition `part` (an
-// aggregate belongs to the part of its seed, its smallest row).
+// aggregate belongs to the part of its seed, its smallest row).  local: a
+// seed takes only neighbours of its own part (no aggregate straddles parts).
 uint32_t aggregate_greedy(size_t n, const uint32_t* row, const uint32_t* col, const std::vector<uint64_t>& part,
-                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart);
+                          std::vector<uint32_t>& agg, std::vector<uint64_t>& cpart, bool local = false);
 // R = P^T of piecewise-constant P: rows = aggregates, fine indices ascending
 void transpose_aggregates(const std::vector<uint32_t>& agg, uint32_t nagg, std::vector<uint32_t>& r_row,
                           std::vector<uint32_t>& r_col);
@@ -235,6 +239,10 @@ struct Solver {
   StateView evrec{};             // check_evolution records fetched from their owners
   uint64_t ev_a = 0, ev_b = 0;   // record range [ev_a, ev_b) this rank's variance reads
   int amg_g = 0;                 // first replicated AMG level (distributed)
+  // partition-aware hierarchy (cfg.amg_local_aggregation on a distributed
+  // solver): the distributed levels' aggregates never straddle ranks, so the
+  // restriction and the prolongation of those levels need no halo
+  bool amg_local = false;
   int m = 50, m1 = 51;
   uint32_t nchunks = 0;
 

@@ -142,6 +142,17 @@ typedef struct cfd_config {
   int32_t amg_rebuild_interval; /* 0: AMG hierarchy frozen after the first AMG solve
                                    (reference, amg.rs); k > 0: rebuilt from the current
                                    matrix every k steps (opt-in deviation) */
+  int32_t amg_local_aggregation; /* distributed solver only.  0 (default): the GLOBAL
+                                   hierarchy -- the reference's greedy index-order
+                                   aggregation over the whole mesh, aggregates may
+                                   straddle ranks, R ranks give one GPU's bits.  1:
+                                   partition-aware -- each row-partitioned level is
+                                   aggregated over the rank's own rows only (cross-rank
+                                   entries ignored by the greedy pass):
+                                   block-diagonal P / R, so the restriction and the
+                                   prolongation need no halo; the hierarchy (and the
+                                   bits) then depend on the rank count, and match the
+                                   oracle run with the same rank count and mode       */
 } cfd_config;
 
 void cfd_config_default(cfd_config* cfg);

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -64,6 +65,14 @@ inline RedGeom red_geom(size_t n) {
   r.nchunks = (n + kChunkCells - 1) / kChunkCells;
   r.nseg = (r.nchunks + r.G - 1) / r.G;
   return r;
+}
+
+// Rows of a level the distributed solver keeps row-partitioned at most
+// (Solver's amg_replicate_rows(), solver_impl.hpp: CFD_AMG_REPLICATE_ROWS,
+// default 2^20): the partition-aware mode aggregates those levels per rank.
+inline uint64_t replicate_rows() {
+  const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
+  return ev ? std::strtoull(ev, nullptr, 10) : (1ull << 20);
 }
 
 // pairwise tree over v[0, n), n a power of two: ((v0 + v1) + (v2 + v3)) + ...
@@ -205,19 +214,34 @@ struct AmgLevel {
 // amg.rs:84-116: greedy, index order, no strength test.  The distributed
 // solver runs this same global pass (its hierarchy does not depend on the
 // rank count).
-void aggregate(const Csr& m, std::vector<size_t>& agg, size_t& nagg) {
+// part (partition-aware mode, cfd_config.amg_local_aggregation):
+// the row partition of the level; a seed takes only free neighbours inside its
+// own part, so no aggregate straddles two ranks.  cpart: the coarse partition
+// (aggregate ids are seed order, hence rank by rank).
+void aggregate(const Csr& m, std::vector<size_t>& agg, size_t& nagg, const std::vector<uint64_t>* part = nullptr,
+               std::vector<uint64_t>* cpart = nullptr) {
   const size_t n = m.rows, NONE = std::numeric_limits<size_t>::max();
   agg.assign(n, NONE);
   nagg = 0;
+  size_t q = 0;  // part of row i: [(*part)[q], (*part)[q + 1])
+  if (cpart) cpart->assign(part->size(), 0);
   for (size_t i = 0; i < n; ++i) {
+    if (part)
+      while ((*part)[q + 1] <= i) {
+        ++q;
+        (*cpart)[q] = nagg;
+      }
     if (agg[i] != NONE) continue;
     agg[i] = nagg;
     for (uint32_t k = m.row[i]; k < m.row[i + 1]; ++k) {
       const size_t j = m.col[k];
+      if (part && (j < (*part)[q] || j >= (*part)[q + 1])) continue;
       if (j != i && agg[j] == NONE) agg[j] = nagg;
     }
     ++nagg;
   }
+  if (cpart)
+    for (++q; q < part->size(); ++q) (*cpart)[q] = nagg;
 }
 
 Csr build_prolongation(const std::vector<size_t>& agg, size_t nagg, size_t nf) {  // :118-139
@@ -300,8 +324,14 @@ struct Amg {
   std::vector<AmgLevel> levels;
   int sem = 0;  // kSemInplaceSmoother | kSemRestrictClamp
 
-  void build(const Csr& fine, size_t max_levels) {  // amg.rs:246-595
+  // part / rep_rows: partition-aware mode on a distributed run -- the levels
+  // the solver keeps row-partitioned (level 0, then every next level of more
+  // than rep_rows rows; Solver::build_amg_device_dist) aggregate rank by rank,
+  // from the first replicated level on the global pass (empty part: global)
+  void build(const Csr& fine, size_t max_levels, std::vector<uint64_t> part = {},
+             uint64_t rep_rows = 0) {  // amg.rs:246-595
     Csr cur = fine;
+    bool local = part.size() > 2;
     for (size_t li = 0; li < max_levels; ++li) {
       AmgLevel L;
       L.n = cur.rows;
@@ -313,7 +343,15 @@ struct Amg {
       if (li < max_levels - 1 && L.n > 100) {
         std::vector<size_t> agg;
         size_t nagg;
-        aggregate(cur, agg, nagg);
+        std::vector<uint64_t> cpart;
+        if (local)
+          aggregate(cur, agg, nagg, &part, &cpart);
+        else
+          aggregate(cur, agg, nagg);
+        if (local) {
+          part = cpart;
+          local = nagg > rep_rows;
+        }
         if (nagg < L.n) {
           L.P = build_prolongation(agg, nagg, L.n);
           L.R = transpose(L.P);
@@ -1194,7 +1232,10 @@ cfd_linear_stats solve(oracle_solver* s) {
   if (s->constants.precond_type == 1 && !s->amg) {  // ensure_amg_resources (:174-209), frozen copy
     s->amg.reset(new Amg);
     s->amg->sem = s->sem;
-    s->amg->build(s->scalar, 20);
+    if (s->cfg.amg_local_aggregation && s->starts.size() > 2)
+      s->amg->build(s->scalar, 20, s->starts, replicate_rows());
+    else
+      s->amg->build(s->scalar, 20);
     s->amg_age = 0;
   }
   const float rhs_norm = std::sqrt(dist_dot(s->rhs.data(), s->rhs.data(), s->starts, s->sem));
@@ -1532,8 +1573,21 @@ oracle_solver* oracle_create_dist(const cfd_mesh_view* mesh, const cfd_config* c
   auto* s = new oracle_solver;
   s->cfg = *cfg;
   s->m = cfg->max_restart > 0 ? cfg->max_restart : 50;
-  s->starts.resize(nranks + 1);
-  for (int r = 0; r <= nranks; ++r) s->starts[r] = (uint64_t)mesh->num_cells * (uint64_t)r / (uint64_t)nranks;
+  // the distributed solver's partition (csrc/host/dist.cpp partition_starts):
+  // whole reduction segments per rank.  Only the partition-aware AMG mode
+  // depends on it; every other result is rank-count invariant.
+  // (more ranks than segments -- a partition the solver refuses -- falls back
+  // to equal cell ranges)
+  {
+    const RedGeom g = red_geom(mesh->num_cells);
+    const uint64_t seg_cells = (uint64_t)kChunkCells * g.G, nc = mesh->num_cells;
+    s->starts.resize(nranks + 1);
+    for (int r = 0; r <= nranks; ++r)
+      s->starts[r] = (size_t)nranks <= g.nseg
+                         ? std::min<uint64_t>(nc, seg_cells * ((uint64_t)g.nseg * (uint64_t)r / (uint64_t)nranks))
+                         : nc * (uint64_t)r / (uint64_t)nranks;
+    s->starts[nranks] = nc;
+  }
   if (!build(s, mesh)) {
     delete s;
     return nullptr;

@@ -12,6 +12,7 @@
 // use-after-free, overflow or other UB aborts the run with a report.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../cfd-demo2_amd/csrc/mesh/mesh.hpp"
@@ -39,7 +40,7 @@ cfd_mesh_view view_of(const cfd2::Mesh& x) {
   return v;
 }
 
-int run(const char* name, const cfd2::Mesh& m, int nranks, uint32_t precond, uint32_t scheme) {
+int run(const char* name, const cfd2::Mesh& m, int nranks, uint32_t precond, uint32_t scheme, int local = 0) {
   cfd_config cfg{};
   cfg.n_outer_correctors = 20;
   cfg.convergence_lag = 1;
@@ -50,6 +51,7 @@ int run(const char* name, const cfd2::Mesh& m, int nranks, uint32_t precond, uin
   cfg.fgmres_rtol = 1e-5f;
   cfg.fgmres_atol = 1e-7f;
   cfg.amg_rebuild_interval = 2;
+  cfg.amg_local_aggregation = local;
   const cfd_mesh_view v = view_of(m);
   oracle_solver* s = oracle_create_dist(&v, &cfg, nranks);
   if (!s) {
@@ -79,8 +81,8 @@ int run(const char* name, const cfd2::Mesh& m, int nranks, uint32_t precond, uin
   for (double x : uv)
     if (!std::isfinite(x)) rc = 1;
   oracle_destroy(s);
-  std::printf("%s: %u cells, %d rank(s), precond %u, scheme %u: %s\n", name, n, nranks, precond, scheme,
-              rc ? "FAILED" : "ok");
+  std::printf("%s: %u cells, %d rank(s)%s, precond %u, scheme %u: %s\n", name, n, nranks,
+              local ? " (partition-aware AMG)" : "", precond, scheme, rc ? "FAILED" : "ok");
   return rc;
 }
 
@@ -100,5 +102,8 @@ int main() {
     rc |= run("voronoi channel", b, nr, 1, 0);
     rc |= run("delaunay channel", c, nr, 0, 2);
   }
+  setenv("CFD_AMG_REPLICATE_ROWS", "40", 1);  // distributed coarse levels on these small meshes
+  rc |= run("cut-cell step", a, 3, 1, 1, 1);
+  rc |= run("voronoi channel", b, 2, 1, 0, 1);
   return rc;
 }

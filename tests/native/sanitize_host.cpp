@@ -97,6 +97,14 @@ void run(const char* name, const cfd2::Mesh& m) {
         A.val[k] = g.scol[k] == i ? (float)(g.srow[i + 1] - g.srow[i]) : -1.0f;
     const auto H = cfd2::build_amg_hierarchy(A, 20, starts);
     check(!H.empty() && H[0].A.rows == n, "empty hierarchy");
+    {  // partition-aware mode: no aggregate of a partitioned level straddles two parts
+      const auto HL = cfd2::build_amg_hierarchy(A, 20, starts, true, 40);
+      for (size_t l = 0; l + 1 < HL.size() && HL[l].A.rows > 40; ++l)
+        for (int q = 0; q < R; ++q)
+          for (uint64_t i = HL[l].part[q]; i < HL[l].part[q + 1]; ++i)
+            check(HL[l].agg[i] >= HL[l + 1].part[q] && HL[l].agg[i] < HL[l + 1].part[q + 1],
+                  "partition-aware aggregate straddles ranks");
+    }
     for (size_t l = 0; l + 1 < H.size(); ++l)
       check(H[l].has_op && H[l + 1].A.rows == H[l].nc, "level sizes");
     for (size_t l = 0; l < H.size(); ++l) {  // coarse rows follow their seeds: a partition in rank order

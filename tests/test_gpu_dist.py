@@ -265,3 +265,93 @@ def test_comm_timing_categories_and_bits(replicate_rows):
         assert r.comm_timing() == []
     grp.close()
     one.close()
+
+
+# ---- partition-aware aggregation (cfd_config.amg_local_aggregation) --------
+# "aggregation restricted to owned rows (block-diagonal P/R,
+# local restriction and prolongation)".  Opt-in: the hierarchy then depends on
+# the rank count, so the bar is GpuGroup(R, local) == OracleSolver(R, local),
+# bit for bit (the oracle runs the same per-rank greedy pass on the same
+# partition), and the V-cycle drops the residual and coarse-x halos of every
+# distributed level.
+
+@pytest.mark.parametrize("nranks,rep,which", [(2, 50, "amg_test"), (4, 120, "amg_test"), (8, 4096, "bench_100k"),
+                                              (2, 262144, "c1"), (8, 4096, "c1")])
+def test_group_local_aggregation_parity(nranks, rep, which, replicate_rows):
+    replicate_rows(rep)
+    if which == "amg_test":
+        mesh = backwards_step()
+        cfg = dict(amg_local_aggregation=1)
+        setup = lambda s: _setup_amg_test(s, mesh, 1)  # noqa: E731
+        steps = 4
+    else:
+        mesh = bench_mesh(0.0055, 30) if which == "bench_100k" else bench_mesh(0.001723, 100)
+        cfg = dict(amg_local_aggregation=1, fixed_outer=1, fixed_inner=6)
+        setup = lambda s: _bench_physics(s, 0.05)  # noqa: E731
+        steps = 2
+    g = GpuGroup(mesh, nranks, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
+    glob = OracleSolver(mesh, config=default_config(**{**cfg, "amg_local_aggregation": 0}), nranks=nranks)
+    for s in (g, o, glob):
+        setup(s)
+    for k in range(steps):
+        for s in (g, o, glob):
+            s.step()
+        _assert_same_fields(g, o, f"local {which} R={nranks} vs oracle(R, local), step {k}")
+        _assert_same_info(g, o, f"local {which} R={nranks} vs oracle(R, local), step {k}")
+    # a different hierarchy from the global one (the mode did something), the
+    # same depth on every rank as the oracle's, level 0 split over the ranks,
+    # the coarsest level replicated
+    ol = o.amg_levels()
+    assert ol != glob.amg_levels()
+    for r in g.ranks:
+        rl = r.amg_levels()
+        assert len(rl) == len(ol) and rl[-1] == ol[-1], (rl, ol)
+    assert sum(r.amg_levels()[0][0] for r in g.ranks) == ol[0][0]
+    g.close()
+
+
+@pytest.mark.parametrize("nranks,rep,which", [(3, 50, "amg_test"), (8, 4096, "c1")])
+def test_group_local_aggregation_host_setup(nranks, rep, which, replicate_rows, monkeypatch):
+    """Partition-aware mode: the device setup (per-rank greedy pass, no
+    imported member rows) builds the host setup's level images byte for byte."""
+    replicate_rows(rep)
+    mesh = backwards_step() if which == "amg_test" else bench_mesh(0.001723, 100)
+    cfg = default_config(fixed_outer=1, fixed_inner=6, amg_local_aggregation=1)
+    groups = {}
+    for path in ("host", "device"):
+        monkeypatch.setenv("CFD_AMG_SETUP", path)
+        g = GpuGroup(mesh, nranks, config=cfg)
+        _bench_physics(g, 0.05)
+        g.step()
+        groups[path] = g
+    monkeypatch.delenv("CFD_AMG_SETUP")
+    h, d = groups["host"], groups["device"]
+    for r in range(nranks):
+        assert h.ranks[r].amg_levels() == d.ranks[r].amg_levels(), f"rank {r}"
+        assert h.ranks[r].amg_setup_info()[1] == d.ranks[r].amg_setup_info()[1], f"rank {r} digests"
+    d.step()
+    h.step()
+    _assert_same_fields(d, h, f"local {which} R={nranks} device vs host setup")
+    h.close()
+    d.close()
+
+
+def test_group_local_aggregation_fewer_exchanges(replicate_rows):
+    """The partition-aware mode removes two halo exchanges per distributed
+    level and V-cycle (the residual before the restriction, the coarse x
+    before the prolongation): exchanges per FGMRES iteration, global vs local."""
+    replicate_rows(4096)
+    mesh = bench_mesh(0.0055, 30)
+    per_it = {}
+    for local in (0, 1):
+        g = GpuGroup(mesh, 4, config=default_config(fixed_outer=1, fixed_inner=8, amg_local_aggregation=local))
+        _bench_physics(g, 0.05)
+        g.step()
+        for r in g.ranks:
+            r.comm_stats(reset=True)
+        g.step()
+        its = g.step_info().total_linear_iterations
+        per_it[local] = max(r.comm_stats()["exchanges"] for r in g.ranks) / its
+        g.close()
+    assert per_it[1] < per_it[0], per_it

@@ -238,3 +238,59 @@ def test_amg_rebuild_interval_changes_only_later_steps():
     # assembled matrices -- the AMG sources -- coincide; step 4 reads step 1's
     assert all(np.array_equal(runs[0][j], runs[1][j]) for j in range(3))
     assert not np.array_equal(runs[0][4], runs[1][4])
+
+
+def _partition(n, nranks):
+    """csrc/host/dist.cpp partition_starts: whole reduction segments per rank."""
+    g = 0
+    while g < 8 and (n >> (g + 1)) >= 16384:
+        g += 1
+    seg = 256 << g
+    nseg = ((n + 255) // 256 + (1 << g) - 1) >> g
+    s = [min(n, seg * (nseg * r // nranks)) for r in range(nranks + 1)]
+    s[-1] = n
+    return s
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_oracle_local_aggregation(nranks, monkeypatch):
+    """Partition-aware AMG mode of the oracle (cfd_config.amg_local_aggregation):
+    level 1 has exactly the aggregates of the greedy index-order pass run on
+    each rank's own rows with the cross-rank entries dropped (restated here on
+    the mesh's face list, init/mesh.rs:27-53 + amg.rs:84-116); the run stays
+    finite; one rank, or the mode off, gives the global hierarchy."""
+    monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "50")
+    mesh = backwards_step()
+    n = mesh.num_cells()
+    a = mesh.arrays()
+    own, nb = a["face_owner"].astype(np.int64), a["face_neighbor"].astype(np.int64)
+    inner = (nb < n) & (nb != own)
+    adj = [set([i]) for i in range(n)]
+    for p, q in zip(own[inner], nb[inner]):
+        adj[p].add(q)
+        adj[q].add(p)
+    starts = _partition(n, nranks)
+    nagg = 0
+    for r in range(nranks):
+        lo, hi = starts[r], starts[r + 1]
+        agg = {}
+        for i in range(lo, hi):
+            if i in agg:
+                continue
+            agg[i] = nagg
+            for j in sorted(adj[i]):
+                if lo <= j < hi and j not in agg:
+                    agg[j] = nagg
+            nagg += 1
+    sols = {}
+    for key, cfg, R in (("local", 1, nranks), ("global", 0, nranks), ("local1", 1, 1)):
+        s = OracleSolver(mesh, config=default_config(amg_local_aggregation=cfg), nranks=R)
+        setup_amg_test(s, mesh, 1)
+        for _ in range(3):
+            s.step()
+        p = s.get_p()
+        assert np.all(np.isfinite(p))
+        sols[key] = (s.amg_levels(), p)
+    assert sols["local"][0][1][0] == nagg, (sols["local"][0][:2], nagg)
+    assert sols["local"][0] != sols["global"][0]
+    assert sols["local1"][0] == sols["global"][0] and np.array_equal(sols["local1"][1], sols["global"][1])
