@@ -296,6 +296,12 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
 // keep_bytes > 0: the last blocks (their j + 2 vectors within keep_bytes) read
 // the basis with the default policy, for a top-down update (rev) after it
+// SpMV fused with the CGS dots (one GPU): y = A x, and chunk partials of
+// <y, V_ii>, ii = 0..j, into cpart[ii * cstride + chunk] (k_cgs_reduce with
+// G = chunks per segment)
+void launch_spmv_dots(const CoupledMatrix& A, const float* x, float* y, const float* basis, const float* binv,
+                      size_t stride, int j, float* cpart, uint32_t cstride, hipStream_t s, bool nt,
+                      size_t keep_bytes);
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
                      uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes = 0);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
@@ -311,7 +317,7 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 // r_in = binv[j] * W_j
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
-                            float* p_prev, hipStream_t s, bool nt = false);
+                            float* p_prev, hipStream_t s, bool nt = false, bool dma = false);
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
