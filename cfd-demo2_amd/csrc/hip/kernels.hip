@@ -1573,7 +1573,8 @@ __device__ __forceinline__ void dma_tile(const CoupledMatrix& A, const float* w_
                                          uint32_t i0, char* slot, uint32_t w, uint32_t lane) {
   for (uint32_t p = w; p < kDmaPieces; p += kDmaLoadWaves) {
     const char* base;
-    const char* end;  // last valid byte + 1 of the array (reads are clamped below it)
+    const char* end;  // end of the array's padded rows, 16-byte aligned (ld is a multiple of 64):
+                      // a clamped read never cuts a 16-byte chunk that still holds valid bytes
     uint32_t q;       // piece within the array's tile image
     if (p < 40) {
       const uint32_t u = p / 8;
@@ -1583,7 +1584,7 @@ __device__ __forceinline__ void dma_tile(const CoupledMatrix& A, const float* w_
     } else if (p < 52) {
       q = p - 40;
       base = reinterpret_cast<const char*>(w_in + 3 * (size_t)i0);
-      end = reinterpret_cast<const char*>(w_in + 3 * (size_t)A.N);
+      end = reinterpret_cast<const char*>(w_in + 3 * (size_t)A.ld);  // vectors are padded to ld rows
     } else if (p < 60) {
       q = p - 52;
       base = reinterpret_cast<const char*>(A.cdiag2 + i0);
@@ -1591,7 +1592,7 @@ __device__ __forceinline__ void dma_tile(const CoupledMatrix& A, const float* w_
     } else if (p < 64) {
       q = p - 60;
       base = reinterpret_cast<const char*>(dinv_p + i0);
-      end = reinterpret_cast<const char*>(dinv_p + A.N);
+      end = reinterpret_cast<const char*>(dinv_p + A.ld);
     } else if (p < 66) {
       q = p - 64;
       base = reinterpret_cast<const char*>(A.lg + i0);
@@ -1601,7 +1602,7 @@ __device__ __forceinline__ void dma_tile(const CoupledMatrix& A, const float* w_
       base = reinterpret_cast<const char*>(A.drank + i0);
       end = reinterpret_cast<const char*>(A.drank + A.ld);
     }
-    const char* last = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(end - 16) & ~(uintptr_t)15);
+    const char* last = end - 16;
     const char* src = base + q * 1024u + lane * 16u;
     if (src > last) src = last;
     __builtin_amdgcn_global_load_lds(src, slot + p * 1024u, 16, 0, NT ? 2 : 0);
@@ -1895,6 +1896,20 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
     }
   }
   [[maybe_unused]] int ag[kU][4];
+  [[maybe_unused]] const bool aggc = PRO && L.aggc != nullptr;
+  if constexpr (PRO) {
+    if (aggc) {  // the slots' aggregates from the static image, issued with the slot values
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const size_t off = (size_t)min(r0 + u, rmax) * L.stride + i0;
+        const int4 a = ldv<NT, int4>(reinterpret_cast<const int4*>(L.aggc + off));
+        ag[u][0] = a.x;
+        ag[u][1] = a.y;
+        ag[u][2] = a.z;
+        ag[u][3] = a.w;
+      }
+    }
+  }
   if constexpr (ALWAYS && MODE == 1) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -1904,11 +1919,13 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       xg[u][2] = q.z;
       xg[u][3] = q.w;
       if constexpr (PRO) {
-        const i4u a = *reinterpret_cast<const i4u*>(L.agg + c[u][0]);
-        ag[u][0] = a.x;
-        ag[u][1] = a.y;
-        ag[u][2] = a.z;
-        ag[u][3] = a.w;
+        if (!aggc) {
+          const i4u a = *reinterpret_cast<const i4u*>(L.agg + c[u][0]);
+          ag[u][0] = a.x;
+          ag[u][1] = a.y;
+          ag[u][2] = a.z;
+          ag[u][3] = a.w;
+        }
       }
     }
 #pragma unroll
@@ -1917,7 +1934,8 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
           xg[u][k] = x[c[u][k]];
-          if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
+          if constexpr (PRO)
+            if (!aggc) ag[u][k] = (int)L.agg[c[u][k]];
         }
       }
   } else {
@@ -1927,7 +1945,8 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       for (int k = 0; k < 4; ++k) {
         xg[u][k] = gat<ALWAYS && MODE == 1>(r0 + u < u4(ln, k), x + c[u][k]);
         // unused slots hold the row's own (valid) column: agg of a real or padding row
-        if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
+        if constexpr (PRO)
+          if (!aggc) ag[u][k] = (int)L.agg[c[u][k]];
       }
   }
   if constexpr (PRO) {
@@ -2214,9 +2233,14 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
     if (sm_out) dec = sm_de[I0 + threadIdx.x];
   }
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
+    // matrix row from the R-ordered image (indexed by p: issued with the
+    // member index, one dependent round trip fewer than through f)
+    // (CFD_AMG_RR_PERM=0: rr_val null, the rows read through f)
     const uint32_t f = L.r_col[p];
-    const uint32_t len = L.len[f], dr = L.drank[f];
-    const float xf = x[f], dvf = L.dv[f];
+    const bool perm = L.rr_val != nullptr;
+    const uint32_t len = perm ? L.rr_len[p] : L.len[f], dr = perm ? L.rr_dr[p] : L.drank[f];
+    const float dvf = perm ? L.rr_dv[p] : L.dv[f];
+    const float xf = x[f];
     float ax = 0.0f;
     uint32_t r0 = 0;
     for (; r0 < len; r0 += 4) {
@@ -2224,9 +2248,15 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
       int c[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const size_t off = (size_t)min(r0 + u, w - 1u) * L.stride + f;
-        v[u] = L.val[off];
-        c[u] = D16 ? (int)f + (int)L.col16[off] : L.col32[off];
+        if (perm) {
+          const size_t off = (size_t)min(r0 + u, w - 1u) * L.rr_ld + p;
+          v[u] = L.rr_val[off];
+          c[u] = L.rr_col[off];
+        } else {
+          const size_t off = (size_t)min(r0 + u, w - 1u) * L.stride + f;
+          v[u] = L.val[off];
+          c[u] = D16 ? (int)f + (int)L.col16[off] : L.col32[off];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) xg[u] = x[c[u]];
@@ -2942,6 +2972,38 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float*
   if (n)
     hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
                        sm_out, sm_de, I0, I1);
+}
+__global__ void __launch_bounds__(kBlock) k_aggc_pack(AmgLevelDev L, int32_t* aggc) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= L.stride) return;
+  const uint32_t w = (uint32_t)max(L.w, 1);
+  for (uint32_t r = 0; r < w; ++r) {
+    const size_t off = (size_t)r * L.stride + i;
+    const int32_t c = L.use16 ? (int32_t)i + (int32_t)L.col16[off] : L.col32[off];
+    aggc[off] = (int32_t)L.agg[c];
+  }
+}
+void launch_aggc_pack(const AmgLevelDev& L, int32_t* aggc, hipStream_t s) {
+  if (L.stride)
+    hipLaunchKernelGGL(k_aggc_pack, dim3((unsigned)((L.stride + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, L, aggc);
+}
+__global__ void __launch_bounds__(kBlock) k_rr_pack(AmgLevelDev L, uint32_t nm) {
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= nm) return;
+  const uint32_t f = L.r_col[p];
+  const uint32_t w = (uint32_t)max(L.w, 1);
+  const_cast<uint8_t*>(L.rr_len)[p] = L.len[f];
+  const_cast<uint8_t*>(L.rr_dr)[p] = L.drank[f];
+  const_cast<float*>(L.rr_dv)[p] = L.dv[f];
+  for (uint32_t r = 0; r < w; ++r) {
+    const size_t off = (size_t)r * L.stride + f, o2 = (size_t)r * L.rr_ld + p;
+    const_cast<float*>(L.rr_val)[o2] = L.val[off];
+    const_cast<int32_t*>(L.rr_col)[o2] = L.use16 ? (int32_t)f + (int32_t)L.col16[off] : L.col32[off];
+  }
+}
+void launch_rr_pack(const AmgLevelDev& L, hipStream_t s) {
+  if (!L.rr_agg || !L.rr_val || !L.nc) return;
+  hipLaunchKernelGGL(k_rr_pack, dim3((unsigned)((L.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, L, L.n);
 }
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* cb, float* cx,
                             float* sm_out, const float* sm_de, hipStream_t s) {

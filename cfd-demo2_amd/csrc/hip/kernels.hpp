@@ -231,6 +231,21 @@ struct AmgLevelDev {
   // k_amg_resrestrict: aggregates per block (0: the level keeps the separate
   // residual + restriction kernels); every block's members fit kRRCap
   uint32_t rr_agg;
+  // ... and the level's rows in R order (member p = r_col[p]): length,
+  // diagonal rank and value, slots [r * rr_ld + p] with ABSOLUTE columns
+  // (k_rr_pack; rebuilt by a numeric re-setup), so a block's matrix loads
+  // depend only on p, not on the member row index loaded first
+  // post-smoother with the prolongation fused (k_amg_smooth<..., PRO>): the
+  // aggregate of every slot's column, [r * stride + i] (k_aggc_pack; pattern
+  // only), so the coarse values are gathered beside x instead of after a
+  // dependent agg gather (null: gathered through agg)
+  const int32_t* aggc;
+  uint32_t rr_ld;
+  const uint8_t* rr_len;
+  const uint8_t* rr_dr;
+  const float* rr_dv;
+  const float* rr_val;
+  const int32_t* rr_col;
 };
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
 // zeroed entries after every level's agg array: the fused prolongation reads
@@ -378,6 +393,10 @@ void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, c
 // residual + restriction fused (k_amg_resrestrict; L.rr_agg > 0, replicated
 // or single-GPU level): coarse_b = R (b - A x), coarse_x cleared or the
 // coarse zero-x pre-smoother written to sm_out (as launch_amg_restrict)
+// the R-ordered member image of a level (AmgLevelDev::rr_*), from its level image
+void launch_rr_pack(const AmgLevelDev& L, hipStream_t s);
+// AmgLevelDev::aggc of a level from its columns and agg
+void launch_aggc_pack(const AmgLevelDev& L, int32_t* aggc, hipStream_t s);
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* coarse_b, float* coarse_x,
                             float* sm_out, const float* sm_de, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,

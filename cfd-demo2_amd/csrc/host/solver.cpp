@@ -1083,6 +1083,22 @@ void Solver::ensure_amg() {
       if (tail_blob_first >= 0) tail_first = t;
     }
   }
+  // fused post-smoothers of the latency-bound levels: the aggregates of the
+  // slots' columns as a static image (AmgLevelDev::aggc, pattern only: a
+  // numeric re-setup keeps it), CFD_AMG_AGGC_ROWS (default 2^18) rows at most
+  {
+    const char* ae = std::getenv("CFD_AMG_AGGC_ROWS");
+    const uint64_t aggc_rows = ae ? std::strtoull(ae, nullptr, 10) : (1ull << 18);
+    for (int li = 0; li < std::min(tail_first, L - 1); ++li) {
+      AmgLevelDev& d = levels[li].dev;
+      d.aggc = nullptr;
+      if (!fused_prolong(li) || !d.agg || d.n > aggc_rows) continue;
+      int32_t* a = arena.alloc<int32_t>((size_t)std::max(d.w, 1) * d.stride);
+      launch_aggc_pack(d, a, stream);
+      d.aggc = a;
+    }
+    check_launch("AMG column-aggregate images");
+  }
   sync();
   amg_built = true;
   if (!from_checkpoint) amg_age = 0;
@@ -1120,6 +1136,20 @@ void Solver::set_resrestrict_blocks() {
       if (worst <= kRRCap) break;
     }
     d.rr_agg = a;
+    // the R-ordered member image (every row is a member of one aggregate:
+    // r_row[nc] == n); the hierarchy's arena (swapped in during the build)
+    if (rr[d.nc] != d.n) throw std::logic_error("AMG: aggregates do not cover the level");
+    const char* pe = std::getenv("CFD_AMG_RR_PERM");
+    if (pe && pe[0] == '0') continue;  // rows read through the member index
+    const uint32_t w = (uint32_t)std::max(d.w, 1);
+    d.rr_ld = (d.n + 63) & ~63u;
+    d.rr_len = arena.alloc<uint8_t>(d.rr_ld);
+    d.rr_dr = arena.alloc<uint8_t>(d.rr_ld);
+    d.rr_dv = arena.alloc<float>(d.rr_ld);
+    d.rr_val = arena.alloc<float>((size_t)w * d.rr_ld);
+    d.rr_col = arena.alloc<int32_t>((size_t)w * d.rr_ld);
+    launch_rr_pack(d, stream);
+    check_launch("AMG R-ordered member image");
   }
 }
 

@@ -514,6 +514,8 @@ VARIANTS = [
     {"CFD_AMG_FUSED_PROLONG": "0", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused, every level, predicated loads
     {"CFD_NT": "63", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG": "off"},  # nontemporal loads everywhere
     {"CFD_NT": "63", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR": "0"},             # ... with predicated slot loads
+    {"CFD_AMG_RR_PERM": "0", "CFD_AMG_AGGC_ROWS": "0"},  # resrestrict through the member index, agg gathers
+    {"CFD_AMG_AGGC_ROWS": "4000000000", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # column-aggregate image everywhere
 ]
 
 
