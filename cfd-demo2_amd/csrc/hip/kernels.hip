@@ -1102,95 +1102,6 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
   }
 }
 
-// SpMV fused with the CGS dots (round 5 experiment, CFD_SPMV_DOTS=1; one GPU):
-// w = A z as k_spmv2 computes it (2 cells per thread, the same block -> rows
-// map), stored for the update, and while w is in registers the chunk
-// partials of <w, V_ii>, ii = 0..j -- the dots pass no longer re-reads w.
-// The canonical tree is kept: a thread holds the adjacent cells 2t, 2t + 1,
-// whose pair sum is the tree's first level; wave_tree64 of the pair sums is
-// a 128-cell subtree = (quarter + quarter); two waves make a chunk, written
-// as a CHUNK partial (k_cgs_reduce reads them with G chunks per segment:
-// seg_values forms the same units and segment trees, the same bits).  Cells
-// past N contribute +0, as load_cells3's zeros do.
-template <bool D16, bool NT, bool SER>
-__global__ void __launch_bounds__(kBlock) k_spmv2_dots(CoupledMatrix A, const float* __restrict__ x,
-                                                       float* __restrict__ y, const float* __restrict__ basis,
-                                                       const float* __restrict__ binv, size_t stride, int j,
-                                                       float* __restrict__ cpart, uint32_t cstride,
-                                                       uint32_t keep_from) {
-  constexpr int U = CFD_SPMV_U, U1 = CFD_SPMV_U1;
-  __shared__ float ql[4 * 64];
-  const uint32_t lb = xcd_block<kRevSpmv>();
-  const uint32_t i0 = lb * (2u * kBlock) + 2u * threadIdx.x;
-  const bool live = i0 < A.N;
-  float wv[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  if (live) {
-    uint32_t lw[2], dr[2];
-    row2_headers<NT>(A, i0, lw, dr);
-    const float4 dd = ldv<NT, float4>(A.cdiag2 + i0);
-    const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
-    const uint32_t maxlen = max(lw[0] & kLgUsedMask, lw[1] & kLgUsedMask);
-    float su[2] = {0.0f, 0.0f}, sv[2] = {0.0f, 0.0f}, sp[2] = {0.0f, 0.0f};
-    float4 pa[U1], pg[U1];
-#pragma unroll
-    for (int u = 0; u < U1; ++u) {
-      const size_t off = (size_t)min((uint32_t)u, (uint32_t)A.ws - 1u) * A.ld + i0;
-      pa[u] = ldv<NT, float4>(A.cval_a + off);
-      pg[u] = ldv<NT, float4>(A.cval_g + off);
-    }
-    if (A.reg && A.ws <= U1 && __all((lw[0] & lw[1] & kLgRegular) != 0u))
-      spmv2_group<D16, U1, true, true, NT>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
-    else
-      spmv2_group<D16, U1, false, true, NT>(A, x, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, su, sv, sp, pa, pg);
-    for (uint32_t r0 = U1; r0 < maxlen; r0 += U)
-      spmv2_group<D16, U, false, false, NT>(A, x, i0, r0, maxlen - 1u, lw, dr, d2, su, sv, sp);
-    float* yo = y + 3 * (size_t)i0;
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    *reinterpret_cast<f4u*>(yo) = f4u{su[0], sv[0], sp[0], su[1]};
-    *reinterpret_cast<f2v*>(yo + 4) = f2v{sv[1], sp[1]};
-    wv[0] = su[0];
-    wv[1] = sv[0];
-    wv[2] = sp[0];
-    if (i0 + 1 < A.N) {  // the second cell of the last pair may be past N: a +0 term
-      wv[3] = su[1];
-      wv[4] = sv[1];
-      wv[5] = sp[1];
-    }
-  }
-  const bool nt_basis = i0 < keep_from;  // the last blocks' lines stay in the cache for the update
-  const uint32_t wave = threadIdx.x >> 6;
-  for (int ii = 0; ii <= j; ++ii) {
-    const float sc = binv[ii];
-    float t = 0.0f;
-    if (live) {
-      const float* vp = basis + (size_t)ii * stride + 3 * (size_t)i0;
-      f4u a;
-      f2u b;
-      if (nt_basis) {
-        a = ldv<true, f4u>(vp);
-        b = ldv<true, f2u>(vp + 4);
-      } else {
-        a = ld4u(vp);
-        b = ld2u(vp + 4);
-      }
-      if constexpr (SER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const float v0[3] = {sc * a.x, sc * a.y, sc * a.z}, v1[3] = {sc * a.w, sc * b.x, sc * b.y};
-      const float w0[3] = {wv[0], wv[1], wv[2]}, w1[3] = {wv[3], wv[4], wv[5]};
-      const float t0 = cell_dot3(w0, v0);
-      const float t1 = (i0 + 1 < A.N) ? cell_dot3(w1, v1) : 0.0f;
-      t = t0 + t1;
-    }
-    const float r = wave_tree64(t);
-    if (red_lane() == 0) ql[4 * ii + wave] = r;
-  }
-  __syncthreads();
-  const uint32_t nchunks = (A.N + kRedChunkCells - 1) / kRedChunkCells;
-  for (uint32_t idx = threadIdx.x; idx < 2u * (uint32_t)(j + 1); idx += kBlock) {
-    const uint32_t ii = idx >> 1, h = idx & 1u, chunk = 2u * lb + h;
-    if (chunk < nchunks) cpart[(size_t)ii * cstride + chunk] = ql[4 * ii + 2 * h] + ql[4 * ii + 2 * h + 1];
-  }
-}
-
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
 __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
   __shared__ float la[kRedMaxSegments], lb[65];
@@ -1453,23 +1364,18 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
 // Same-box A/B at C2 (profiles/r03/ab_rev_schur_early_c2.txt): prediction
 // 152.3 -> 144.9, correction 135.8 -> 132.4 us, 254.8 -> 253.1 ms/step;
 // C1 39.95 -> 39.22.
-// PRE: the group's cval_g slots come from the caller (k_precond_predict2_dma:
-// staged in LDS by the loader waves)
-template <bool D16, int U, bool REG = false, bool NT = false, bool PRE = false>  // REG: see spmv2_group
+template <bool D16, int U, bool REG = false, bool NT = false>  // REG: see spmv2_group
 __device__ __forceinline__ void predict2_group(const CoupledMatrix& A, const float* __restrict__ w_in, float sc,
                                                const float* __restrict__ dinv_uv, uint32_t i0, uint32_t r0,
                                                uint32_t rmax, const uint32_t lw[2], const uint32_t dr[2],
-                                               const float2 d2[2], float rhs[2], const float4* pg = nullptr) {
+                                               const float2 d2[2], float rhs[2]) {
   float4 g[U];
   int c[U][2];
   float gd[U][2], gu[U][2], gv[U][2];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const size_t off = (size_t)min(r0 + u, rmax) * A.ld + i0;
-    if constexpr (PRE)
-      g[u] = pg[u];
-    else
-      g[u] = ldv<NT, float4>(A.cval_g + off);
+    g[u] = ldv<NT, float4>(A.cval_g + off);
     if constexpr (REG) {
       c[u][0] = (int)i0 + A.tmode[u];
       c[u][1] = c[u][0] + 1;
@@ -1544,136 +1450,6 @@ __global__ void __launch_bounds__(kBlock) k_precond_predict2(CoupledMatrix A, co
   *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
   if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
 }
-// ---- Schur prediction with LDS-DMA loader waves (round 5 experiment,
-// CFD_PREDICT_DMA=1) ----
-// Persistent form: one block per CU walks a contiguous range of 1024-cell
-// tiles (XCD-contiguous, as xcd_block).  Two loader waves stream every
-// once-read array of the next tile -- the cval_g slots, the rows' own w_in,
-// cdiag2, dinv_p and the row headers, 67 KiB -- into the other half of a
-// two-tile LDS ring with global_load_lds_dwordx4 (nt: the kernel is the last
-// reader of its matrix), while eight compute waves take the current tile's
-// operands from LDS and keep only the neighbour gathers (dinv_uv, w_in) and
-// the row arithmetic: predict2_group's operations, in its order (bit-exact).
-// One barrier per tile; a loader waits for its own DMA (vmcnt) before it.
-constexpr uint32_t kDmaTile = 1024;  // cells per tile (2 per compute thread)
-constexpr uint32_t kDmaLoadWaves = 2, kDmaCompWaves = 8;
-constexpr uint32_t kDmaThreads = 64 * (kDmaLoadWaves + kDmaCompWaves);
-constexpr uint32_t kDmaG = 0;                         // cval_g, 5 slots x 8 KiB
-constexpr uint32_t kDmaW = kDmaG + 5 * kDmaTile * 8;  // w_in of the tile's cells, 12 KiB
-constexpr uint32_t kDmaD = kDmaW + kDmaTile * 12;     // cdiag2, 8 KiB
-constexpr uint32_t kDmaP = kDmaD + kDmaTile * 8;      // dinv_p, 4 KiB
-constexpr uint32_t kDmaH = kDmaP + kDmaTile * 4;      // lg (u16), 2 KiB
-constexpr uint32_t kDmaR = kDmaH + kDmaTile * 2;      // drank (u8), 1 KiB
-constexpr uint32_t kDmaSlot = kDmaR + kDmaTile;       // 68,608 B per tile
-constexpr uint32_t kDmaPieces = kDmaSlot / 1024;      // 67 wave instructions of 64 x 16 B
-
-// issue tile t's pieces [w, w + kDmaLoadWaves, ...) of one loader wave into `slot`
-template <bool NT>
-__device__ __forceinline__ void dma_tile(const CoupledMatrix& A, const float* w_in, const float* dinv_p,
-                                         uint32_t i0, char* slot, uint32_t w, uint32_t lane) {
-  for (uint32_t p = w; p < kDmaPieces; p += kDmaLoadWaves) {
-    const char* base;
-    const char* end;  // end of the array's padded rows, 16-byte aligned (ld is a multiple of 64):
-                      // a clamped read never cuts a 16-byte chunk that still holds valid bytes
-    uint32_t q;       // piece within the array's tile image
-    if (p < 40) {
-      const uint32_t u = p / 8;
-      q = p % 8;
-      base = reinterpret_cast<const char*>(A.cval_g + (size_t)u * A.ld + i0);
-      end = reinterpret_cast<const char*>(A.cval_g + (size_t)A.ws * A.ld);
-    } else if (p < 52) {
-      q = p - 40;
-      base = reinterpret_cast<const char*>(w_in + 3 * (size_t)i0);
-      end = reinterpret_cast<const char*>(w_in + 3 * (size_t)A.ld);  // vectors are padded to ld rows
-    } else if (p < 60) {
-      q = p - 52;
-      base = reinterpret_cast<const char*>(A.cdiag2 + i0);
-      end = reinterpret_cast<const char*>(A.cdiag2 + A.ld);
-    } else if (p < 64) {
-      q = p - 60;
-      base = reinterpret_cast<const char*>(dinv_p + i0);
-      end = reinterpret_cast<const char*>(dinv_p + A.ld);
-    } else if (p < 66) {
-      q = p - 64;
-      base = reinterpret_cast<const char*>(A.lg + i0);
-      end = reinterpret_cast<const char*>(A.lg + A.ld);
-    } else {
-      q = 0;
-      base = reinterpret_cast<const char*>(A.drank + i0);
-      end = reinterpret_cast<const char*>(A.drank + A.ld);
-    }
-    const char* last = end - 16;
-    const char* src = base + q * 1024u + lane * 16u;
-    if (src > last) src = last;
-    __builtin_amdgcn_global_load_lds(src, slot + p * 1024u, 16, 0, NT ? 2 : 0);
-  }
-}
-
-template <bool D16, bool NT>
-__global__ void __launch_bounds__(kDmaThreads) k_precond_predict2_dma(CoupledMatrix A,
-                                                                      const float* __restrict__ w_in,
-                                                                      const float* __restrict__ binv, int jv,
-                                                                      const float* __restrict__ dinv_uv,
-                                                                      const float* __restrict__ dinv_p,
-                                                                      float* temp_p, float* p_sol, float* p_prev) {
-  extern __shared__ float dma_lds[];
-  char* const ring = reinterpret_cast<char*>(dma_lds);
-  const uint32_t ntiles = (A.N + kDmaTile - 1) / kDmaTile, nb = gridDim.x, lb = xcd_block();
-  const uint32_t t0 = (uint32_t)((uint64_t)lb * ntiles / nb), t1 = (uint32_t)((uint64_t)(lb + 1) * ntiles / nb);
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64), lane = threadIdx.x % 64;
-  const bool loader = wave < kDmaLoadWaves;
-  const float sc = binv[jv];
-  if (loader && t0 < t1) {
-    dma_tile<NT>(A, w_in, dinv_p, t0 * kDmaTile, ring, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  for (uint32_t t = t0; t < t1; ++t) {
-    char* const cur = ring + ((t - t0) & 1u) * kDmaSlot;
-    if (loader) {
-      if (t + 1 < t1) {
-        dma_tile<NT>(A, w_in, dinv_p, (t + 1) * kDmaTile, ring + ((t + 1 - t0) & 1u) * kDmaSlot, wave, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      const uint32_t ct = threadIdx.x - 64 * kDmaLoadWaves;  // 0 .. 511: cells 2 ct, 2 ct + 1 of the tile
-      const uint32_t i0 = t * kDmaTile + 2 * ct;
-      if (i0 < A.N) {
-        const uint32_t hw = *reinterpret_cast<const uint32_t*>(cur + kDmaH + 4 * ct);
-        const uint32_t dw = *reinterpret_cast<const uint16_t*>(cur + kDmaR + 2 * ct);
-        const float4 dd = *reinterpret_cast<const float4*>(cur + kDmaD + 16 * ct);
-        const float2 dp = *reinterpret_cast<const float2*>(cur + kDmaP + 8 * ct);
-        const float* wl = reinterpret_cast<const float*>(cur + kDmaW + 24 * ct);
-        const float2 w01 = *reinterpret_cast<const float2*>(wl);
-        const float2 w23 = *reinterpret_cast<const float2*>(wl + 2);
-        const float2 w45 = *reinterpret_cast<const float2*>(wl + 4);
-        float4 g[5];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) g[u] = *reinterpret_cast<const float4*>(cur + kDmaG + u * (kDmaTile * 8) + 16 * ct);
-        (void)w01;
-        (void)w45;
-        float rhs[2] = {sc * w23.x, sc * w45.y};
-        const uint32_t lw[2] = {hw & 0xFFFFu, hw >> 16}, dr[2] = {dw & 0xFFu, dw >> 8};
-        const float2 d2[2] = {make_float2(dd.x, dd.y), make_float2(dd.z, dd.w)};
-        if (__all((lw[0] & lw[1] & kLgRegular) != 0u))
-          predict2_group<D16, 5, true, NT, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs, g);
-        else
-          predict2_group<D16, 5, false, NT, true>(A, w_in, sc, dinv_uv, i0, 0, (uint32_t)A.ws - 1u, lw, dr, d2, rhs,
-                                                  g);
-        *reinterpret_cast<float2*>(temp_p + i0) = make_float2(rhs[0], rhs[1]);
-        *reinterpret_cast<float2*>(p_sol + i0) = make_float2(dp.x * rhs[0], dp.y * rhs[1]);
-        if (p_prev) *reinterpret_cast<float2*>(p_prev + i0) = make_float2(0.0f, 0.0f);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-}
-
 template <bool D16, int U, bool REG = false>  // REG: see spmv2_group
 __device__ __forceinline__ void correct2_group(const CoupledMatrix& A, const float* __restrict__ p_sol, uint32_t i0,
                                                uint32_t r0, uint32_t rmax, const uint32_t lw[2], float cu[2],
@@ -1896,20 +1672,6 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
     }
   }
   [[maybe_unused]] int ag[kU][4];
-  [[maybe_unused]] const bool aggc = PRO && L.aggc != nullptr;
-  if constexpr (PRO) {
-    if (aggc) {  // the slots' aggregates from the static image, issued with the slot values
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const size_t off = (size_t)min(r0 + u, rmax) * L.stride + i0;
-        const int4 a = ldv<NT, int4>(reinterpret_cast<const int4*>(L.aggc + off));
-        ag[u][0] = a.x;
-        ag[u][1] = a.y;
-        ag[u][2] = a.z;
-        ag[u][3] = a.w;
-      }
-    }
-  }
   if constexpr (ALWAYS && MODE == 1) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -1919,13 +1681,11 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       xg[u][2] = q.z;
       xg[u][3] = q.w;
       if constexpr (PRO) {
-        if (!aggc) {
-          const i4u a = *reinterpret_cast<const i4u*>(L.agg + c[u][0]);
-          ag[u][0] = a.x;
-          ag[u][1] = a.y;
-          ag[u][2] = a.z;
-          ag[u][3] = a.w;
-        }
+        const i4u a = *reinterpret_cast<const i4u*>(L.agg + c[u][0]);
+        ag[u][0] = a.x;
+        ag[u][1] = a.y;
+        ag[u][2] = a.z;
+        ag[u][3] = a.w;
       }
     }
 #pragma unroll
@@ -1934,8 +1694,7 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
           xg[u][k] = x[c[u][k]];
-          if constexpr (PRO)
-            if (!aggc) ag[u][k] = (int)L.agg[c[u][k]];
+          if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
         }
       }
   } else {
@@ -1945,8 +1704,7 @@ __device__ __forceinline__ void gather_group(const AmgLevelDev& L, const float* 
       for (int k = 0; k < 4; ++k) {
         xg[u][k] = gat<ALWAYS && MODE == 1>(r0 + u < u4(ln, k), x + c[u][k]);
         // unused slots hold the row's own (valid) column: agg of a real or padding row
-        if constexpr (PRO)
-          if (!aggc) ag[u][k] = (int)L.agg[c[u][k]];
+        if constexpr (PRO) ag[u][k] = (int)L.agg[c[u][k]];
       }
   }
   if constexpr (PRO) {
@@ -2233,14 +1991,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
     if (sm_out) dec = sm_de[I0 + threadIdx.x];
   }
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
-    // matrix row from the R-ordered image (indexed by p: issued with the
-    // member index, one dependent round trip fewer than through f)
-    // (CFD_AMG_RR_PERM=0: rr_val null, the rows read through f)
     const uint32_t f = L.r_col[p];
-    const bool perm = L.rr_val != nullptr;
-    const uint32_t len = perm ? L.rr_len[p] : L.len[f], dr = perm ? L.rr_dr[p] : L.drank[f];
-    const float dvf = perm ? L.rr_dv[p] : L.dv[f];
-    const float xf = x[f];
+    const uint32_t len = L.len[f], dr = L.drank[f];
+    const float xf = x[f], dvf = L.dv[f];
     float ax = 0.0f;
     uint32_t r0 = 0;
     for (; r0 < len; r0 += 4) {
@@ -2248,15 +2001,9 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
       int c[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (perm) {
-          const size_t off = (size_t)min(r0 + u, w - 1u) * L.rr_ld + p;
-          v[u] = L.rr_val[off];
-          c[u] = L.rr_col[off];
-        } else {
-          const size_t off = (size_t)min(r0 + u, w - 1u) * L.stride + f;
-          v[u] = L.val[off];
-          c[u] = D16 ? (int)f + (int)L.col16[off] : L.col32[off];
-        }
+        const size_t off = (size_t)min(r0 + u, w - 1u) * L.stride + f;
+        v[u] = L.val[off];
+        c[u] = D16 ? (int)f + (int)L.col16[off] : L.col32[off];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) xg[u] = x[c[u]];
@@ -2803,25 +2550,6 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
                     : (nt ? k_spmv2<false, true> : k_spmv2<false, false>);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, x, y, b);
 }
-void launch_spmv_dots(const CoupledMatrix& A, const float* x, float* y, const float* basis, const float* binv,
-                      size_t stride, int j, float* cpart, uint32_t cstride, hipStream_t s, bool nt,
-                      size_t keep_bytes) {
-  if (!A.N) return;
-  if (A.r0 != 0 || A.r1 < A.N || A.r3 > A.r2) throw std::invalid_argument("spmv_dots: one GPU, all rows");
-  const unsigned nb = rows2x_grid(0, A.N, 0, 0);
-  // the last cells whose basis lines (j + 1 vectors + w) fit keep_bytes: default policy
-  const size_t keep_cells = keep_bytes / ((size_t)(j + 2) * 12u);
-  const uint32_t keep_from = keep_cells >= A.N ? 0u : A.N - (uint32_t)keep_cells;
-  const bool ser = A.N >= CFD_CGS_SER_MIN_CELLS;
-using SdFn = void (*)(CoupledMatrix, const float*, float*, const float*, const float*, size_t, int, float*, uint32_t,
-                       uint32_t);
-  const SdFn fns[2][2][2] = {{{k_spmv2_dots<false, false, false>, k_spmv2_dots<false, false, true>},
-                              {k_spmv2_dots<false, true, false>, k_spmv2_dots<false, true, true>}},
-                             {{k_spmv2_dots<true, false, false>, k_spmv2_dots<true, false, true>},
-                              {k_spmv2_dots<true, true, false>, k_spmv2_dots<true, true, true>}}};
-  const SdFn fn = fns[A.use16 ? 1 : 0][nt ? 1 : 0][ser ? 1 : 0];
-  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, x, y, basis, binv, stride, j, cpart, cstride, keep_from);
-}
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
                      uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes) {
   if (!N) return;
@@ -2857,19 +2585,9 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 }
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
-                            float* p_prev, hipStream_t s, bool nt, bool dma) {
+                            float* p_prev, hipStream_t s, bool nt) {
   if (A.r1 <= A.r0 && A.r3 <= A.r2) return;
   const unsigned nb = rows2x_grid(A.r0, A.r1, A.r2, A.r3);
-  if (dma && A.r0 == 0 && A.r1 >= A.N && A.r3 <= A.r2 && A.reg && A.ws >= 1 && A.ws <= 5 &&
-      A.N >= kDmaTile) {
-    // one block per CU: 256 CUs (the grid size only sets the tiles per block)
-    const unsigned nbd = std::min<unsigned>(256u, (A.N + kDmaTile - 1) / kDmaTile);
-    auto fd = A.use16 ? (nt ? k_precond_predict2_dma<true, true> : k_precond_predict2_dma<true, false>)
-                      : (nt ? k_precond_predict2_dma<false, true> : k_precond_predict2_dma<false, false>);
-    hipLaunchKernelGGL(fd, dim3(nbd), dim3(kDmaThreads), 2 * kDmaSlot, s, A, w_in, binv, j, dinv_uv, dinv_p, temp_p,
-                       p_sol, p_prev);
-    return;
-  }
   auto fn = A.use16 ? (nt ? k_precond_predict2<true, true> : k_precond_predict2<true, false>)
                     : (nt ? k_precond_predict2<false, true> : k_precond_predict2<false, false>);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p, temp_p, p_sol, p_prev);
@@ -2973,38 +2691,6 @@ void launch_amg_restrict(const AmgLevelDev& L, const float* r, float* cb, float*
     hipLaunchKernelGGL(k_amg_restrict, dim3(grid_for(n)), dim3(kBlock), 0, s, L, r, cb, cx, stride_c, glo, ghi,
                        sm_out, sm_de, I0, I1);
 }
-__global__ void __launch_bounds__(kBlock) k_aggc_pack(AmgLevelDev L, int32_t* aggc) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= L.stride) return;
-  const uint32_t w = (uint32_t)max(L.w, 1);
-  for (uint32_t r = 0; r < w; ++r) {
-    const size_t off = (size_t)r * L.stride + i;
-    const int32_t c = L.use16 ? (int32_t)i + (int32_t)L.col16[off] : L.col32[off];
-    aggc[off] = (int32_t)L.agg[c];
-  }
-}
-void launch_aggc_pack(const AmgLevelDev& L, int32_t* aggc, hipStream_t s) {
-  if (L.stride)
-    hipLaunchKernelGGL(k_aggc_pack, dim3((unsigned)((L.stride + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, L, aggc);
-}
-__global__ void __launch_bounds__(kBlock) k_rr_pack(AmgLevelDev L, uint32_t nm) {
-  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-  if (p >= nm) return;
-  const uint32_t f = L.r_col[p];
-  const uint32_t w = (uint32_t)max(L.w, 1);
-  const_cast<uint8_t*>(L.rr_len)[p] = L.len[f];
-  const_cast<uint8_t*>(L.rr_dr)[p] = L.drank[f];
-  const_cast<float*>(L.rr_dv)[p] = L.dv[f];
-  for (uint32_t r = 0; r < w; ++r) {
-    const size_t off = (size_t)r * L.stride + f, o2 = (size_t)r * L.rr_ld + p;
-    const_cast<float*>(L.rr_val)[o2] = L.val[off];
-    const_cast<int32_t*>(L.rr_col)[o2] = L.use16 ? (int32_t)f + (int32_t)L.col16[off] : L.col32[off];
-  }
-}
-void launch_rr_pack(const AmgLevelDev& L, hipStream_t s) {
-  if (!L.rr_agg || !L.rr_val || !L.nc) return;
-  hipLaunchKernelGGL(k_rr_pack, dim3((unsigned)((L.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, L, L.n);
-}
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* cb, float* cx,
                             float* sm_out, const float* sm_de, hipStream_t s) {
   if (!L.nc || !L.rr_agg) return;
@@ -3058,13 +2744,6 @@ size_t init_kernel_attributes(int device) {
     if (e == hipSuccess)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
-    // the LDS-DMA Schur prediction's two-tile ring
-    for (const void* f : {reinterpret_cast<const void*>(&k_precond_predict2_dma<true, true>),
-                          reinterpret_cast<const void*>(&k_precond_predict2_dma<true, false>),
-                          reinterpret_cast<const void*>(&k_precond_predict2_dma<false, true>),
-                          reinterpret_cast<const void*>(&k_precond_predict2_dma<false, false>)})
-      if (e == hipSuccess && optin >= (int)(2 * kDmaSlot))
-        e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(2 * kDmaSlot));
     status[device] = e;
     budget[device] = lim;
   });

@@ -231,21 +231,6 @@ struct AmgLevelDev {
   // k_amg_resrestrict: aggregates per block (0: the level keeps the separate
   // residual + restriction kernels); every block's members fit kRRCap
   uint32_t rr_agg;
-  // ... and the level's rows in R order (member p = r_col[p]): length,
-  // diagonal rank and value, slots [r * rr_ld + p] with ABSOLUTE columns
-  // (k_rr_pack; rebuilt by a numeric re-setup), so a block's matrix loads
-  // depend only on p, not on the member row index loaded first
-  // post-smoother with the prolongation fused (k_amg_smooth<..., PRO>): the
-  // aggregate of every slot's column, [r * stride + i] (k_aggc_pack; pattern
-  // only), so the coarse values are gathered beside x instead of after a
-  // dependent agg gather (null: gathered through agg)
-  const int32_t* aggc;
-  uint32_t rr_ld;
-  const uint8_t* rr_len;
-  const uint8_t* rr_dr;
-  const float* rr_dv;
-  const float* rr_val;
-  const int32_t* rr_col;
 };
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
 // zeroed entries after every level's agg array: the fused prolongation reads
@@ -311,12 +296,6 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
 // partial[ii * np + k] of <w, V_ii>, ii = 0..j
 // keep_bytes > 0: the last blocks (their j + 2 vectors within keep_bytes) read
 // the basis with the default policy, for a top-down update (rev) after it
-// SpMV fused with the CGS dots (one GPU): y = A x, and chunk partials of
-// <y, V_ii>, ii = 0..j, into cpart[ii * cstride + chunk] (k_cgs_reduce with
-// G = chunks per segment)
-void launch_spmv_dots(const CoupledMatrix& A, const float* x, float* y, const float* basis, const float* binv,
-                      size_t stride, int j, float* cpart, uint32_t cstride, hipStream_t s, bool nt,
-                      size_t keep_bytes);
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
                      uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes = 0);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
@@ -332,7 +311,7 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 // r_in = binv[j] * W_j
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
-                            float* p_prev, hipStream_t s, bool nt = false, bool dma = false);
+                            float* p_prev, hipStream_t s, bool nt = false);
 void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
                            const float* sval, const float* dinv_p, const float* temp_p,
                            const float* p_sol, float* p_prev, hipStream_t s);
@@ -393,10 +372,6 @@ void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, c
 // residual + restriction fused (k_amg_resrestrict; L.rr_agg > 0, replicated
 // or single-GPU level): coarse_b = R (b - A x), coarse_x cleared or the
 // coarse zero-x pre-smoother written to sm_out (as launch_amg_restrict)
-// the R-ordered member image of a level (AmgLevelDev::rr_*), from its level image
-void launch_rr_pack(const AmgLevelDev& L, hipStream_t s);
-// AmgLevelDev::aggc of a level from its columns and agg
-void launch_aggc_pack(const AmgLevelDev& L, int32_t* aggc, hipStream_t s);
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* coarse_b, float* coarse_x,
                             float* sm_out, const float* sm_de, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,

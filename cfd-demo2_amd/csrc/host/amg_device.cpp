@@ -881,7 +881,6 @@ void Solver::refresh_amg() {
     }
   }
   CFD_HIP(hipGetLastError());
-  for (const AmgGpuLevel& G : levels) launch_rr_pack(G.dev, stream);  // new values, same R order
   if (tail_blob_first >= 0) build_tail_blob(tail_blob_first, true);
   sync();
 }

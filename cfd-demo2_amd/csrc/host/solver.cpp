@@ -88,14 +88,6 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
   if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
   if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
-  if (const char* sd = std::getenv("CFD_SPMV_DOTS")) spmv_dots = sd[0] == '1' && !dist();
-  if (const char* pd = std::getenv("CFD_PREDICT_DMA")) {
-    // one GPU, and at least CFD_PREDICT_DMA_MIN cells (default 2^18: a tile
-    // range per CU; smaller values only for the parity tests)
-    const char* pm = std::getenv("CFD_PREDICT_DMA_MIN");
-    const uint64_t min_cells = pm ? std::strtoull(pm, nullptr, 10) : (1ull << 18);
-    predict_dma = pd[0] == '1' && !dist() && N >= min_cells;
-  }
   // C1-size meshes: 64 MB of the dots pass kept in the Infinity Cache for a
   // top-down update (profiles/r04/ab_cgskeep2_c1.txt: update 36.5-36.9 ->
   // 32.3 us, dots +0.3 us per iteration); from 2^22 cells on the kept lines
@@ -586,10 +578,6 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   temp_p = valloc<float>(1);
   p_sol = valloc<float>(1);
   partial = arena.alloc<float>((size_t)m1 * pstride);
-  if (spmv_dots) {
-    cstride = (nchunks + 3) & ~3u;
-    cpart = arena.alloc<float>((size_t)m1 * cstride);
-  }
   partial_n = arena.alloc<float>(pstride);
   const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
   dsc = arena.alloc<float>(nsc);
@@ -1083,22 +1071,6 @@ void Solver::ensure_amg() {
       if (tail_blob_first >= 0) tail_first = t;
     }
   }
-  // fused post-smoothers of the latency-bound levels: the aggregates of the
-  // slots' columns as a static image (AmgLevelDev::aggc, pattern only: a
-  // numeric re-setup keeps it), CFD_AMG_AGGC_ROWS (default 2^18) rows at most
-  {
-    const char* ae = std::getenv("CFD_AMG_AGGC_ROWS");
-    const uint64_t aggc_rows = ae ? std::strtoull(ae, nullptr, 10) : (1ull << 18);
-    for (int li = 0; li < std::min(tail_first, L - 1); ++li) {
-      AmgLevelDev& d = levels[li].dev;
-      d.aggc = nullptr;
-      if (!fused_prolong(li) || !d.agg || d.n > aggc_rows) continue;
-      int32_t* a = arena.alloc<int32_t>((size_t)std::max(d.w, 1) * d.stride);
-      launch_aggc_pack(d, a, stream);
-      d.aggc = a;
-    }
-    check_launch("AMG column-aggregate images");
-  }
   sync();
   amg_built = true;
   if (!from_checkpoint) amg_age = 0;
@@ -1136,20 +1108,6 @@ void Solver::set_resrestrict_blocks() {
       if (worst <= kRRCap) break;
     }
     d.rr_agg = a;
-    // the R-ordered member image (every row is a member of one aggregate:
-    // r_row[nc] == n); the hierarchy's arena (swapped in during the build)
-    if (rr[d.nc] != d.n) throw std::logic_error("AMG: aggregates do not cover the level");
-    const char* pe = std::getenv("CFD_AMG_RR_PERM");
-    if (pe && pe[0] == '0') continue;  // rows read through the member index
-    const uint32_t w = (uint32_t)std::max(d.w, 1);
-    d.rr_ld = (d.n + 63) & ~63u;
-    d.rr_len = arena.alloc<uint8_t>(d.rr_ld);
-    d.rr_dr = arena.alloc<uint8_t>(d.rr_ld);
-    d.rr_dv = arena.alloc<float>(d.rr_ld);
-    d.rr_val = arena.alloc<float>((size_t)w * d.rr_ld);
-    d.rr_col = arena.alloc<int32_t>((size_t)w * d.rr_ld);
-    launch_rr_pack(d, stream);
-    check_launch("AMG R-ordered member image");
   }
 }
 
@@ -1486,8 +1444,7 @@ void Solver::precondition(int j, float* z) {
     Ar.r1 = b;
     Ar.r2 = a2;
     Ar.r3 = b2;
-    launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream, nt(4),
-                           predict_dma);
+    launch_precond_predict(Ar, v, binv, j, dinv_uv, dinv_p, temp_p, p_sol, jacobi ? temp : nullptr, stream, nt(4));
   });
   bool in_sol = true;
   if (!jacobi) {
@@ -1591,35 +1548,17 @@ void Solver::iteration(int j, float* pin) {
   float* zj = zvec + (size_t)j * stride;
   precondition(j, zj);
   const CommScope cs(this, kCommKrylovHalo);
-  if (spmv_dots) {
-    launch_spmv_dots(cmat(), zj, w, basis, binv, stride, j, cpart, cstride, stream, nt(8), 0);
-  } else {
-    overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
-      CoupledMatrix A = cmat();
-      A.r0 = a;
-      A.r1 = b;
-      A.r2 = a2;
-      A.r3 = b2;
-      launch_spmv(A, zj, w, stream, nullptr, nt(8));
-    });
-  }
-  if (spmv_dots) {
-    // the dots' chunk partials came with w (launch_spmv_dots above); the
-    // reduction reads them as units of one chunk
-    RedSrc r;
-    r.p = cpart;
-    r.stride = cstride;
-    r.nchunks = nchunks;
-    r.G = red.G;
-    r.nseg = red.nseg;
-    r.nvec = (uint32_t)(j + 1);
-    launch_cgs_reduce(r, j, H, m1, stream);
-    launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, false);
-  } else {
-    launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
-    launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-    launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0);
-  }
+  overlapped(cell_plan, {{zj, 3}}, N, [&](uint32_t a, uint32_t b, uint32_t a2, uint32_t b2) {
+    CoupledMatrix A = cmat();
+    A.r0 = a;
+    A.r1 = b;
+    A.r2 = a2;
+    A.r3 = b2;
+    launch_spmv(A, zj, w, stream, nullptr, nt(8));
+  });
+  launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
+  launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
+  launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0);
   launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
   check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
 }

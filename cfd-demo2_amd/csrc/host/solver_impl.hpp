@@ -329,14 +329,6 @@ struct Solver {
   // prepare / assemble (assemble re-reads prepare's face slots), the
   // restriction maps.
   unsigned nt_mask = 47;  // same-box A/B, profiles/r04/ab_nt_c2.txt, ab_nt2_c2.txt
-  // Schur prediction by the LDS-DMA loader / compute-wave kernel
-  // (k_precond_predict2_dma; CFD_PREDICT_DMA=1, one GPU, >= 2^18 cells)
-  bool predict_dma = false;
-  // SpMV fused with the CGS dots (k_spmv2_dots; CFD_SPMV_DOTS=1, one GPU):
-  // chunk partials cpart[ii * cstride + chunk]
-  bool spmv_dots = false;
-  float* cpart = nullptr;
-  uint32_t cstride = 0;
   // an in-process group step failed on some rank: the ranks stopped at
   // different points of the step (ring rotation, time, FGMRES state), so the
   // group refuses to step until its state is restored on every rank

@@ -514,8 +514,6 @@ VARIANTS = [
     {"CFD_AMG_FUSED_PROLONG": "0", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused, every level, predicated loads
     {"CFD_NT": "63", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG": "off"},  # nontemporal loads everywhere
     {"CFD_NT": "63", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR": "0"},             # ... with predicated slot loads
-    {"CFD_AMG_RR_PERM": "0", "CFD_AMG_AGGC_ROWS": "0"},  # resrestrict through the member index, agg gathers
-    {"CFD_AMG_AGGC_ROWS": "4000000000", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # column-aggregate image everywhere
 ]
 
 
@@ -644,60 +642,3 @@ def test_fixed_schedule_early_exits(inlet):
         o.step()
         _assert_same_fields(g, o, f"inlet={inlet} step {k}")
         _assert_same_info(g, o, f"inlet={inlet} step {k}")
-
-
-@pytest.mark.parametrize("which", ["amg_test", "bench_100k"])
-def test_predict_dma_parity(which, monkeypatch):
-    """The LDS-DMA Schur prediction (k_precond_predict2_dma, CFD_PREDICT_DMA=1:
-    loader waves stage the once-read arrays in an LDS ring, compute waves keep
-    the gathers): GPU == oracle bit-exact, and == the plain kernel."""
-    monkeypatch.setenv("CFD_PREDICT_DMA", "1")
-    monkeypatch.setenv("CFD_PREDICT_DMA_MIN", "1024")
-    if which == "amg_test":
-        mesh = backwards_step()
-        cfg = dict()
-        setup = lambda s: _setup_amg_test(s, mesh, 1)  # noqa: E731
-        steps = 3
-    else:
-        mesh = bench_mesh(0.0055, 30)
-        cfg = dict(fixed_outer=2, fixed_inner=8)
-        setup = lambda s: _setup_amg_test(s, mesh, 1)  # noqa: E731
-        steps = 2
-    g, o = _pair(mesh, **cfg)
-    monkeypatch.setenv("CFD_PREDICT_DMA", "0")
-    plain = GpuSolver(mesh, config=default_config(**cfg))
-    for s in (g, o, plain):
-        setup(s)
-    for k in range(steps):
-        for s in (g, o, plain):
-            s.step()
-        _assert_same_fields(g, plain, f"dma vs plain {which} step {k}")
-        _assert_same_fields(g, o, f"dma vs oracle {which} step {k}")
-        _assert_same_info(g, o, f"dma vs oracle {which} step {k}")
-
-
-@pytest.mark.parametrize("which", ["amg_test", "bench_100k", "c1"])
-def test_spmv_dots_parity(which, monkeypatch):
-    """SpMV fused with the CGS dots (k_spmv2_dots, CFD_SPMV_DOTS=1: chunk
-    partials of <w, V_ii> while w is in registers, reduced with G chunks per
-    segment): GPU == oracle (small meshes) and == the separate kernels, bit-exact."""
-    monkeypatch.setenv("CFD_SPMV_DOTS", "1")
-    if which == "amg_test":
-        mesh, cfg, steps, oracle = backwards_step(), dict(), 3, True
-    elif which == "bench_100k":
-        mesh, cfg, steps, oracle = bench_mesh(0.0055, 30), dict(fixed_outer=2, fixed_inner=8), 2, True
-    else:
-        mesh, cfg, steps, oracle = bench_mesh(0.001723, 100), dict(fixed_outer=1, fixed_inner=6), 1, False
-    g = GpuSolver(mesh, config=default_config(**cfg))
-    o = OracleSolver(mesh, config=default_config(**cfg)) if oracle else None
-    monkeypatch.setenv("CFD_SPMV_DOTS", "0")
-    plain = GpuSolver(mesh, config=default_config(**cfg))
-    for s in (g, plain) + ((o,) if o else ()):
-        _setup_amg_test(s, mesh, 1)
-    for k in range(steps):
-        for s in (g, plain) + ((o,) if o else ()):
-            s.step()
-        _assert_same_fields(g, plain, f"spmv+dots vs separate {which} step {k}")
-        _assert_same_info(g, plain, f"spmv+dots vs separate {which} step {k}")
-        if o:
-            _assert_same_fields(g, o, f"spmv+dots vs oracle {which} step {k}")
