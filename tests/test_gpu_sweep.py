@@ -60,7 +60,14 @@ def _case(seed):
                 time_scheme=rng.choice([0, 1]), precond=rng.choice([0, 1, 1]), alpha_u=rng.choice([0.7, 0.9]),
                 alpha_p=rng.choice([0.3, 0.9]))
     nranks = rng.choice([1, 1, 2, 3] + ([4, 6, 8] if os.environ.get("CFD_SWEEP_MANY_RANKS") else []))
-    return kind, mesh, cfg, phys, nranks, rng.randrange(1 << 30)
+    useed = rng.randrange(1 << 30)
+    # round 5 (drawn after the earlier choices, so older seeds keep their cases):
+    # the partition-aware AMG mode on several ranks (the oracle runs the same
+    # mode at the same rank count), hipGraph replay on one GPU
+    if rng.random() < 0.35:
+        cfg.update(amg_local_aggregation=1)
+    graph = rng.random() < 0.3
+    return kind, mesh, cfg, phys, nranks, useed, graph
 
 
 def _setup(s, mesh, phys, useed):
@@ -84,16 +91,18 @@ def _setup(s, mesh, phys, useed):
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
-    kind, mesh, cfg, phys, nranks, useed = _case(seed)
+    kind, mesh, cfg, phys, nranks, useed, graph = _case(seed)
     # ranks own whole reduction segments (>= 256 cells): small meshes take fewer ranks
     nranks = min(nranks, max_ranks(mesh.num_cells()))
     monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "200")  # distributed coarse levels on these small meshes
     c = default_config(**cfg)
     g = GpuSolver(mesh, config=c) if nranks == 1 else GpuGroup(mesh, nranks, config=c)
+    if nranks == 1 and graph:
+        g.graph_enable(True)
     o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
     for s in (g, o):
         _setup(s, mesh, phys, useed)
-    ctx = f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}"
+    ctx = f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}, graph={graph}"
     for k in range(3):
         g.step()
         o.step()
