@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "cfd-demo2_amd"))
 
-from cfd2_amd import GpuSolver  # noqa: E402
+from cfd2_amd import GpuSolver, default_config  # noqa: E402
 from tests.meshes import backwards_step  # noqa: E402
 from tests.test_gpu_parity import _setup_amg_test  # noqa: E402
 
@@ -22,7 +22,8 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     mesh = backwards_step()
-    s = GpuSolver.create_dist_host(mesh, world, rank, device=0)
+    local = int(os.environ.get("CFD_TEST_AMG_LOCAL", "0"))  # partition-aware AMG aggregation
+    s = GpuSolver.create_dist_host(mesh, world, rank, device=0, config=default_config(amg_local_aggregation=local))
     _setup_amg_test(s, mesh, 1)
     for _ in range(steps):
         s.step()

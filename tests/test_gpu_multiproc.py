@@ -29,10 +29,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nranks,overlap", [(2, False), (3, False), (2, True)])
-def test_multiprocess_host_transport_parity(nranks, overlap, tmp_path):
+@pytest.mark.parametrize("nranks,overlap,local", [(2, False, 0), (3, False, 0), (2, True, 0), (3, False, 1)])
+def test_multiprocess_host_transport_parity(nranks, overlap, local, tmp_path, monkeypatch):
+    """local: the partition-aware AMG mode (cfd_config.amg_local_aggregation),
+    against the oracle run with the same mode and rank count."""
     steps = 3
-    env = dict(os.environ, CFD_AMG_REPLICATE_ROWS="50", MASTER_ADDR="127.0.0.1")
+    monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "50")  # the oracle's partitioned levels (local mode) follow it
+    env = dict(os.environ, CFD_AMG_REPLICATE_ROWS="50", MASTER_ADDR="127.0.0.1", CFD_TEST_AMG_LOCAL=str(local))
     if overlap:  # the interior/boundary split of every halo'd launch (production: >= 1M rows per rank)
         env["CFD_OVERLAP_MIN_ROWS"] = "64"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
@@ -41,7 +44,10 @@ def test_multiprocess_host_transport_parity(nranks, overlap, tmp_path):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     mesh = backwards_step()
-    o = OracleSolver(mesh, nranks=nranks)  # the replication threshold moves work, not results
+    # the replication threshold moves work, not results -- except in the local mode, where it
+    # decides which levels aggregate per rank (the same threshold on both sides)
+    from cfd2_amd import default_config
+    o = OracleSolver(mesh, config=default_config(amg_local_aggregation=local), nranks=nranks)
     _setup_amg_test(o, mesh, 1)
     for _ in range(steps):
         o.step()
