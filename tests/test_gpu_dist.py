@@ -355,3 +355,23 @@ def test_group_local_aggregation_fewer_exchanges(replicate_rows):
         per_it[local] = max(r.comm_stats()["exchanges"] for r in g.ranks) / its
         g.close()
     assert per_it[1] < per_it[0], per_it
+
+
+@pytest.mark.parametrize("refresh", ["1", "0"])
+def test_group_local_aggregation_rebuild(refresh, replicate_rows, monkeypatch):
+    """Partition-aware mode with the AMG re-setup every step (numeric refresh
+    over the per-rank structure, or a full rebuild): == oracle(R, local)."""
+    monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
+    replicate_rows(50)
+    mesh = backwards_step()
+    cfg = dict(amg_local_aggregation=1, amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8)
+    g = GpuGroup(mesh, 3, config=default_config(**cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg), nranks=3)
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    for k in range(5):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"local rebuild refresh={refresh} step {k}")
+        _assert_same_info(g, o, f"local rebuild refresh={refresh} step {k}")
+    g.close()
