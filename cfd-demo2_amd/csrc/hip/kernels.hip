@@ -718,14 +718,19 @@ __device__ __forceinline__ void load_cells3(const float* p, uint32_t N, float v[
     }
   }
 }
-template <bool FULL>
+template <bool FULL, bool NT = true>
 __device__ __forceinline__ void store_cells3_stream(float* p, uint32_t N, const float v[4][3], uint32_t b = ~0u) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const size_t c = cell_qb(b == ~0u ? blockIdx.x : b, q);
     if (FULL || c < N) {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
+      for (int e = 0; e < 3; ++e) {
+        if constexpr (NT)
+          __builtin_nontemporal_store(v[q][e], p + 3 * c + e);
+        else
+          p[3 * c + e] = v[q][e];
+      }
     }
   }
 }
@@ -1112,7 +1117,10 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 
 // update_w_cgs (gmres_cgs.wgsl:125-166) fused with the ||w||^2 unit partial; the
 // updated w is written straight into basis slot j+1 (unnormalised, see binv).
-template <bool FULL, bool SER>
+// NTB: nontemporal basis loads and store of the new vector (the default);
+// false when the whole basis stays in the caches (small meshes, see
+// launch_cgs_update_norm)
+template <bool FULL, bool SER, bool NTB>
 __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
                                                  const float* hcol, const float* scol, uint32_t N, float t[4],
                                                  uint32_t b) {
@@ -1120,7 +1128,7 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
-    load_cells3<FULL, true, SER>(basis + (size_t)ii * stride, N, v, b);
+    load_cells3<FULL, NTB, SER>(basis + (size_t)ii * stride, N, v, b);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1134,9 +1142,9 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
     for (int e = 0; e < 3; ++e) wn[q][e] = wn[q][e] - corr[q][e];
     t[q] = cell_dot3(wn[q], wn[q]);
   }
-  store_cells3_stream<FULL>(basis + (size_t)(j + 1) * stride, N, wn, b);
+  store_cells3_stream<FULL, NTB>(basis + (size_t)(j + 1) * stride, N, wn, b);
 }
-template <bool SER>
+template <bool SER, bool NTB = true>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
                                                             const float* __restrict__ binv,
@@ -1152,9 +1160,9 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   __syncthreads();
   float t[4];
   if (block_full(N, b))
-    cgs_update_cells<true, SER>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<true, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
   else
-    cgs_update_cells<false, SER>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<false, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
   quarter_trees(t, ql);
   __syncthreads();
   const uint32_t UB = 4 / U, unit = b * UB + threadIdx.x;
@@ -2208,6 +2216,9 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 }
 
 
+#ifndef CFD_TAIL_TK
+#define CFD_TAIL_TK 8
+#endif
 // The LDS tail with every matrix of the tail levels in LDS as well (the blob
 // built once by the host from the level images: off-diagonal CSR with u16
 // columns, dv/de, drank, P and R).  Each phase is then LDS reads + one
@@ -2267,12 +2278,33 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
   __syncthreads();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
   auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
+  // Row loops in chunks of TK entries: every column (and value) of a chunk
+  // read from LDS first, then every gather, then the accumulation in entry
+  // order -- two dependent LDS round trips per chunk instead of two per
+  // entry (round 5); the same operations in the same order.  CFD_TAIL_TK=1
+  // is the per-entry form (A/B variant).
+  constexpr uint32_t TK = CFD_TAIL_TK;
   auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
     const uint32_t* ro = bw + D.rowoff;
     const float* val = fw(D.val);
     const uint16_t* col = hw(D.col);
+    const uint32_t e0 = ro[i], e1 = ro[i + 1];
     float sigma = 0.0f;
-    for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) sigma += val[e] * xin[col[e]];
+    for (uint32_t c0 = e0; c0 < e1; c0 += TK) {
+      float vv[TK], xg[TK];
+      uint32_t jj[TK];
+#pragma unroll
+      for (uint32_t k = 0; k < TK; ++k) {
+        const uint32_t e = min(c0 + k, e1 - 1);
+        jj[k] = col[e];
+        vv[k] = val[e];
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < TK; ++k) xg[k] = xin[jj[k]];
+#pragma unroll
+      for (uint32_t k = 0; k < TK; ++k)
+        if (c0 + k < e1) sigma += vv[k] * xg[k];
+    }
     return wmix(xin[i], (B[i] - sigma) / fw(D.de)[i], 0.8f);
   };
   for (int l = first; l + 1 < nlev; ++l) {
@@ -2295,12 +2327,30 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       const float xti = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
       XT[i] = xti;
       const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
+      const float dvi = dv[i];
       float ax = 0.0f;
-      for (uint32_t r = 0; r <= len; ++r) {
-        if (r == dr) ax += dv[i] * xti;
-        if (r == len) break;
-        const uint32_t j = col[e0 + r];
-        ax += val[e0 + r] * wmix(0.0f, (B[j] - 0.0f) / de[j], 0.8f);
+      for (uint32_t r0 = 0; r0 <= len; r0 += TK) {
+        float vv[TK], bj[TK], dj[TK];
+        uint32_t jj[TK];
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) {
+          const uint32_t e = e0 + min(r0 + k, len > 0 ? len - 1 : 0u);  // clamped: a row's own entries
+          jj[k] = len > 0 ? col[e] : i;
+          vv[k] = len > 0 ? val[e] : 0.0f;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) {
+          bj[k] = B[jj[k]];
+          dj[k] = de[jj[k]];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) {
+          const uint32_t r = r0 + k;
+          if (r > len) break;
+          if (r == dr) ax += dvi * xti;
+          if (r == len) break;
+          ax += vv[k] * wmix(0.0f, (bj[k] - 0.0f) / dj[k], 0.8f);
+        }
       }
       Rr[i] = B[i] - ax;
     }
@@ -2311,7 +2361,15 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       const uint16_t* rcol = hw(D.r_col);
       for (uint32_t I = t; I < D.nc; I += nt) {
         float sum = 0.0f;
-        for (uint32_t k = rrow[I]; k < rrow[I + 1]; ++k) sum += 1.0f * Rr[rcol[k]];
+        const uint32_t k0 = rrow[I], k1 = rrow[I + 1];
+        for (uint32_t c0 = k0; c0 < k1; c0 += TK) {
+          float rv[TK];
+#pragma unroll
+          for (uint32_t k = 0; k < TK; ++k) rv[k] = Rr[rcol[min(c0 + k, k1 - 1)]];
+#pragma unroll
+          for (uint32_t k = 0; k < TK; ++k)
+            if (c0 + k < k1) sum += 1.0f * rv[k];
+        }
         CB[I] = sum;
       }
     }
@@ -2370,9 +2428,26 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     const float* de = fw(D.de);
     for (uint32_t i = t; i < D.n; i += nt) {
       float sigma = 0.0f;
-      for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) {
-        const uint32_t j = col[e];
-        sigma += val[e] * prolonged(XT[j], XC[agg[j]]);
+      const uint32_t e0 = ro[i], e1 = ro[i + 1];
+      for (uint32_t c0 = e0; c0 < e1; c0 += TK) {
+        float vv[TK], xv[TK], cv[TK];
+        uint32_t jj[TK], aa[TK];
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) {
+          const uint32_t e = min(c0 + k, e1 - 1);
+          jj[k] = col[e];
+          vv[k] = val[e];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) {
+          xv[k] = XT[jj[k]];
+          aa[k] = agg[jj[k]];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k) cv[k] = XC[aa[k]];
+#pragma unroll
+        for (uint32_t k = 0; k < TK; ++k)
+          if (c0 + k < e1) sigma += vv[k] * prolonged(xv[k], cv[k]);
       }
       X[i] = wmix(prolonged(XT[i], XC[agg[i]]), (B[i] - sigma) / de[i], 0.8f);
     }
@@ -2569,14 +2644,13 @@ void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) 
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
                             const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s,
-                            bool rev) {
+                            bool rev, bool ntb) {
   if (!N) return;
-  if (N >= CFD_CGS_SER_MIN_CELLS)
-    hipLaunchKernelGGL(k_cgs_update_norm<true>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
-                       m1, N, U, partial, rev ? 1 : 0);
-  else
-    hipLaunchKernelGGL(k_cgs_update_norm<false>, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H,
-                       m1, N, U, partial, rev ? 1 : 0);
+  const bool ser = N >= CFD_CGS_SER_MIN_CELLS;
+  auto fn = ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
+                : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
+  hipLaunchKernelGGL(fn, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial,
+                     rev ? 1 : 0);
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, float* host_resid, hipStream_t s) {

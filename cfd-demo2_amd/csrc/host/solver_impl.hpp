@@ -343,6 +343,9 @@ struct Solver {
   // basis read nontemporal, both passes bottom-up (CFD_CGS_KEEP_MB; default
   // set in the constructor: 64 MB below 2^22 cells, else 0)
   size_t cgs_keep_bytes = 0;
+  // CGS update: nontemporal basis loads / new-vector store even when the
+  // whole basis fits the kept bytes (CFD_CGS_UPDATE_NT=1; A/B)
+  bool cgs_update_nt = false;
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {
