@@ -2216,9 +2216,6 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 }
 
 
-#ifndef CFD_TAIL_TK
-#define CFD_TAIL_TK 8
-#endif
 // The LDS tail with every matrix of the tail levels in LDS as well (the blob
 // built once by the host from the level images: off-diagonal CSR with u16
 // columns, dv/de, drank, P and R).  Each phase is then LDS reads + one
@@ -2278,33 +2275,12 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
   __syncthreads();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
   auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
-  // Row loops in chunks of TK entries: every column (and value) of a chunk
-  // read from LDS first, then every gather, then the accumulation in entry
-  // order -- two dependent LDS round trips per chunk instead of two per
-  // entry (round 5); the same operations in the same order.  CFD_TAIL_TK=1
-  // is the per-entry form (A/B variant).
-  constexpr uint32_t TK = CFD_TAIL_TK;
   auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
     const uint32_t* ro = bw + D.rowoff;
     const float* val = fw(D.val);
     const uint16_t* col = hw(D.col);
-    const uint32_t e0 = ro[i], e1 = ro[i + 1];
     float sigma = 0.0f;
-    for (uint32_t c0 = e0; c0 < e1; c0 += TK) {
-      float vv[TK], xg[TK];
-      uint32_t jj[TK];
-#pragma unroll
-      for (uint32_t k = 0; k < TK; ++k) {
-        const uint32_t e = min(c0 + k, e1 - 1);
-        jj[k] = col[e];
-        vv[k] = val[e];
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < TK; ++k) xg[k] = xin[jj[k]];
-#pragma unroll
-      for (uint32_t k = 0; k < TK; ++k)
-        if (c0 + k < e1) sigma += vv[k] * xg[k];
-    }
+    for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) sigma += val[e] * xin[col[e]];
     return wmix(xin[i], (B[i] - sigma) / fw(D.de)[i], 0.8f);
   };
   for (int l = first; l + 1 < nlev; ++l) {
@@ -2327,30 +2303,12 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       const float xti = wmix(0.0f, (B[i] - 0.0f) / de[i], 0.8f);
       XT[i] = xti;
       const uint32_t e0 = ro[i], len = ro[i + 1] - e0, dr = drank[i];
-      const float dvi = dv[i];
       float ax = 0.0f;
-      for (uint32_t r0 = 0; r0 <= len; r0 += TK) {
-        float vv[TK], bj[TK], dj[TK];
-        uint32_t jj[TK];
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) {
-          const uint32_t e = e0 + min(r0 + k, len > 0 ? len - 1 : 0u);  // clamped: a row's own entries
-          jj[k] = len > 0 ? col[e] : i;
-          vv[k] = len > 0 ? val[e] : 0.0f;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) {
-          bj[k] = B[jj[k]];
-          dj[k] = de[jj[k]];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) {
-          const uint32_t r = r0 + k;
-          if (r > len) break;
-          if (r == dr) ax += dvi * xti;
-          if (r == len) break;
-          ax += vv[k] * wmix(0.0f, (bj[k] - 0.0f) / dj[k], 0.8f);
-        }
+      for (uint32_t r = 0; r <= len; ++r) {
+        if (r == dr) ax += dv[i] * xti;
+        if (r == len) break;
+        const uint32_t j = col[e0 + r];
+        ax += val[e0 + r] * wmix(0.0f, (B[j] - 0.0f) / de[j], 0.8f);
       }
       Rr[i] = B[i] - ax;
     }
@@ -2361,15 +2319,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       const uint16_t* rcol = hw(D.r_col);
       for (uint32_t I = t; I < D.nc; I += nt) {
         float sum = 0.0f;
-        const uint32_t k0 = rrow[I], k1 = rrow[I + 1];
-        for (uint32_t c0 = k0; c0 < k1; c0 += TK) {
-          float rv[TK];
-#pragma unroll
-          for (uint32_t k = 0; k < TK; ++k) rv[k] = Rr[rcol[min(c0 + k, k1 - 1)]];
-#pragma unroll
-          for (uint32_t k = 0; k < TK; ++k)
-            if (c0 + k < k1) sum += 1.0f * rv[k];
-        }
+        for (uint32_t k = rrow[I]; k < rrow[I + 1]; ++k) sum += 1.0f * Rr[rcol[k]];
         CB[I] = sum;
       }
     }
@@ -2428,26 +2378,9 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     const float* de = fw(D.de);
     for (uint32_t i = t; i < D.n; i += nt) {
       float sigma = 0.0f;
-      const uint32_t e0 = ro[i], e1 = ro[i + 1];
-      for (uint32_t c0 = e0; c0 < e1; c0 += TK) {
-        float vv[TK], xv[TK], cv[TK];
-        uint32_t jj[TK], aa[TK];
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) {
-          const uint32_t e = min(c0 + k, e1 - 1);
-          jj[k] = col[e];
-          vv[k] = val[e];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) {
-          xv[k] = XT[jj[k]];
-          aa[k] = agg[jj[k]];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k) cv[k] = XC[aa[k]];
-#pragma unroll
-        for (uint32_t k = 0; k < TK; ++k)
-          if (c0 + k < e1) sigma += vv[k] * prolonged(xv[k], cv[k]);
+      for (uint32_t e = ro[i]; e < ro[i + 1]; ++e) {
+        const uint32_t j = col[e];
+        sigma += val[e] * prolonged(XT[j], XC[agg[j]]);
       }
       X[i] = wmix(prolonged(XT[i], XC[agg[i]]), (B[i] - sigma) / de[i], 0.8f);
     }

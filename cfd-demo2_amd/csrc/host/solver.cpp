@@ -1559,10 +1559,13 @@ void Solver::iteration(int j, float* pin) {
   });
   launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
   launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
-  // the whole basis and w within the kept bytes (small meshes): the dots pass
-  // already reads every block with the default policy (launch_cgs_dots), and
-  // the update reads / writes the basis with it too, from the caches
-  const bool basis_kept = (size_t)(j + 2) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
+  // the whole restart basis and w within the kept bytes (small meshes): the
+  // dots pass already reads every block with the default policy
+  // (launch_cgs_dots), and the update reads / writes the basis with it too,
+  // from the caches.  C0 21.2 -> 12.4 us per launch, -1.3 to -1.6 ms/step;
+  // on C1's first iterations alone (the j + 2 vectors fitting) it lost
+  // ≈ 0.1-0.2 ms/step, hence the whole-basis test (profiles/r05/ab_log.md).
+  const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
   launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0,
                          !basis_kept);
   launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
