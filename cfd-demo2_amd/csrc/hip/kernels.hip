@@ -1144,20 +1144,71 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
   }
   store_cells3_stream<FULL, NTB>(basis + (size_t)(j + 1) * stride, N, wn, b);
 }
-template <bool SER, bool NTB = true>
+// k_cgs_reduce's totals computed by every block of the update for itself (one
+// GPU, at most 256 padded units: meshes up to ≈ 260 k cells).  The canonical
+// total of a vector (red_total: segment trees of GU units, then the tree over
+// the P segment values) is the pairwise tree over its unit partials padded
+// with +0 to T = P GU values; here L = T / K lanes hold K = min(4, T)
+// consecutive units each and a lane tree finishes it -- the same tree.  All
+// (j + 1) L lane slots are loaded before any tree (RB rounds of the block in
+// flight).  hcol[ii] = the total of vector ii.
+__device__ __forceinline__ void cgs_reduce_local(const RedSrc& r, int j, float* hcol) {
+  const uint32_t T = pow2_ceil(r.nseg) * r.G, K = T >= 4 ? 4u : T, L = T / K;
+  const uint32_t slots = (uint32_t)(j + 1) * L;
+  constexpr int RB = 4;
+  for (uint32_t base = 0; base < slots; base += RB * kBlock) {
+    float e[RB][4];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      const uint32_t sl = base + rr * kBlock + threadIdx.x;
+      const uint32_t ii = sl / L, k0 = (sl % L) * K;
+      const float* pv = r.p + (size_t)ii * r.stride;
+      if (K == 4 && sl < slots && k0 + 3 < r.nchunks) {  // stride and k0 multiples of 4
+        const float4 q = *reinterpret_cast<const float4*>(pv + k0);
+        e[rr][0] = q.x;
+        e[rr][1] = q.y;
+        e[rr][2] = q.z;
+        e[rr][3] = q.w;
+        continue;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) e[rr][q] = (sl < slots && q < K && k0 + q < r.nchunks) ? pv[k0 + q] : 0.0f;
+    }
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      float v = K == 4 ? (e[rr][0] + e[rr][1]) + (e[rr][2] + e[rr][3]) : (K == 2 ? e[rr][0] + e[rr][1] : e[rr][0]);
+      for (uint32_t st = 1; st < L; st <<= 1) v = v + __shfl_down(v, st);
+      const uint32_t sl = base + rr * kBlock + threadIdx.x;
+      if (sl < slots && sl % L == 0) hcol[sl / L] = v;
+    }
+  }
+}
+
+// FR: the CGS totals reduced in the kernel (cgs_reduce_local from the dots'
+// unit partials fr; block 0 stores the Hessenberg column) instead of by
+// k_cgs_reduce -- one launch fewer per FGMRES iteration on small meshes
+template <bool SER, bool NTB = true, bool FR = false>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
                                                             const float* __restrict__ binv,
                                                             size_t stride, int j,
-                                                            const float* __restrict__ H, int m1,
-                                                            uint32_t N, uint32_t U, float* partial, int rev) {
+                                                            float* __restrict__ H, int m1,
+                                                            uint32_t N, uint32_t U, float* partial, int rev,
+                                                            RedSrc fr) {
   __shared__ float hcol[64], scol[64], ql[16];
   const uint32_t b = rev ? gridDim.x - 1u - blockIdx.x : blockIdx.x;  // rev: top-down (after the dots)
-  if (threadIdx.x <= (unsigned)j) {
-    hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
-    scol[threadIdx.x] = binv[threadIdx.x];
+  if constexpr (FR) {
+    if (threadIdx.x <= (unsigned)j) scol[threadIdx.x] = binv[threadIdx.x];
+    cgs_reduce_local(fr, j, hcol);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x <= (unsigned)j) H[(size_t)j * m1 + threadIdx.x] = hcol[threadIdx.x];
+  } else {
+    if (threadIdx.x <= (unsigned)j) {
+      hcol[threadIdx.x] = H[(size_t)j * m1 + threadIdx.x];
+      scol[threadIdx.x] = binv[threadIdx.x];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   float t[4];
   if (block_full(N, b))
     cgs_update_cells<true, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
@@ -2575,15 +2626,21 @@ void launch_cgs_dots(const float* w, const float* basis, const float* binv, size
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s) {
   hipLaunchKernelGGL(k_cgs_reduce, dim3(j + 1), dim3(kRedFinalThreads), 0, s, r, j, H, m1);
 }
-void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s,
-                            bool rev, bool ntb) {
+bool cgs_reduce_fusable(const RedSrc& r) {
+  return !r.seg_src && (uint64_t)pow2_ceil(r.nseg) * r.G <= 256u;
+}
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
+                            int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev, bool ntb,
+                            const RedSrc* fr) {
   if (!N) return;
   const bool ser = N >= CFD_CGS_SER_MIN_CELLS;
-  auto fn = ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
-                : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
+  if (fr && (ser || !cgs_reduce_fusable(*fr)))
+    throw std::logic_error("launch_cgs_update_norm: fused CGS reduction past its size limit");
+  auto fn = fr ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
+               : ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
+                     : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
   hipLaunchKernelGGL(fn, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial,
-                     rev ? 1 : 0);
+                     rev ? 1 : 0, fr ? *fr : RedSrc{});
 }
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,
                         float* resid_hist, float* host_resid, hipStream_t s) {

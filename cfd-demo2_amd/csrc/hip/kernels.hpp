@@ -301,9 +301,13 @@ void launch_cgs_dots(const float* w, const float* basis, const float* binv, size
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
 // W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
-void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j,
-                            const float* H, int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s,
-                            bool rev = false, bool ntb = true);
+// fr != null: the CGS totals (H column j) reduced inside the update from the
+// dots' unit partials (k_cgs_reduce not launched); only where
+// cgs_reduce_fusable(*fr) holds -- one GPU, at most 256 padded units
+void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
+                            int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev = false,
+                            bool ntb = true, const RedSrc* fr = nullptr);
+bool cgs_reduce_fusable(const RedSrc& r);
 // ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|,
 // also into host_resid[j] (device view of pinned host memory) when non-null
 void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens, float* g, float* binv,

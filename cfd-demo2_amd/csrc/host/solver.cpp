@@ -95,6 +95,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   cgs_keep_bytes = N < (1u << 22) ? (size_t)64 << 20 : 0;  // (kernels.hip CFD_CGS_SER_MIN_CELLS)
   if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
   if (const char* cu = std::getenv("CFD_CGS_UPDATE_NT")) cgs_update_nt = cu[0] == '1';
+  if (const char* cf = std::getenv("CFD_CGS_FUSE_REDUCE")) cgs_fuse_reduce = cf[0] != '0';
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   amg_local = dist() && cfg.amg_local_aggregation != 0;
   {
@@ -1558,7 +1559,9 @@ void Solver::iteration(int j, float* pin) {
     launch_spmv(A, zj, w, stream, nullptr, nt(8));
   });
   launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
-  launch_cgs_reduce(combine(partial, j + 1), j, H, m1, stream);
+  const RedSrc dots = combine(partial, j + 1);
+  const bool fuse_reduce = cgs_fuse_reduce && cgs_reduce_fusable(dots);
+  if (!fuse_reduce) launch_cgs_reduce(dots, j, H, m1, stream);
   // the whole restart basis and w within the kept bytes (small meshes): the
   // dots pass already reads every block with the default policy
   // (launch_cgs_dots), and the update reads / writes the basis with it too,
@@ -1567,7 +1570,7 @@ void Solver::iteration(int j, float* pin) {
   // ≈ 0.1-0.2 ms/step, hence the whole-basis test (profiles/r05/ab_log.md).
   const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
   launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0,
-                         !basis_kept);
+                         !basis_kept, fuse_reduce ? &dots : nullptr);
   launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
   check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
 }

@@ -346,6 +346,9 @@ struct Solver {
   // CGS update: nontemporal basis loads / new-vector store even when the
   // whole basis fits the kept bytes (CFD_CGS_UPDATE_NT=1; A/B)
   bool cgs_update_nt = false;
+  // small meshes: the CGS totals reduced inside the update kernel
+  // (CFD_CGS_FUSE_REDUCE=0: k_cgs_reduce launched as on large meshes)
+  bool cgs_fuse_reduce = true;
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {
