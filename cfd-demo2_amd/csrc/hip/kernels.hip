@@ -2192,7 +2192,7 @@ __global__ void __launch_bounds__(1024) k_amg_tail(const AmgTailLevel* __restric
 // memory, x of every tail level known zero (cleared by the restriction), so
 // each pre-smoother is the elementwise zero-x sweep.  Exit: x of `first`
 // written back for the host-side prolongation.
-__host__ __device__ __forceinline__ uint32_t r4(uint32_t n) { return (n + 3) & ~3u; }
+__device__ __forceinline__ uint32_t r4(uint32_t n) { return (n + 3) & ~3u; }
 
 __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __restrict__ tail, int first,
                                                        int nlev) {
@@ -2274,53 +2274,19 @@ __global__ void __launch_bounds__(1024) k_amg_tail_lds(const AmgTailLevel* __res
 // arithmetic, in the same order, as smooth_row / residual_row.
 // The zero-x pre-smoother is fused with the residual, and the prolongation
 // with the post-smoother (two barriers fewer per level, round 3).
-//
-// HYB (round 5): one more level G = first - 1 on top of the image levels,
-// whose matrix does not fit the LDS image (C0's 2.8 k-row level 1, C1's
-// 3.6 k-row level 5): its vectors (pre-smoothed x, b, r, agg) live in LDS and
-// its matrix is read from the level image in global memory (L2), a thread's
-// kTailHybRows rows' slot loads issued together per group of 4 slots.  Its
-// phases replace two row-kernel launches (the fused residual + restriction
-// and the fused prolongation + post-smoother) with the same f32 operations:
-// zero-x pre-smoother (k_amg_smooth_zero), residual (k_amg_resrestrict's
-// order: slots, the diagonal at its rank), restriction (restrict_sum) into
-// the first image level's b in LDS; after the image levels, the post-smoother
-// reading x + P x_c (k_amg_smooth<..., PRO>), stored to G's x for the
-// host-side prolongation of level G - 1.  Entry: b of G (b_first, n_first).
-constexpr uint32_t kTailHybRows = 4;  // rows per thread of level G: n_G <= 4096
-template <bool HYB>
 __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __restrict__ tail,
                                                         const TailBlobLevel* __restrict__ desc,
                                                         const uint32_t* __restrict__ blob, uint32_t blob_words,
                                                         uint32_t vec_floats, int first, int nlev,
-                                                        const float* __restrict__ b_first, uint32_t n_first,
-                                                        AmgLevelDev G, float* __restrict__ x_g) {
+                                                        const float* __restrict__ b_first, uint32_t n_first) {
   extern __shared__ float sm[];
   const uint32_t t = threadIdx.x, nt = blockDim.x;
   uint32_t* bw = reinterpret_cast<uint32_t*>(sm + vec_floats);
-  // level G's region (HYB): XT, B, R, agg of r4(n_G) entries each, then the image levels' vectors
-  const uint32_t gnr = HYB ? r4(G.n) : 0u;
-  float* const XTg = sm;
-  float* const Bg = sm + gnr;
-  float* const Rg = sm + 2 * gnr;
-  uint32_t* const AGg = reinterpret_cast<uint32_t*>(sm + 3 * gnr);
   auto base = [&](int l) {
-    uint32_t o = 4 * gnr;
+    uint32_t o = 0;
     for (int k = first; k < l; ++k) o += 4 * r4(desc[k].n);
     return sm + o;
   };
-  // level G's smoother diagonals and aggregates of this thread's rows, loaded
-  // with the image (the aggregates are stored to LDS after it)
-  [[maybe_unused]] float deg[kTailHybRows];
-  [[maybe_unused]] uint32_t agv[kTailHybRows];
-  if constexpr (HYB) {
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) {
-      const uint32_t i = min(t + k * 1024u, G.n - 1);
-      deg[k] = G.de[i];
-      agv[k] = G.agg[i];
-    }
-  }
   {
     // every global load of the blob and of b issued before the first LDS
     // store: one memory round trip instead of one per 16 KiB pass (the blob
@@ -2352,88 +2318,14 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
       const uint32_t w = 4 * (t + k * NT);
       if (w < blob_words) *reinterpret_cast<uint4*>(bw + w) = v[k];
     }
-    float* B0 = HYB ? Bg : base(first) + 2 * r4(n);
+    float* B0 = base(first) + 2 * r4(n);
 #pragma unroll
     for (uint32_t k = 0; k < KV; ++k)
       if (t + k * NT < n) B0[t + k * NT] = bv[k];
-    if constexpr (HYB) {
-#pragma unroll
-      for (uint32_t k = 0; k < kTailHybRows; ++k)
-        if (t + k * NT < G.n) AGg[t + k * NT] = agv[k];
-    }
   }
   __syncthreads();
   auto fw = [&](uint32_t off) { return reinterpret_cast<const float*>(bw + off); };
   auto hw = [&](uint32_t off) { return reinterpret_cast<const uint16_t*>(bw + off); };
-  // level G's slot groups: for r0 = 0, 4, ... below the ELL width, the
-  // thread's rows' 4 slots each (clamped to the width, columns of slots past
-  // a row's length replaced by the row itself), then fn(k, i, r0, v, xc)
-  [[maybe_unused]] auto g_groups = [&](auto&& fn) {
-    const uint32_t wg = (uint32_t)max(G.w, 1);
-    uint32_t r0 = 0;
-    for (; r0 < wg; r0 += 4) {
-      float v[kTailHybRows][4];
-      int c[kTailHybRows][4];
-#pragma unroll
-      for (uint32_t k = 0; k < kTailHybRows; ++k) {
-        const uint32_t i = min(t + k * 1024u, G.n - 1);
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
-          const size_t off = (size_t)min(r0 + u, wg - 1u) * G.stride + i;
-          v[k][u] = G.val[off];
-          c[k][u] = col_at(G, off, i);
-        }
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < kTailHybRows; ++k) fn(k, r0, v[k], c[k]);
-    }
-    return r0;
-  };
-  [[maybe_unused]] uint32_t glen[kTailHybRows], gdr[kTailHybRows];
-  if constexpr (HYB) {
-    // zero-x pre-smoother of G (its x was cleared by level G - 1's restriction)
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) {
-      const uint32_t i = t + k * 1024u;
-      if (i < G.n) XTg[i] = wmix(0.0f, (Bg[i] - 0.0f) / deg[k], 0.8f);
-      const uint32_t ic = min(i, G.n - 1);
-      glen[k] = G.len[ic];
-      gdr[k] = G.drank[ic];
-    }
-    __syncthreads();
-    // residual: slots in order, the diagonal at its rank (k_amg_resrestrict)
-    float ax[kTailHybRows], dvg[kTailHybRows], xtg[kTailHybRows];
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) {
-      const uint32_t ic = min(t + k * 1024u, G.n - 1);
-      ax[k] = 0.0f;
-      dvg[k] = G.dv[ic];
-      xtg[k] = XTg[ic];
-    }
-    const uint32_t rend = g_groups([&](uint32_t k, uint32_t r0, const float* v, const int* c) {
-      const uint32_t i = min(t + k * 1024u, G.n - 1);
-      float xg[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) xg[u] = XTg[r0 + u < glen[k] ? c[u] : (int)i];
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) {
-        const uint32_t r = r0 + u;
-        if (r == gdr[k]) ax[k] += dvg[k] * xtg[k];
-        if (r < glen[k]) ax[k] += v[u] * xg[u];
-      }
-    });
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) {
-      const uint32_t i = t + k * 1024u;
-      if (gdr[k] >= rend) ax[k] += dvg[k] * xtg[k];  // a diagonal ranked after every slot comes last
-      if (i < G.n) Rg[i] = Bg[i] - ax[k];
-    }
-    __syncthreads();
-    // restriction into the first image level's b
-    float* CB = base(first) + 2 * r4(desc[first].n);
-    for (uint32_t I = t; I < G.nc; I += nt) CB[I] = restrict_sum(G, Rg, I);
-    __syncthreads();
-  }
   auto smooth = [&](const TailBlobLevel& D, const float* xin, const float* B, uint32_t i) {
     const uint32_t* ro = bw + D.rowoff;
     const float* val = fw(D.val);
@@ -2546,33 +2438,8 @@ __global__ void __launch_bounds__(1024) k_amg_tail_blob(const AmgTailLevel* __re
     __syncthreads();
   }
   const float* X0 = base(first);
-  if constexpr (HYB) {
-    // level G: prolongation from the first image level + post-smoother
-    // (k_amg_smooth<..., PRO>: every value read is prolonged as it is read)
-    float sg[kTailHybRows];
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) sg[k] = 0.0f;
-    g_groups([&](uint32_t k, uint32_t r0, const float* v, const int* c) {
-      const uint32_t i = min(t + k * 1024u, G.n - 1);
-      float xg[4];
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u) {
-        const int j = r0 + u < glen[k] ? c[u] : (int)i;
-        xg[u] = prolonged(XTg[j], X0[AGg[j]]);
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < 4; ++u)
-        if (r0 + u < glen[k]) sg[k] += v[u] * xg[u];
-    });
-#pragma unroll
-    for (uint32_t k = 0; k < kTailHybRows; ++k) {
-      const uint32_t i = t + k * 1024u;
-      if (i < G.n) x_g[i] = wmix(prolonged(XTg[i], X0[AGg[i]]), (Bg[i] - sg[k]) / deg[k], 0.8f);
-    }
-  } else {
-    float* gx = tail[first].x;
-    for (uint32_t i = t; i < desc[first].n; i += nt) gx[i] = X0[i];
-  }
+  float* gx = tail[first].x;
+  for (uint32_t i = t; i < desc[first].n; i += nt) gx[i] = X0[i];
 }
 
 // ---------------------- check_evolution statistics --------------------------
@@ -2911,23 +2778,13 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 }
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, const float* b_first,
-                          uint32_t n_first, hipStream_t s, const AmgLevelDev* hyb, float* x_hyb) {
-  if (hyb) {  // level G = first - 1 from global memory: its 4 vectors in front of the image levels'
-    if (hyb->n == 0 || hyb->n > 1024u * kTailHybRows || hyb->n != n_first || hyb->len16 || !x_hyb)
-      throw std::invalid_argument("AMG hybrid tail: level size / layout");
-    vec_floats += 4 * r4(hyb->n);
-  }
+                          uint32_t n_first, hipStream_t s) {
   const size_t lds = 4 * ((size_t)vec_floats + blob_words);
   if (lds > kTailLdsMax || blob_words % 4 || blob_words == 0) throw std::invalid_argument("AMG tail blob larger than the kernel's LDS image");
   if (n_first == 0 || 16 * (size_t)n_first > kTailLdsMax) throw std::invalid_argument("AMG tail: first level size");
-  if (hyb)
-    hipLaunchKernelGGL(k_amg_tail_blob<true>, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats,
-                       first, nlev, b_first, n_first, *hyb, x_hyb);
-  else
-    hipLaunchKernelGGL(k_amg_tail_blob<false>, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words,
-                       vec_floats, first, nlev, b_first, n_first, AmgLevelDev{}, nullptr);
+  hipLaunchKernelGGL(k_amg_tail_blob, dim3(1), dim3(1024), lds, s, tail, desc, blob, blob_words, vec_floats, first,
+                     nlev, b_first, n_first);
 }
-uint32_t amg_tail_hyb_floats(uint32_t n) { return 4 * r4(n); }
 // Per-device kernel attributes: the LDS-resident tail kernels take more than
 // the default 64 KiB of dynamic LDS.  The attribute belongs to the device that
 // is current when it is set, so each device gets it once (std::call_once per
@@ -2949,10 +2806,7 @@ size_t init_kernel_attributes(int device) {
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_lds),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob<true>),
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_amg_tail_blob),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim);
     status[device] = e;
     budget[device] = lim;

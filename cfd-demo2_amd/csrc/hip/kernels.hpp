@@ -369,15 +369,9 @@ void launch_amg_tail(const AmgTailLevel* tail, int first, int nlev, size_t lds_b
 // The LDS tail with the matrices in LDS too: `blob` (blob_words 32-bit words,
 // a multiple of 4) is copied into LDS after the vectors (vec_floats floats);
 // desc[l] describes level l (l in [first, nlev)).  lds_bytes = 4 * (vec_floats + blob_words).
-// hyb != null: level first - 1 (hyb, n <= 4096 rows, not wide) runs inside the
-// kernel too, its matrix read from global memory, its 4 vectors in LDS in
-// front of the image levels' (amg_tail_hyb_floats(n) more floats); b_first /
-// n_first are then that level's b and size, x_hyb its x (written).
 void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, const uint32_t* blob,
                           uint32_t blob_words, uint32_t vec_floats, int first, int nlev, const float* b_first,
-                          uint32_t n_first, hipStream_t s, const AmgLevelDev* hyb = nullptr,
-                          float* x_hyb = nullptr);
-uint32_t amg_tail_hyb_floats(uint32_t n);
+                          uint32_t n_first, hipStream_t s);
 // fine rows [f0, f1) (multiples of 4 but f1 = L.n; f1 = 0: all)
 // residual + restriction fused (k_amg_resrestrict; L.rr_agg > 0, replicated
 // or single-GPU level): coarse_b = R (b - A x), coarse_x cleared or the

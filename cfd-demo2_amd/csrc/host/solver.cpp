@@ -954,7 +954,6 @@ void Solver::drop_amg() {
   levels.clear();
   d_tail = nullptr;
   tail_blob_first = -1;
-  tail_hybrid = -1;
   d_tail_blob = nullptr;
   d_tail_desc = nullptr;
   tail_blob_words = tail_vec_floats = 0;
@@ -1072,20 +1071,6 @@ void Solver::ensure_amg() {
       if (t > t0 && levels[t - 1].wide) break;  // wide levels run only in the tail kernels
       build_tail_blob(t);
       if (tail_blob_first >= 0) tail_first = t;
-    }
-    // the level just above a shifted image joins the tail with its matrix in
-    // global memory (C0's 2.8 k-row level 1, C1's 3.6 k-row level 5): two
-    // row-kernel launches fewer per V-cycle (profiles/r05/ab_log.md)
-    const char* hy_env = std::getenv("CFD_AMG_TAIL_HYBRID");
-    const int g = tail_blob_first - 1;
-    if (!(hy_env && hy_env[0] == '0') && tail_blob_first > t0 && g >= std::max(1, dist() ? amg_g : 0)) {
-      const AmgGpuLevel& Gl = levels[g];
-      const size_t lds = 4 * ((size_t)tail_vec_floats + amg_tail_hyb_floats(Gl.dev.n) + tail_blob_words);
-      if (!Gl.wide && !Gl.dist && Gl.dev.n > 0 && Gl.dev.n <= 4096 && Gl.dev.nc == levels[g + 1].dev.n &&
-          lds <= lds_budget) {
-        tail_hybrid = g;
-        tail_first = g;
-      }
     }
   }
   sync();
@@ -1409,10 +1394,7 @@ void Solver::v_cycle() {
       timed_gather(kCommRepGather, off[rk + 1] - off[rk], [&] { comm->allgatherv_inplace(C.b, off, stream); });
     }
   }
-  if (tf < L && tf == tail_hybrid && tf + 1 == tail_blob_first) {
-    launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf + 1, L, levels[tf].b,
-                         levels[tf].dev.n, stream, &levels[tf].dev, levels[tf].x);
-  } else if (tf < L && tf == tail_blob_first) {
+  if (tf < L && tf == tail_blob_first) {
     launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf, L, levels[tf].b,
                          levels[tf].dev.n, stream);
   } else if (tf < L) {
@@ -2190,8 +2172,6 @@ double Solver::layout_step_bytes() const {
         vc += (12 * n + 4 * nc) + smooth;                              // prolongation, post-smoother
     } else if (i == down) {
       vc += 4.0 * tail_blob_words + 16.0 * tail_vec_floats;            // single-workgroup tail (LDS image in)
-      if (i == tail_hybrid)  // its first level from global memory: b, agg, diagonals in; the image read twice; x out
-        vc += 4 * n + 4 * n + 9 * n + 2 * (img + 2 * st) + 8 * levels[i + 1].dev.n + 4 * n + 4 * n;
     }
   }
   double inner = 0.0;

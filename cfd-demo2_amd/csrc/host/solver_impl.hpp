@@ -357,10 +357,6 @@ struct Solver {
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   // k_amg_tail_blob: LDS image of the tail levels [tail_blob_first, L) (-1: none)
   int tail_blob_first = -1;
-  // level tail_blob_first - 1 run inside the LDS tail with its matrix in
-  // global memory (k_amg_tail_blob<true>; -1: none).  CFD_AMG_TAIL_HYBRID=0
-  // keeps it on the row kernels.
-  int tail_hybrid = -1;
   uint32_t* d_tail_blob = nullptr;
   TailBlobLevel* d_tail_desc = nullptr;
   uint32_t tail_blob_words = 0, tail_vec_floats = 0;

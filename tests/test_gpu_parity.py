@@ -509,7 +509,6 @@ VARIANTS = [
     {"CFD_CGS_KEEP_MB": "1"},         # CGS dots' last blocks default-policy, update top-down
     {"CFD_CGS_FUSE_REDUCE": "0"},     # k_cgs_reduce launched (production: meshes past 256 reduction units)
     {"CFD_CGS_UPDATE_NT": "1"},       # nontemporal CGS update although the basis is cache-kept
-    {"CFD_AMG_TAIL_HYBRID": "0"},     # the level above a shifted LDS image on the row kernels
     {"CFD_AMG_FUSED_RR": "0"},        # separate residual + restriction kernels on every level
     {"CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused residual-restriction on every level, predicated loads
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
@@ -570,36 +569,10 @@ def test_amg_blob_shift_parity(shift, monkeypatch, capfd):
     tail, blob = int(m.group(1)), int(m.group(2))
     if shift == "0":
         assert blob == -1 and tail == 1, (tail, blob)  # level 1's image does not fit: no image tail
-    elif blob >= 0:  # the level above a shifted image may join it from global memory (hybrid tail)
-        assert blob in (tail, tail + 1) and 1 < blob <= 1 + int(shift), (tail, blob)
+    elif blob >= 0:
+        assert blob == tail and 1 < tail <= 1 + int(shift), (tail, blob)
     else:
         assert tail == 1 and shift != "4", (tail, blob)  # four levels down the image fits
-
-
-@pytest.mark.parametrize("hybrid", ["1", "0"])
-def test_amg_tail_hybrid_parity(hybrid, monkeypatch, capfd):
-    """CFD_AMG_TAIL_HYBRID: the level above a shifted LDS image (here level 2,
-    2,571 rows, whose image does not fit; the image starts at level 3) runs
-    inside the tail kernel with its matrix read from global memory instead of
-    as two row-kernel launches (production: C0's level 1, C1's level 5) --
-    GPU == oracle bit-exact either way."""
-    monkeypatch.setenv("CFD_AMG_TAIL_HYBRID", hybrid)
-    monkeypatch.setenv("CFD_AMG_SETUP_TIMING", "1")
-    mesh = channel_obstacle(h=0.012)
-    g, o = _pair(mesh, fixed_outer=2, fixed_inner=8)
-    for s in (g, o):
-        _setup_amg_test(s, mesh, 1)
-    capfd.readouterr()
-    for k in range(2):
-        g.step()
-        o.step()
-        _assert_same_fields(g, o, f"hybrid {hybrid} step {k}")
-        _assert_same_info(g, o, f"hybrid {hybrid} step {k}")
-    import re
-    m = re.search(r"tail from level (-?\d+) \(LDS image from level (-?\d+)\)", capfd.readouterr().err)
-    assert m, "no AMG setup line"
-    tail, blob = int(m.group(1)), int(m.group(2))
-    assert blob == 3 and tail == (2 if hybrid == "1" else 3), (tail, blob)
 
 
 def test_midrun_api_changes_parity():
