@@ -1107,6 +1107,59 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
   }
 }
 
+// Latency form of the CGS passes for small meshes (round 5): with a few
+// blocks on a mostly idle chip each basis vector's loads are a dependent
+// round trip of their own when the loop over ii issues one vector at a time,
+// so C0's dots / update ran ≈ 10 / 12 us for ≈ 1 us of bytes.  Here KB
+// vectors are loaded together before any of them is used, and the dots are
+// spread over blockIdx.y (KB vectors per block, w read by each): the same
+// cell terms, quarter trees and unit values per vector and chunk, the update's
+// corrections accumulated in ii order as before.
+#ifndef CFD_CGS_LAT_MAX_CELLS
+#define CFD_CGS_LAT_MAX_CELLS (1u << 17)
+#endif
+constexpr int kCgsLatDots = 4, kCgsLatUpdate = 8;
+template <bool FULL, int KB>
+__device__ __forceinline__ void cgs_dots_cells_batch(const float* __restrict__ w, const float* __restrict__ basis,
+                                                     const float* __restrict__ binv, size_t stride, int ii0, int j,
+                                                     uint32_t N, float* ql) {
+  float wv[4][3], v[KB][4][3];
+  load_cells3<FULL>(w, N, wv);
+#pragma unroll
+  for (int k = 0; k < KB; ++k) load_cells3<FULL>(basis + (size_t)min(ii0 + k, j) * stride, N, v[k]);
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    if (ii0 + k > j) break;
+    const float sc = binv[ii0 + k];
+    float t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) v[k][q][e] = sc * v[k][q][e];
+      t[q] = cell_dot3(wv[q], v[k][q]);
+    }
+    quarter_trees(t, ql + 16 * k);
+  }
+}
+__global__ void __launch_bounds__(kBlock) k_cgs_dots_lat(const float* __restrict__ w,
+                                                         const float* __restrict__ basis,
+                                                         const float* __restrict__ binv, size_t stride, int j,
+                                                         uint32_t N, uint32_t U, float* partial, uint32_t np) {
+  constexpr int KB = kCgsLatDots;
+  __shared__ float ql[16 * KB];
+  const int ii0 = (int)blockIdx.y * KB;
+  if (block_full(N))
+    cgs_dots_cells_batch<true, KB>(w, basis, binv, stride, ii0, j, N, ql);
+  else
+    cgs_dots_cells_batch<false, KB>(w, basis, binv, stride, ii0, j, N, ql);
+  __syncthreads();
+  const uint32_t UB = 4 / U, nk = (uint32_t)min(KB, j + 1 - ii0);
+  for (uint32_t idx = threadIdx.x; idx < nk * UB; idx += kBlock) {
+    const uint32_t k = idx / UB, u = idx % UB, unit = blockIdx.x * UB + u;
+    if ((size_t)unit * U * kRedChunkCells < N) partial[(size_t)(ii0 + k) * np + unit] = unit_value_q(ql + 16 * k, U, u);
+  }
+}
+
 // reduce_dots_cgs (gmres_cgs.wgsl:86-120): H[j][ii] for ii = blockIdx.x
 __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j, float* H, int m1) {
   __shared__ float la[kRedMaxSegments], lb[65];
@@ -1120,11 +1173,38 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 // NTB: nontemporal basis loads and store of the new vector (the default);
 // false when the whole basis stays in the caches (small meshes, see
 // launch_cgs_update_norm)
-template <bool FULL, bool SER, bool NTB>
+template <bool FULL, bool SER, bool NTB, bool LAT = false>
 __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
                                                  const float* hcol, const float* scol, uint32_t N, float t[4],
                                                  uint32_t b) {
   float corr[4][3] = {};
+  if constexpr (LAT) {  // latency form (see k_cgs_dots_lat): kCgsLatUpdate vectors loaded per round trip
+    constexpr int KB = kCgsLatUpdate;
+    float wn[4][3];
+    load_cells3<FULL>(w, N, wn, b);
+    for (int ii0 = 0; ii0 <= j; ii0 += KB) {
+      float v[KB][4][3];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) load_cells3<FULL>(basis + (size_t)min(ii0 + k, j) * stride, N, v[k], b);
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (ii0 + k > j) break;
+        const float h = hcol[ii0 + k], sc = scol[ii0 + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) corr[q][e] += h * (sc * v[k][q][e]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) wn[q][e] = wn[q][e] - corr[q][e];
+      t[q] = cell_dot3(wn[q], wn[q]);
+    }
+    store_cells3_stream<FULL, false>(basis + (size_t)(j + 1) * stride, N, wn, b);
+    return;
+  }
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
@@ -1187,7 +1267,7 @@ __device__ __forceinline__ void cgs_reduce_local(const RedSrc& r, int j, float* 
 // FR: the CGS totals reduced in the kernel (cgs_reduce_local from the dots'
 // unit partials fr; block 0 stores the Hessenberg column) instead of by
 // k_cgs_reduce -- one launch fewer per FGMRES iteration on small meshes
-template <bool SER, bool NTB = true, bool FR = false>
+template <bool SER, bool NTB = true, bool FR = false, bool LAT = false>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
                                                             const float* __restrict__ binv,
@@ -1211,9 +1291,9 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   }
   float t[4];
   if (block_full(N, b))
-    cgs_update_cells<true, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<true, SER, NTB, LAT>(w, basis, stride, j, hcol, scol, N, t, b);
   else
-    cgs_update_cells<false, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<false, SER, NTB, LAT>(w, basis, stride, j, hcol, scol, N, t, b);
   quarter_trees(t, ql);
   __syncthreads();
   const uint32_t UB = 4 / U, unit = b * UB + threadIdx.x;
@@ -2609,10 +2689,17 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
                     : (nt ? k_spmv2<false, true> : k_spmv2<false, false>);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, x, y, b);
 }
+bool cgs_latency_form(uint32_t N) { return N <= CFD_CGS_LAT_MAX_CELLS; }
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t N,
-                     uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes) {
+                     uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes, bool lat) {
   if (!N) return;
   const uint32_t nb = red_blocks(N);
+  if (lat) {
+    if (!cgs_latency_form(N)) throw std::logic_error("launch_cgs_dots: latency form past its size limit");
+    hipLaunchKernelGGL(k_cgs_dots_lat, dim3(nb, (unsigned)(j + kCgsLatDots) / kCgsLatDots), dim3(kBlock), 0, s, w,
+                       basis, binv, stride, j, N, U, partial, np);
+    return;
+  }
   // the last blocks whose basis lines (j + 1 vectors + w, 12 B per cell each) fit keep_bytes
   const size_t keep_blocks = keep_bytes / ((size_t)(j + 2) * 12u * 1024u);
   const uint32_t tb = keep_blocks >= nb ? 0u : nb - (uint32_t)keep_blocks;
@@ -2631,14 +2718,17 @@ bool cgs_reduce_fusable(const RedSrc& r) {
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
                             int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev, bool ntb,
-                            const RedSrc* fr) {
+                            const RedSrc* fr, bool lat) {
   if (!N) return;
   const bool ser = N >= CFD_CGS_SER_MIN_CELLS;
   if (fr && (ser || !cgs_reduce_fusable(*fr)))
     throw std::logic_error("launch_cgs_update_norm: fused CGS reduction past its size limit");
-  auto fn = fr ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
-               : ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
-                     : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
+  if (lat && !cgs_latency_form(N)) throw std::logic_error("launch_cgs_update_norm: latency form past its size limit");
+  // the latency form stores and loads with the default policy (ntb ignored)
+  auto fn = lat ? (fr ? k_cgs_update_norm<false, false, true, true> : k_cgs_update_norm<false, false, false, true>)
+          : fr  ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
+          : ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
+                : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
   hipLaunchKernelGGL(fn, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial,
                      rev ? 1 : 0, fr ? *fr : RedSrc{});
 }

@@ -297,7 +297,8 @@ void launch_spmv(const CoupledMatrix& A, const float* x, float* y, hipStream_t s
 // keep_bytes > 0: the last blocks (their j + 2 vectors within keep_bytes) read
 // the basis with the default policy, for a top-down update (rev) after it
 void launch_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j,
-                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes = 0);
+                     uint32_t N, uint32_t U, float* partial, uint32_t np, hipStream_t s, size_t keep_bytes = 0,
+                     bool lat = false);
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
 // W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
@@ -306,7 +307,10 @@ void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
 // cgs_reduce_fusable(*fr) holds -- one GPU, at most 256 padded units
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
                             int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev = false,
-                            bool ntb = true, const RedSrc* fr = nullptr);
+                            bool ntb = true, const RedSrc* fr = nullptr, bool lat = false);
+// small meshes (<= CFD_CGS_LAT_MAX_CELLS): the CGS dots / update in their
+// latency form (several basis vectors per load round trip; same bits)
+bool cgs_latency_form(uint32_t N);
 bool cgs_reduce_fusable(const RedSrc& r);
 // ||W_{j+1}|| = sqrt(total of r) -> H[j+1,j], binv[j+1]; Givens update of column j; resid_hist[j] = |g[j+1]|,
 // also into host_resid[j] (device view of pinned host memory) when non-null

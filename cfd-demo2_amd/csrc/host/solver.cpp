@@ -96,6 +96,7 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
   if (const char* cu = std::getenv("CFD_CGS_UPDATE_NT")) cgs_update_nt = cu[0] == '1';
   if (const char* cf = std::getenv("CFD_CGS_FUSE_REDUCE")) cgs_fuse_reduce = cf[0] != '0';
+  if (const char* cl = std::getenv("CFD_CGS_LAT")) cgs_lat = cl[0] != '0';
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   amg_local = dist() && cfg.amg_local_aggregation != 0;
   {
@@ -1558,7 +1559,8 @@ void Solver::iteration(int j, float* pin) {
     A.r3 = b2;
     launch_spmv(A, zj, w, stream, nullptr, nt(8));
   });
-  launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes);
+  const bool lat = cgs_lat && cgs_latency_form(N);
+  launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes, lat);
   const RedSrc dots = combine(partial, j + 1);
   const bool fuse_reduce = cgs_fuse_reduce && cgs_reduce_fusable(dots);
   if (!fuse_reduce) launch_cgs_reduce(dots, j, H, m1, stream);
@@ -1570,7 +1572,7 @@ void Solver::iteration(int j, float* pin) {
   // ≈ 0.1-0.2 ms/step, hence the whole-basis test (profiles/r05/ab_log.md).
   const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
   launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0,
-                         !basis_kept, fuse_reduce ? &dots : nullptr);
+                         !basis_kept, fuse_reduce ? &dots : nullptr, lat);
   launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
   check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
 }

@@ -349,6 +349,9 @@ struct Solver {
   // small meshes: the CGS totals reduced inside the update kernel
   // (CFD_CGS_FUSE_REDUCE=0: k_cgs_reduce launched as on large meshes)
   bool cgs_fuse_reduce = true;
+  // small meshes: the CGS dots / update in their latency form (several basis
+  // vectors per load round trip; CFD_CGS_LAT=0: the streaming form)
+  bool cgs_lat = true;
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {
