@@ -1118,7 +1118,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs_dots(const float* __restrict__ w
 #ifndef CFD_CGS_LAT_MAX_CELLS
 #define CFD_CGS_LAT_MAX_CELLS (1u << 17)
 #endif
-constexpr int kCgsLatDots = 4, kCgsLatUpdate = 8;
+constexpr int kCgsLatDots = 4, kCgsLatUpdate = 20;
 template <bool FULL, int KB>
 __device__ __forceinline__ void cgs_dots_cells_batch(const float* __restrict__ w, const float* __restrict__ basis,
                                                      const float* __restrict__ binv, size_t stride, int ii0, int j,
@@ -1173,38 +1173,11 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_cgs_reduce(RedSrc r, int j
 // NTB: nontemporal basis loads and store of the new vector (the default);
 // false when the whole basis stays in the caches (small meshes, see
 // launch_cgs_update_norm)
-template <bool FULL, bool SER, bool NTB, bool LAT = false>
+template <bool FULL, bool SER, bool NTB>
 __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, float* basis, size_t stride, int j,
                                                  const float* hcol, const float* scol, uint32_t N, float t[4],
                                                  uint32_t b) {
   float corr[4][3] = {};
-  if constexpr (LAT) {  // latency form (see k_cgs_dots_lat): kCgsLatUpdate vectors loaded per round trip
-    constexpr int KB = kCgsLatUpdate;
-    float wn[4][3];
-    load_cells3<FULL>(w, N, wn, b);
-    for (int ii0 = 0; ii0 <= j; ii0 += KB) {
-      float v[KB][4][3];
-#pragma unroll
-      for (int k = 0; k < KB; ++k) load_cells3<FULL>(basis + (size_t)min(ii0 + k, j) * stride, N, v[k], b);
-#pragma unroll
-      for (int k = 0; k < KB; ++k) {
-        if (ii0 + k > j) break;
-        const float h = hcol[ii0 + k], sc = scol[ii0 + k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int e = 0; e < 3; ++e) corr[q][e] += h * (sc * v[k][q][e]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e) wn[q][e] = wn[q][e] - corr[q][e];
-      t[q] = cell_dot3(wn[q], wn[q]);
-    }
-    store_cells3_stream<FULL, false>(basis + (size_t)(j + 1) * stride, N, wn, b);
-    return;
-  }
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
@@ -1232,15 +1205,16 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
 // consecutive units each and a lane tree finishes it -- the same tree.  All
 // (j + 1) L lane slots are loaded before any tree (RB rounds of the block in
 // flight).  hcol[ii] = the total of vector ii.
+template <int NT = kBlock>
 __device__ __forceinline__ void cgs_reduce_local(const RedSrc& r, int j, float* hcol) {
   const uint32_t T = pow2_ceil(r.nseg) * r.G, K = T >= 4 ? 4u : T, L = T / K;
   const uint32_t slots = (uint32_t)(j + 1) * L;
-  constexpr int RB = 4;
-  for (uint32_t base = 0; base < slots; base += RB * kBlock) {
+  constexpr int RB = NT >= 1024 ? 1 : 4;  // 1,024 threads: one slot each per round (registers)
+  for (uint32_t base = 0; base < slots; base += RB * NT) {
     float e[RB][4];
 #pragma unroll
     for (int rr = 0; rr < RB; ++rr) {
-      const uint32_t sl = base + rr * kBlock + threadIdx.x;
+      const uint32_t sl = base + rr * NT + threadIdx.x;
       const uint32_t ii = sl / L, k0 = (sl % L) * K;
       const float* pv = r.p + (size_t)ii * r.stride;
       if (K == 4 && sl < slots && k0 + 3 < r.nchunks) {  // stride and k0 multiples of 4
@@ -1258,7 +1232,7 @@ __device__ __forceinline__ void cgs_reduce_local(const RedSrc& r, int j, float* 
     for (int rr = 0; rr < RB; ++rr) {
       float v = K == 4 ? (e[rr][0] + e[rr][1]) + (e[rr][2] + e[rr][3]) : (K == 2 ? e[rr][0] + e[rr][1] : e[rr][0]);
       for (uint32_t st = 1; st < L; st <<= 1) v = v + __shfl_down(v, st);
-      const uint32_t sl = base + rr * kBlock + threadIdx.x;
+      const uint32_t sl = base + rr * NT + threadIdx.x;
       if (sl < slots && sl % L == 0) hcol[sl / L] = v;
     }
   }
@@ -1267,7 +1241,7 @@ __device__ __forceinline__ void cgs_reduce_local(const RedSrc& r, int j, float* 
 // FR: the CGS totals reduced in the kernel (cgs_reduce_local from the dots'
 // unit partials fr; block 0 stores the Hessenberg column) instead of by
 // k_cgs_reduce -- one launch fewer per FGMRES iteration on small meshes
-template <bool SER, bool NTB = true, bool FR = false, bool LAT = false>
+template <bool SER, bool NTB = true, bool FR = false>
 __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restrict__ w,
                                                             float* basis,
                                                             const float* __restrict__ binv,
@@ -1291,13 +1265,87 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   }
   float t[4];
   if (block_full(N, b))
-    cgs_update_cells<true, SER, NTB, LAT>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<true, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
   else
-    cgs_update_cells<false, SER, NTB, LAT>(w, basis, stride, j, hcol, scol, N, t, b);
+    cgs_update_cells<false, SER, NTB>(w, basis, stride, j, hcol, scol, N, t, b);
   quarter_trees(t, ql);
   __syncthreads();
   const uint32_t UB = 4 / U, unit = b * UB + threadIdx.x;
   if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, threadIdx.x);
+}
+
+// Latency form of the update (small meshes, see k_cgs_dots_lat): blocks of
+// 1,024 threads, one cell per thread -- thread t of block b holds cell
+// 1024 b + t, so wavefront t / 64 holds quarter (t / 64) % 4 of chunk t / 256,
+// the cells of load_cells3's quarter -- and the first kCgsLatUpdate basis
+// vectors (3 floats each) loaded with w before the Hessenberg column is
+// known (with FR, while the totals are reduced): one round trip for
+// j < kCgsLatUpdate.  Corrections accumulated in ii order, the same norm
+// quarter trees and unit values as k_cgs_update_norm.
+template <bool FR>
+__global__ void __launch_bounds__(1024) k_cgs_update_norm_lat(const float* __restrict__ w, float* basis,
+                                                              const float* __restrict__ binv, size_t stride, int j,
+                                                              float* __restrict__ H, int m1, uint32_t N, uint32_t U,
+                                                              float* partial, RedSrc fr) {
+  constexpr int KB = kCgsLatUpdate;
+  __shared__ float hcol[64], scol[64], ql[16];
+  const uint32_t t = threadIdx.x;
+  const size_t c = (size_t)blockIdx.x * 1024u + t;
+  const bool in = c < N;
+  const size_t cc = in ? c : 0;
+  float wn[3], v[KB][3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) wn[e] = w[3 * cc + e];
+#pragma unroll
+  for (int k = 0; k < KB; ++k)
+#pragma unroll
+    for (int e = 0; e < 3; ++e) v[k][e] = basis[(size_t)min(k, j) * stride + 3 * cc + e];
+  if (t <= (unsigned)j) scol[t] = binv[t];
+  if constexpr (FR) {
+    cgs_reduce_local<1024>(fr, j, hcol);
+  } else {
+    if (t <= (unsigned)j) hcol[t] = H[(size_t)j * m1 + t];
+  }
+  __syncthreads();
+  if constexpr (FR) {
+    if (blockIdx.x == 0 && t <= (unsigned)j) H[(size_t)j * m1 + t] = hcol[t];
+  }
+  float corr[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    if (k <= j) {  // predicated, not a break: v stays in registers
+      const float h = hcol[k], sc = scol[k];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) corr[e] += h * (sc * v[k][e]);
+    }
+  }
+  for (int ii0 = KB; ii0 <= j; ii0 += KB) {  // j >= KB: further batches
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) v[k][e] = basis[(size_t)min(ii0 + k, j) * stride + 3 * cc + e];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      if (ii0 + k <= j) {
+        const float h = hcol[ii0 + k], sc = scol[ii0 + k];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) corr[e] += h * (sc * v[k][e]);
+      }
+    }
+  }
+  float tq = 0.0f;  // cells past N: 0 (load_cells3's zero cells)
+  if (in) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) wn[e] = wn[e] - corr[e];
+    tq = cell_dot3(wn, wn);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) basis[(size_t)(j + 1) * stride + 3 * c + e] = wn[e];
+  }
+  const float r = wave_tree64(tq);
+  if (red_lane() == 0) ql[t >> 6] = r;
+  __syncthreads();
+  const uint32_t UB = 4 / U, unit = blockIdx.x * UB + t;
+  if (t < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, t);
 }
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
@@ -2724,9 +2772,12 @@ void launch_cgs_update_norm(const float* w, float* basis, const float* binv, siz
   if (fr && (ser || !cgs_reduce_fusable(*fr)))
     throw std::logic_error("launch_cgs_update_norm: fused CGS reduction past its size limit");
   if (lat && !cgs_latency_form(N)) throw std::logic_error("launch_cgs_update_norm: latency form past its size limit");
-  // the latency form stores and loads with the default policy (ntb ignored)
-  auto fn = lat ? (fr ? k_cgs_update_norm<false, false, true, true> : k_cgs_update_norm<false, false, false, true>)
-          : fr  ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
+  if (lat) {  // default-policy loads and store (ntb and rev do not apply)
+    hipLaunchKernelGGL(fr ? k_cgs_update_norm_lat<true> : k_cgs_update_norm_lat<false>, dim3((N + 1023) / 1024),
+                       dim3(1024), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial, fr ? *fr : RedSrc{});
+    return;
+  }
+  auto fn = fr  ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
           : ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
                 : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);
   hipLaunchKernelGGL(fn, dim3(red_blocks(N)), dim3(kBlock), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial,
