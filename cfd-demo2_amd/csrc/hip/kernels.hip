@@ -1274,10 +1274,6 @@ __global__ void __launch_bounds__(kBlock) k_cgs_update_norm(const float* __restr
   if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, threadIdx.x);
 }
 
-template <int NT>
-__device__ __forceinline__ void norm_givens_block(const RedSrc& r, int j, float* H, int m1, float* givens, float* g,
-                                                  float* binv, float* resid_hist, float* host_resid, float* la,
-                                                  float* lb);
 // Latency form of the update (small meshes, see k_cgs_dots_lat): blocks of
 // 1,024 threads, one cell per thread -- thread t of block b holds cell
 // 1024 b + t, so wavefront t / 64 holds quarter (t / 64) % 4 of chunk t / 256,
@@ -1286,23 +1282,13 @@ __device__ __forceinline__ void norm_givens_block(const RedSrc& r, int j, float*
 // known (with FR, while the totals are reduced): one round trip for
 // j < kCgsLatUpdate.  Corrections accumulated in ii order, the same norm
 // quarter trees and unit values as k_cgs_update_norm.
-//
-// NG: the block that finishes last also runs k_norm_givens (the norm's total
-// from every block's unit partial, Hessenberg column, Givens rotation, binv,
-// residual estimate) -- one launch fewer per iteration.  The hand-off is the
-// counter form of cdna_hip_programming.md Guideline 16: each block's
-// partial stores drained, a release fence at agent scope, then a relaxed
-// agent-scope ticket; the block drawing the last ticket fences with acquire
-// before reading the partials, and resets the counter for the next launch.
-template <bool FR, bool NG = false>
+template <bool FR>
 __global__ void __launch_bounds__(1024) k_cgs_update_norm_lat(const float* __restrict__ w, float* basis,
-                                                              float* binv, size_t stride, int j,
+                                                              const float* __restrict__ binv, size_t stride, int j,
                                                               float* __restrict__ H, int m1, uint32_t N, uint32_t U,
-                                                              float* partial, RedSrc fr, RedSrc rn, float* givens,
-                                                              float* g, float* resid_hist, float* host_resid,
-                                                              uint32_t* ticket) {
+                                                              float* partial, RedSrc fr) {
   constexpr int KB = kCgsLatUpdate;
-  __shared__ float hcol[64], scol[64], ql[17];
+  __shared__ float hcol[64], scol[64], ql[16];
   const uint32_t t = threadIdx.x;
   const size_t c = (size_t)blockIdx.x * 1024u + t;
   const bool in = c < N;
@@ -1360,36 +1346,14 @@ __global__ void __launch_bounds__(1024) k_cgs_update_norm_lat(const float* __res
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + t;
   if (t < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(ql, U, t);
-  if constexpr (NG) {
-    __shared__ float la[kRedMaxSegments], lb[65];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t k = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ql[16] = (k == gridDim.x - 1) ? 1.0f : 0.0f;
-    }
-    __syncthreads();
-    if (ql[16] == 0.0f) return;
-    if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *ticket = 0u;  // every block has drawn: ready for the next launch
-    }
-    __syncthreads();
-    norm_givens_block<1024>(rn, j, H, m1, givens, g, binv, resid_hist, host_resid, la, lb);
-  }
 }
 
 // reduce_final_and_finish_norm (gmres_ops.wgsl:270-293) + update_hessenberg_givens
 // (gmres_logic.wgsl:24-76).
-// The body, run by a whole block of NT threads (NT >= j + 2): k_norm_givens,
-// and the last block of k_cgs_update_norm_lat<..., true> (the same operations).
-template <int NT>
-__device__ __forceinline__ void norm_givens_block(const RedSrc& r, int j, float* H, int m1, float* givens, float* g,
-                                                  float* binv, float* resid_hist, float* host_resid, float* la,
-                                                  float* lb) {
+__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
+                                                                  float* givens, float* g, float* binv,
+                                                                  float* resid_hist, float* host_resid) {
+  __shared__ float la[kRedMaxSegments], lb[65];
   // Hessenberg column j and the rotations so far, staged in LDS by the block
   // (issued before the reduction): the serial Givens chain then makes LDS
   // round trips instead of dependent global ones
@@ -1401,7 +1365,7 @@ __device__ __forceinline__ void norm_givens_block(const RedSrc& r, int j, float*
     gva = givens[2 * t];
     gvb = givens[2 * t + 1];
   }
-  const float s = red_total<float, NT>(r, 0, la, lb);  // ends with a barrier
+  const float s = red_total<float, kRedFinalThreads>(r, 0, la, lb);  // ends with a barrier
   float* hc = la;         // [j + 2]
   float* gv = la + 128;   // [2 j]
   if (t <= (uint32_t)j) hc[t] = hv;
@@ -1441,12 +1405,6 @@ __device__ __forceinline__ void norm_givens_block(const RedSrc& r, int j, float*
   // the host's lag-model read (coupled_solver.rs:326-435): written straight into
   // pinned host memory, so no copy is enqueued per iteration
   if (host_resid) host_resid[0] = fabsf(gn);
-}
-__global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int j, float* H, int m1,
-                                                                  float* givens, float* g, float* binv,
-                                                                  float* resid_hist, float* host_resid) {
-  __shared__ float la[kRedMaxSegments], lb[65];
-  norm_givens_block<kRedFinalThreads>(r, j, H, m1, givens, g, binv, resid_hist, host_resid, la, lb);
 }
 
 #ifndef CFD_PREDICT_U1
@@ -2808,24 +2766,17 @@ bool cgs_reduce_fusable(const RedSrc& r) {
 }
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
                             int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev, bool ntb,
-                            const RedSrc* fr, bool lat, const CgsGivens* ng) {
+                            const RedSrc* fr, bool lat) {
   if (!N) return;
   const bool ser = N >= CFD_CGS_SER_MIN_CELLS;
   if (fr && (ser || !cgs_reduce_fusable(*fr)))
     throw std::logic_error("launch_cgs_update_norm: fused CGS reduction past its size limit");
   if (lat && !cgs_latency_form(N)) throw std::logic_error("launch_cgs_update_norm: latency form past its size limit");
   if (lat) {  // default-policy loads and store (ntb and rev do not apply)
-    if (ng && (!ng->ticket || ng->rn.seg_src)) throw std::logic_error("launch_cgs_update_norm: fused Givens setup");
-    auto fn = ng ? (fr ? k_cgs_update_norm_lat<true, true> : k_cgs_update_norm_lat<false, true>)
-                 : (fr ? k_cgs_update_norm_lat<true> : k_cgs_update_norm_lat<false>);
-    const CgsGivens z{};
-    const CgsGivens& q = ng ? *ng : z;
-    hipLaunchKernelGGL(fn, dim3((N + 1023) / 1024), dim3(1024), 0, s, w, basis, const_cast<float*>(binv), stride,
-                       j, H, m1, N, U, partial, fr ? *fr : RedSrc{}, q.rn, q.givens, q.g, q.resid_hist,
-                       q.host_resid, q.ticket);
+    hipLaunchKernelGGL(fr ? k_cgs_update_norm_lat<true> : k_cgs_update_norm_lat<false>, dim3((N + 1023) / 1024),
+                       dim3(1024), 0, s, w, basis, binv, stride, j, H, m1, N, U, partial, fr ? *fr : RedSrc{});
     return;
   }
-  if (ng) throw std::logic_error("launch_cgs_update_norm: fused Givens needs the latency form");
   auto fn = fr  ? (ntb ? k_cgs_update_norm<false, true, true> : k_cgs_update_norm<false, false, true>)
           : ser ? (ntb ? k_cgs_update_norm<true, true> : k_cgs_update_norm<true, false>)
                 : (ntb ? k_cgs_update_norm<false, true> : k_cgs_update_norm<false, false>);

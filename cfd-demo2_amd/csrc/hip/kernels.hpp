@@ -302,24 +302,12 @@ void launch_cgs_dots(const float* w, const float* basis, const float* binv, size
 // H[j][ii] = total of vector ii of r (r.nvec = j + 1)
 void launch_cgs_reduce(const RedSrc& r, int j, float* H, int m1, hipStream_t s);
 // W_{j+1} = w - sum_i H[i,j] V_i  (written into basis slot j+1) + ||W_{j+1}||^2 unit partials
-// ng != null (latency form only): the block finishing last also runs
-// k_norm_givens's work (launch_norm_givens is then not called); ticket: a
-// zeroed device counter the kernel leaves zeroed
-struct CgsGivens {
-  RedSrc rn;  // the norm's unit partials (partial of the same launch)
-  float* givens = nullptr;
-  float* g = nullptr;
-  float* resid_hist = nullptr;
-  float* host_resid = nullptr;
-  uint32_t* ticket = nullptr;
-};
 // fr != null: the CGS totals (H column j) reduced inside the update from the
 // dots' unit partials (k_cgs_reduce not launched); only where
 // cgs_reduce_fusable(*fr) holds -- one GPU, at most 256 padded units
 void launch_cgs_update_norm(const float* w, float* basis, const float* binv, size_t stride, int j, float* H,
                             int m1, uint32_t N, uint32_t U, float* partial, hipStream_t s, bool rev = false,
-                            bool ntb = true, const RedSrc* fr = nullptr, bool lat = false,
-                            const CgsGivens* ng = nullptr);
+                            bool ntb = true, const RedSrc* fr = nullptr, bool lat = false);
 // small meshes (<= CFD_CGS_LAT_MAX_CELLS): the CGS dots / update in their
 // latency form (several basis vectors per load round trip; same bits)
 bool cgs_latency_form(uint32_t N);

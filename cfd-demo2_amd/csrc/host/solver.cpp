@@ -97,7 +97,6 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   if (const char* cu = std::getenv("CFD_CGS_UPDATE_NT")) cgs_update_nt = cu[0] == '1';
   if (const char* cf = std::getenv("CFD_CGS_FUSE_REDUCE")) cgs_fuse_reduce = cf[0] != '0';
   if (const char* cl = std::getenv("CFD_CGS_LAT")) cgs_lat = cl[0] != '0';
-  if (const char* cg = std::getenv("CFD_CGS_FUSE_GIVENS")) cgs_fuse_givens = cg[0] != '0';
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   amg_local = dist() && cfg.amg_local_aggregation != 0;
   {
@@ -583,8 +582,6 @@ void Solver::ensure_fgmres() {  // coupled_solver_fgmres.rs:212-1280 (lazy)
   p_sol = valloc<float>(1);
   partial = arena.alloc<float>((size_t)m1 * pstride);
   partial_n = arena.alloc<float>(pstride);
-  d_ticket = arena.alloc<uint32_t>(1);  // the fused Givens step's counter (left zeroed by every launch)
-  CFD_HIP(hipMemsetAsync(d_ticket, 0, sizeof(uint32_t), stream));
   const size_t nsc = kHOff + (size_t)m1 * m + 2 * (size_t)m + m1 + m + m + m1;
   dsc = arena.alloc<float>(nsc);
   CFD_HIP(hipMemsetAsync(dsc, 0, nsc * sizeof(float), stream));
@@ -1574,20 +1571,9 @@ void Solver::iteration(int j, float* pin) {
   // on C1's first iterations alone (the j + 2 vectors fitting) it lost
   // ≈ 0.1-0.2 ms/step, hence the whole-basis test (profiles/r05/ab_log.md).
   const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
-  // small meshes: the update's last block also runs the norm + Givens step
-  const bool fuse_givens = lat && cgs_fuse_givens && !dist();
-  CgsGivens ng;
-  if (fuse_givens) {
-    ng.rn = combine(partial_n, 1);
-    ng.givens = givens;
-    ng.g = g;
-    ng.resid_hist = resid_hist;
-    ng.host_resid = pin;
-    ng.ticket = d_ticket;
-  }
   launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0,
-                         !basis_kept, fuse_reduce ? &dots : nullptr, lat, fuse_givens ? &ng : nullptr);
-  if (!fuse_givens) launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
+                         !basis_kept, fuse_reduce ? &dots : nullptr, lat);
+  launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
   check_launch("FGMRES iteration (Schur preconditioner, V-cycle, SpMV, CGS)");
 }
 

@@ -352,10 +352,6 @@ struct Solver {
   // small meshes: the CGS dots / update in their latency form (several basis
   // vectors per load round trip; CFD_CGS_LAT=0: the streaming form)
   bool cgs_lat = true;
-  // latency form: the update's last block also runs the norm + Givens step
-  // (CFD_CGS_FUSE_GIVENS=0: k_norm_givens launched); d_ticket: its counter
-  bool cgs_fuse_givens = true;
-  uint32_t* d_ticket = nullptr;
   int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
   uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
   bool fused_prolong(int li) const {

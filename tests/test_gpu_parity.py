@@ -510,7 +510,6 @@ VARIANTS = [
     {"CFD_CGS_FUSE_REDUCE": "0"},     # k_cgs_reduce launched (production: meshes past 256 reduction units)
     {"CFD_CGS_UPDATE_NT": "1"},       # nontemporal CGS update although the basis is cache-kept
     {"CFD_CGS_LAT": "0"},             # CGS dots / update in the streaming form (production: > 131 k cells)
-    {"CFD_CGS_FUSE_GIVENS": "0"},     # k_norm_givens launched after the latency-form update
     {"CFD_AMG_FUSED_RR": "0"},        # separate residual + restriction kernels on every level
     {"CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused residual-restriction on every level, predicated loads
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
