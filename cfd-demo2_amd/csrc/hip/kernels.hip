@@ -1728,6 +1728,9 @@ __global__ void __launch_bounds__(256) k_solve_triangular(const float* H, const 
     for (int li = 0; li < k; ++li) {
       const int i = k - 1 - li;
       float sum = gs[i];
+      // unrolled: the LDS loads of 8 terms issue together, only the
+      // subtractions form the chain (same operations, same order)
+#pragma unroll 8
       for (int jj = i + 1; jj < k; ++jj) sum -= hs[jj * m1 + i] * ys[jj];
       const float diag = hs[i * m1 + i];
       ys[i] = (fabsf(diag) > 1e-12f) ? sum / diag : 0.0f;
