@@ -31,15 +31,6 @@ namespace {
 // loads win (same-box A/B at C2: update 346 -> 295, dots 294 -> 281 us); with
 // ~4 blocks per CU nothing hides a wavefront's one-at-a-time loads (C1: dots
 // 41.8 -> 31.0, update 40.5 -> 36.2 us unserialised; profiles/r03/ab_log.md).
-// basis vectors per iteration of the streaming CGS loops (loads of the next
-// vector may issue before the current one's arithmetic; SER still waits
-// after every load) -- A/B knob
-#ifdef CFD_CGS_UNROLL
-#define CFD_STR2(x) #x
-#define CFD_CGS_UNROLL_HINT _Pragma(CFD_STR2(unroll CFD_CGS_UNROLL))
-#else
-#define CFD_CGS_UNROLL_HINT
-#endif
 #ifndef CFD_CGS_SER_MIN_CELLS
 #define CFD_CGS_SER_MIN_CELLS (1u << 22)
 #endif
@@ -1075,31 +1066,6 @@ __device__ __forceinline__ void cgs_dots_cells(const float* __restrict__ w, cons
                                                float* ql) {
   float wv[4][3];
   load_cells3<FULL>(w, N, wv);
-#ifdef CFD_CGS_UNROLL
-  if constexpr (!SER) {  // A/B: CFD_CGS_UNROLL vectors' loads issued together (the trees hold convergent ops)
-    constexpr int B = CFD_CGS_UNROLL;
-    for (int ii0 = 0; ii0 <= j; ii0 += B) {
-      float v[B][4][3];
-#pragma unroll
-      for (int k = 0; k < B; ++k) load_cells3<FULL, NTB, false>(basis + (size_t)min(ii0 + k, j) * stride, N, v[k]);
-#pragma unroll
-      for (int k = 0; k < B; ++k) {
-        if (ii0 + k <= j) {
-          const float sc = binv[ii0 + k];
-          float t[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-#pragma unroll
-            for (int e = 0; e < 3; ++e) v[k][q][e] = sc * v[k][q][e];
-            t[q] = cell_dot3(wv[q], v[k][q]);
-          }
-          quarter_trees(t, ql + 16 * (ii0 + k));
-        }
-      }
-    }
-    return;
-  }
-#endif
   for (int ii = 0; ii <= j; ++ii) {
     const float sc = binv[ii];
     float v[4][3], t[4];
@@ -1212,7 +1178,6 @@ __device__ __forceinline__ void cgs_update_cells(const float* __restrict__ w, fl
                                                  const float* hcol, const float* scol, uint32_t N, float t[4],
                                                  uint32_t b) {
   float corr[4][3] = {};
-  CFD_CGS_UNROLL_HINT
   for (int ii = 0; ii <= j; ++ii) {
     const float h = hcol[ii], sc = scol[ii];
     float v[4][3];
