@@ -1450,9 +1450,6 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 // sigma bit for bit -- the f32 result of k_relax_pressure, without a compare
 // and select per entry.
 constexpr int kRelaxThreads = 1024;
-#ifndef CFD_RELAX_DPP
-#define CFD_RELAX_DPP 1  // 0: no DPP neighbour path, unpacked addresses (the round-4 kernel; A/B)
-#endif
 template <int RPT, int OD>
 __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t N, uint32_t ld,
                                                                       const int32_t* __restrict__ col,
@@ -1470,25 +1467,16 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
   // a sweep's mix operand (the destination's previous value, written by this
   // thread two sweeps earlier) is read from them, not from LDS
   float own[2][RPT];
-  // LDS byte addresses of the entries' columns; OD = 4 (8 rows per thread):
-  // two 16-bit halves per register (every address < 64 KiB), fewer spills
-  constexpr bool PACK = OD == 4 && CFD_RELAX_DPP;
-  constexpr int OP = PACK ? (OD + 1) / 2 : OD;
-  uint32_t adp[RPT][OP];
-  auto ad = [&](int k, int e) -> uint32_t {
-    if constexpr (PACK)
-      return (e & 1) ? adp[k][e >> 1] >> 16 : adp[k][e >> 1] & 0xFFFFu;
-    else
-      return adp[k][e];
-  };
+  uint32_t ad[RPT][OD];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const uint32_t i = t + (uint32_t)k * kRelaxThreads;
     dv[k] = tp[k] = own[0][k] = own[1][k] = 0.0f;
 #pragma unroll
-    for (int e = 0; e < OD; ++e) v[k][e] = 0.0f;
-#pragma unroll
-    for (int e = 0; e < OP; ++e) adp[k][e] = PACK ? (4u * N) | ((4u * N) << 16) : 4u * N;  // the zero row
+    for (int e = 0; e < OD; ++e) {
+      v[k][e] = 0.0f;
+      ad[k][e] = 4u * N;  // the zero row
+    }
     if (i < N) {
       own[0][k] = relax_lds[i] = p_sol[i];
       own[1][k] = relax_lds[kT / 4 + i] = temp[i];
@@ -1507,11 +1495,7 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
             for (int q = 0; q < OD; ++q)
               if (q == e) {
                 v[k][q] = sval[slot];
-                const uint32_t a = 4u * (uint32_t)cc;
-                if constexpr (PACK)
-                  adp[k][q >> 1] = (q & 1) ? (adp[k][q >> 1] & 0xFFFFu) | (a << 16) : (adp[k][q >> 1] & 0xFFFF0000u) | a;
-                else
-                  adp[k][q] = a;
+                ad[k][q] = 4u * (uint32_t)cc;
               }
             ++e;
           }
@@ -1520,22 +1504,6 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
     }
   }
   if (t == 0) relax_lds[N] = relax_lds[kT / 4 + N] = 0.0f;
-  // Regular row groups (OD = 4, quad meshes, round 5): where all 64 rows of a
-  // wavefront's group k have their second and third off-diagonal entries at
-  // columns i - 1 and i + 1 -- lanes l - 1 and l + 1 of the same wavefront --
-  // those two neighbour values come from the lanes' own registers by DPP
-  // wavefront shifts (the wavefront's edge lanes by one broadcast LDS read
-  // each) instead of two LDS gathers per row: the same values, summed in the
-  // same slot order.  Bit k of regk: group k regular.
-  [[maybe_unused]] uint32_t regk = 0;
-  if constexpr (PACK) {
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const uint32_t i = t + (uint32_t)k * kRelaxThreads;
-      const bool reg = i < N && i > 0 && ad(k, 1) == 4u * (i - 1) && ad(k, 2) == 4u * (i + 1);
-      if (__all(reg)) regk |= 1u << k;
-    }
-  }
   __syncthreads();
   // SRC = byte offset of the source iterate (0: P, kT: T)
   auto sweep = [&](auto src_off) {
@@ -1547,29 +1515,8 @@ __global__ void __launch_bounds__(kRelaxThreads) k_relax_pressure_fused(uint32_t
       // they write mix(+0, +0, 1.2) = +0 back into it (branch-free sweep)
       const uint32_t i = min(t + (uint32_t)k * kRelaxThreads, N);
       float sigma = 0.0f;
-      if constexpr (PACK) {
-        if (regk & (1u << k)) {
-          const float xs = own[1 - DI][k];  // this row's value in the source iterate
-          float xl = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xs), 0x138, 0xF, 0xF, false));
-          float xr = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(xs), 0x130, 0xF, 0xF, false));
-          const uint32_t i0 = (t & ~63u) + (uint32_t)k * kRelaxThreads;  // the wavefront's first row (> 0)
-          const float bl = *reinterpret_cast<const float*>(base + 4u * (i0 - 1u) + SRC);
-          const float br = *reinterpret_cast<const float*>(base + 4u * (i0 + 64u) + SRC);
-          const uint32_t lane = red_lane();
-          xl = lane == 0 ? bl : xl;
-          xr = lane == 63 ? br : xr;
-          sigma += v[k][0] * *reinterpret_cast<const float*>(base + ad(k, 0) + SRC);
-          sigma += v[k][1] * xl;
-          sigma += v[k][2] * xr;
-          sigma += v[k][3] * *reinterpret_cast<const float*>(base + ad(k, 3) + SRC);
-          const float hat_x = dv[k] * (tp[k] - sigma);
-          own[DI][k] = wmix(own[DI][k], hat_x, 1.2f);
-          *reinterpret_cast<float*>(base + 4u * i + DST) = own[DI][k];
-          continue;
-        }
-      }
 #pragma unroll
-      for (int e = 0; e < OD; ++e) sigma += v[k][e] * *reinterpret_cast<const float*>(base + ad(k, e) + SRC);
+      for (int e = 0; e < OD; ++e) sigma += v[k][e] * *reinterpret_cast<const float*>(base + ad[k][e] + SRC);
       const float hat_x = dv[k] * (tp[k] - sigma);
       // own row: only this thread touches it in this sweep
       own[DI][k] = wmix(own[DI][k], hat_x, 1.2f);
