@@ -2829,7 +2829,7 @@ bool launch_relax_pressure_fused(uint32_t N, uint32_t ld, uint32_t ws, const int
                        p_sol, temp, iters);                                                                   \
     return true;                                                                                              \
   }
-  CFD_RELAX_FUSED_CASE(1, 15)  // register budget at 1024 threads: 128 VGPRs, no spills
+  CFD_RELAX_FUSED_CASE(1, 15)  // register budget at 1024 threads: 128 VGPRs (the 8 x 4 case spills 16)
   CFD_RELAX_FUSED_CASE(2, 15)
   CFD_RELAX_FUSED_CASE(4, 9)
   CFD_RELAX_FUSED_CASE(8, 4)
