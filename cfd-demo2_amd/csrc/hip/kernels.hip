@@ -1792,6 +1792,41 @@ __global__ void __launch_bounds__(kBlock) k_update_x(float* x, const float* __re
   }
 }
 
+// Latency form (small meshes, as the CGS passes': k_cgs_dots_lat): 16 of the
+// Z vectors' loads issued per round trip instead of 2, the updates applied in
+// ascending i as above -- same operations.
+__global__ void __launch_bounds__(kBlock) k_update_x_lat(float* x, const float* __restrict__ z, size_t stride,
+                                                         const float* __restrict__ y, int k, size_t n) {
+  constexpr int KB = 16;
+  const size_t e = 4 * ((size_t)blockIdx.x * kBlock + threadIdx.x);
+  if (e >= n) return;
+  if (e + 3 < n) {
+    float4 xv = *reinterpret_cast<const float4*>(x + e);
+    for (int ii0 = 0; ii0 < k; ii0 += KB) {
+      float4 zb[KB];
+#pragma unroll
+      for (int q = 0; q < KB; ++q) zb[q] = *reinterpret_cast<const float4*>(z + (size_t)min(ii0 + q, k - 1) * stride + e);
+#pragma unroll
+      for (int q = 0; q < KB; ++q) {
+        if (ii0 + q < k) {
+          const float yq = y[ii0 + q];
+          xv.x = yq * zb[q].x + xv.x;
+          xv.y = yq * zb[q].y + xv.y;
+          xv.z = yq * zb[q].z + xv.z;
+          xv.w = yq * zb[q].w + xv.w;
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(x + e) = xv;
+    return;
+  }
+  for (size_t f = e; f < n; ++f) {
+    float xv = x[f];
+    for (int ii = 0; ii < k; ++ii) xv = y[ii] * z[(size_t)ii * stride + f] + xv;
+    x[f] = xv;
+  }
+}
+
 // ------------------------------- AMG ---------------------------------------
 // Each thread owns 4 consecutive rows: b, x, de and every ELL slot are one
 // 16-byte load per thread (coalesced 1 KiB per wavefront), column deltas are
@@ -2852,6 +2887,10 @@ void launch_solve_triangular(const float* H, const float* g, float* y, int k, in
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
                      hipStream_t s) {
   if (!n) return;
+  if (n / 3 <= CFD_CGS_LAT_MAX_CELLS && k > 2) {
+    hipLaunchKernelGGL(k_update_x_lat, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
+    return;
+  }
   if (n / 3 >= CFD_CGS_SER_MIN_CELLS)
     hipLaunchKernelGGL(k_update_x<true>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
   else
