@@ -1379,18 +1379,12 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int 
   const float norm = sqrtf(s);
   hc[j + 1] = norm;
   binv[j + 1] = norm > 1e-20f ? 1.0f / norm : 0.0f;
-  // the rotated entry ii + 1 is the next rotation's h_ij: carried in a
-  // register, so the chain is the arithmetic only (the unrolled loads of
-  // h_(i+1)j and the rotations do not depend on it); the same operations
-  float carry = hc[0];
-#pragma unroll 4
   for (int ii = 0; ii < j; ++ii) {
-    const float hij = carry, hi1j = hc[ii + 1];
+    const float hij = hc[ii], hi1j = hc[ii + 1];
     const float cc = gv[2 * ii], ss = gv[2 * ii + 1];
     hc[ii] = cc * hij + ss * hi1j;
-    carry = -ss * hij + cc * hi1j;
+    hc[ii + 1] = -ss * hij + cc * hi1j;
   }
-  hc[j] = carry;
   const float hjj = hc[j], hj1j = hc[j + 1];
   float cc = 1.0f, ss = 0.0f;
   const float rho = sqrtf(hjj * hjj + hj1j * hj1j);
