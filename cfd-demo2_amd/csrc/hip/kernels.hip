@@ -2001,14 +2001,38 @@ __device__ __forceinline__ float4 smooth4(const AmgLevelDev& L, const float* __r
   o.w = wmix(xx.w, (bb.w - sg[3]) / dd.w, 0.8f);
   return o;
 }
+// The level's fields the sweep needs first (row lengths, slot values and
+// columns, the row ranges, ELL stride and width) and x, b lead the argument
+// list: those 16 dwords arrive preloaded in SGPRs (kernarg preload, §4), so
+// the first loads wait for no kernarg round trip; the rest of the level
+// image comes with L.
 template <bool D16, int MODE, bool PRO = false, bool NT = false>
-__global__ void __launch_bounds__(kBlock) k_amg_smooth(AmgLevelDev L, const float* __restrict__ x,
+__global__ void __launch_bounds__(kBlock) k_amg_smooth(const uint8_t* len, const float* val, const void* col,
+                                                       uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3,
+                                                       uint32_t stride, int w, const float* __restrict__ x,
                                                        const float* __restrict__ b, float* __restrict__ x_out,
-                                                       const float* __restrict__ xc) {
+                                                       AmgLevelDev L, const float* __restrict__ xc) {
   uint32_t i0;
-  if (!row_range<kRevSmooth>(L.r0, L.r1, L.r2, L.r3, i0)) return;
-  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(L, x, b, i0, xc);
+  if (!row_range<kRevSmooth>(r0, r1, r2, r3, i0)) return;
+  AmgLevelDev Lk = L;
+  Lk.len = len;
+  Lk.val = val;
+  if constexpr (D16)
+    Lk.col16 = static_cast<const int16_t*>(col);
+  else
+    Lk.col32 = static_cast<const int32_t*>(col);
+  Lk.r0 = r0;
+  Lk.r1 = r1;
+  Lk.r2 = r2;
+  Lk.r3 = r3;
+  Lk.stride = stride;
+  Lk.w = w;
+  *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(Lk, x, b, i0, xc);
 }
+// the leading arguments of k_amg_smooth from a level image
+#define CFD_AMG_HEAD(L) \
+  (L).len, (L).val, ((L).use16 ? (const void*)(L).col16 : (const void*)(L).col32), (L).r0, (L).r1, (L).r2, (L).r3, \
+      (L).stride, (L).w
 
 // smooth_op on a level whose x is identically +0 (every coarse level's
 // pre-smoother: restrict just cleared it): sigma = +0, so the sweep is the
@@ -2907,9 +2931,10 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
   auto fn = nt ? CFD_AMG_INSTANCE(k_amg_smooth, L, false, true) : CFD_AMG_INSTANCE(k_amg_smooth, L, false, false);
   if (ev0)  // timed launch: events recorded by the GPU at kernel start / end
-    hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, L, x, b, x_out, nullptr);
+    hipExtLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, ev0, ev1, 0, CFD_AMG_HEAD(L), x, b, x_out, L,
+                          (const float*)nullptr);
   else
-    hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, nullptr);
+    hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, CFD_AMG_HEAD(L), x, b, x_out, L, (const float*)nullptr);
 }
 void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b, float* x_out,
                                hipStream_t s) {
@@ -2918,7 +2943,7 @@ void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float
   const unsigned nb = rows2_grid(L.r0, L.r1, L.r2, L.r3);
   auto fn = L.use16 ? (L.full ? k_amg_smooth<true, 1, true> : k_amg_smooth<true, 0, true>)
                     : (L.full ? k_amg_smooth<false, 1, true> : k_amg_smooth<false, 0, true>);
-  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, L, x, b, x_out, xc);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, CFD_AMG_HEAD(L), x, b, x_out, L, xc);
 }
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s) {
   if (L.n) hipLaunchKernelGGL(k_amg_smooth_zero, dim3(grid_for((L.n + 3) / 4)), dim3(kBlock), 0, s, L, b, x_out);
