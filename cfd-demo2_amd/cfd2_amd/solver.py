@@ -46,6 +46,7 @@ def _bind():
     for n in ("cfd_update_constants", "cfd_initialize_history", "cfd_step", "cfd_synchronize"):
         getattr(L, n).argtypes = [_vp]
     L.cfd_get_step_info.argtypes = [_vp, C.POINTER(_ffi.StepInfo)]
+    L.cfd_set_stop_state.argtypes = [_vp, C.c_int32, C.c_uint32, C.c_uint32]
     L.cfd_num_cells.argtypes = [_vp]
     L.cfd_num_cells.restype = C.c_uint32
     L.cfd_num_faces.argtypes = [_vp]
@@ -272,12 +273,31 @@ class GpuSolver:
         self._call("cfd_get_step_info", C.byref(i))
         return i
 
+    # should_stop / degenerate_count / steady_state_count are plain public
+    # fields in the reference (structs.rs:244-247): the GUI clears should_stop
+    # before it resumes stepping (src/ui/app.rs:852-857)
+    def set_stop_state(self, should_stop, degenerate_count, steady_state_count):
+        self._call("cfd_set_stop_state", 1 if should_stop else 0, int(degenerate_count), int(steady_state_count))
+
+    def _set_stop_field(self, **kw):
+        i = self.step_info()
+        cur = dict(should_stop=i.should_stop, degenerate_count=i.degenerate_count,
+                   steady_state_count=i.steady_state_count)
+        cur.update(kw)
+        self.set_stop_state(**cur)
+
     @property
     def should_stop(self) -> bool: return bool(self.step_info().should_stop)
+    @should_stop.setter
+    def should_stop(self, v): self._set_stop_field(should_stop=bool(v))
     @property
     def degenerate_count(self) -> int: return int(self.step_info().degenerate_count)
+    @degenerate_count.setter
+    def degenerate_count(self, v): self._set_stop_field(degenerate_count=int(v))
     @property
     def steady_state_count(self) -> int: return int(self.step_info().steady_state_count)
+    @steady_state_count.setter
+    def steady_state_count(self, v): self._set_stop_field(steady_state_count=int(v))
     @property
     def outer_iterations(self) -> int: return int(self.step_info().outer_iterations)
 
@@ -471,8 +491,14 @@ class GpuGroup:
 
     @property
     def should_stop(self): return self.ranks[0].should_stop
+    @should_stop.setter
+    def should_stop(self, v):
+        for r in self.ranks:
+            r.should_stop = v
     @property
     def degenerate_count(self): return self.ranks[0].degenerate_count
+    @property
+    def steady_state_count(self): return self.ranks[0].steady_state_count
 
 
 def dist_plan(mesh, nranks: int, rank: int) -> dict:

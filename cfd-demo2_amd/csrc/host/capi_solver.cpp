@@ -178,6 +178,17 @@ cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out) {
   *out = s->s->info;
   return CFD_OK;
 }
+// The reference's stop state is three plain public fields (structs.rs:244-247)
+// that callers write between steps (the GUI clears should_stop before it
+// resumes, src/ui/app.rs:852-857); check_evolution reads and updates them.
+cfd_status cfd_set_stop_state(cfd_solver* s, int32_t should_stop, uint32_t degenerate_count,
+                              uint32_t steady_state_count) {
+  CHECK_S(s);
+  s->s->info.should_stop = should_stop ? 1 : 0;
+  s->s->info.degenerate_count = degenerate_count;
+  s->s->info.steady_state_count = steady_state_count;
+  return CFD_OK;
+}
 cfd_status cfd_state_save(cfd_solver* s, const char* path) {
   CHECK_S(s);
   if (!path) return set_error(CFD_ERR_INVALID, "null path");

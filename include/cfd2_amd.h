@@ -213,6 +213,14 @@ cfd_status cfd_get_u(cfd_solver* s, double* uv /* [2N] */);
 cfd_status cfd_get_p(cfd_solver* s, double* p /* [N] */);
 cfd_status cfd_get_d_p(cfd_solver* s, double* dp /* [N] */);
 cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out);
+/* The caller-writable part of the step info: the reference's public fields
+ * should_stop / degenerate_count / steady_state_count (structs.rs:244-247),
+ * which the GUI writes between steps (src/ui/app.rs:852-857: should_stop =
+ * false before it resumes) and check_evolution then reads and updates
+ * (coupled_solver.rs:553-578).  Distributed solver: call it on every rank
+ * with the same values (the counters are global).                          */
+cfd_status cfd_set_stop_state(cfd_solver* s, int32_t should_stop, uint32_t degenerate_count,
+                              uint32_t steady_state_count);
 uint32_t cfd_num_cells(const cfd_solver* s);
 uint32_t cfd_num_faces(const cfd_solver* s);
 

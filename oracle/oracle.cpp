@@ -1666,6 +1666,15 @@ int oracle_get_step_info(const oracle_solver* s, cfd_step_info* out) {
   *out = s->info;
   return 0;
 }
+// public fields should_stop / degenerate_count / steady_state_count
+// (structs.rs:244-247), written by callers between steps (src/ui/app.rs:856)
+int oracle_set_stop_state(oracle_solver* s, int should_stop, uint32_t degenerate_count,
+                          uint32_t steady_state_count) {
+  s->info.should_stop = should_stop ? 1 : 0;
+  s->info.degenerate_count = degenerate_count;
+  s->info.steady_state_count = steady_state_count;
+  return 0;
+}
 
 size_t oracle_debug_buffer_len(const oracle_solver* s, int id) {
   const size_t N = s->N;

@@ -54,6 +54,21 @@ int main(int argc, char** argv) {
     fprintf(stderr, "stats_p.time_s not filled: %g\n", info.stats_p.time_s);
     return 1;
   }
+  /* the public stop fields are caller-writable (structs.rs:244-247; the GUI
+   * clears should_stop before it resumes, src/ui/app.rs:852-857) */
+  CHECK(cfd_set_stop_state(s, 1, 0, 7));
+  CHECK(cfd_get_step_info(s, &info));
+  if (info.should_stop != 1 || info.degenerate_count != 0 || info.steady_state_count != 7) {
+    fprintf(stderr, "cfd_set_stop_state not applied\n");
+    return 1;
+  }
+  CHECK(cfd_set_stop_state(s, 0, 0, 0));
+  CHECK(cfd_step(s));
+  CHECK(cfd_get_step_info(s, &info));
+  if (info.should_stop != 0) { /* the flow still evolves: no stop */
+    fprintf(stderr, "should_stop set again on an evolving flow\n");
+    return 1;
+  }
   CHECK(cfd_state_save(s, state_path));
   /* a bad call reports a status and a message instead of aborting */
   if (cfd_set_u(NULL, uv) != CFD_ERR_INVALID || cfd_last_error()[0] == '\0') {

@@ -43,6 +43,7 @@ def olib():
         L.oracle_initialize_history.argtypes = [vp]
         L.oracle_step.argtypes = [vp]
         L.oracle_get_step_info.argtypes = [vp, C.POINTER(_ffi.StepInfo)]
+        L.oracle_set_stop_state.argtypes = [vp, C.c_int, C.c_uint32, C.c_uint32]
         L.oracle_debug_buffer_len.argtypes = [vp, C.c_int]
         L.oracle_debug_buffer_len.restype = C.c_size_t
         L.oracle_debug_buffer.argtypes = [vp, C.c_int, C.POINTER(C.c_float), C.c_size_t]
@@ -161,10 +162,29 @@ class OracleSolver:
         olib().oracle_get_step_info(self._h, C.byref(i))
         return i
 
+    def set_stop_state(self, should_stop, degenerate_count, steady_state_count):
+        _ck(olib().oracle_set_stop_state(self._h, int(bool(should_stop)), int(degenerate_count),
+                                         int(steady_state_count)), "set_stop_state")
+
+    def _set_stop_field(self, **kw):
+        i = self.step_info()
+        cur = dict(should_stop=i.should_stop, degenerate_count=i.degenerate_count,
+                   steady_state_count=i.steady_state_count)
+        cur.update(kw)
+        self.set_stop_state(**cur)
+
     @property
     def should_stop(self): return bool(self.step_info().should_stop)
+    @should_stop.setter
+    def should_stop(self, v): self._set_stop_field(should_stop=bool(v))
     @property
     def degenerate_count(self): return int(self.step_info().degenerate_count)
+    @degenerate_count.setter
+    def degenerate_count(self, v): self._set_stop_field(degenerate_count=int(v))
+    @property
+    def steady_state_count(self): return int(self.step_info().steady_state_count)
+    @steady_state_count.setter
+    def steady_state_count(self, v): self._set_stop_field(steady_state_count=int(v))
 
     def debug_buffer(self, bid: int) -> np.ndarray:
         n = olib().oracle_debug_buffer_len(self._h, bid)
