@@ -10,7 +10,11 @@ the deterministic cut-cell mesh of ChannelWithObstacle{3x1, (1.0,0.51), r 0.1}
 (h=5.449e-4 -> ~10M cells per GPU), smoothed (0.3, 100); initial u = p = 0.
 
 Launch: ``python bench.py`` (N=1) or, for N GPUs, under torch.distributed.run
-with one process per GPU; rank 0 prints ONE JSON line.  N > 1 is weak
+with one process per GPU; rank 0 prints ONE JSON line.  ``python bench.py
+--gpus N`` started WITHOUT a launcher (no WORLD_SIZE in the env) starts
+torch.distributed.run itself, as a child process, before anything touches
+the GPU, and exits with its status; under a launcher --gpus must equal
+WORLD_SIZE (else exit 2).  N > 1 is weak
 scaling (BASELINE configs[3..4]): the mesh is refined to
 ~10M x N cells (h / sqrt(N)), every rank owns one vertical slab of ~10M
 cells, halos and reductions go over RCCL (xGMI); torch.distributed (gloo)
@@ -285,6 +289,42 @@ def comm_timing_summary(t):
                     "wait = compute-stream stall, comm = transport time (RCCL: includes peer skew)"}
 
 
+def rank_launch_cmd(n, argv, port):
+    """torch.distributed.run command that runs this script as n local ranks
+    (the driver's own launch line, 127.0.0.1 rendezvous)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n, argv):
+    """--gpus N > 1 without a launcher: run the N ranks through
+    torch.distributed.run in a CHILD process and return its exit status.  This
+    process never touches the GPU (no torch import, no HIP call) and never
+    re-execs; the ranks' stdout is this process's stdout, so rank 0's JSON line
+    is the one line printed."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = rank_launch_cmd(n, argv, port)
+    log(f"bench.py: --gpus {n} without a launcher: starting {n} ranks via torch.distributed.run (port {port})")
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+def check_world(gpus, env):
+    """(world size, error message or None): --gpus against the launcher's WORLD_SIZE."""
+    ws = env.get("WORLD_SIZE")
+    world = int(ws) if ws else 1
+    if gpus < 1:
+        return world, f"--gpus must be >= 1 (got {gpus})"
+    if ws and gpus != world:
+        return world, (f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks: "
+                       f"run with --gpus {world}, or start bench.py --gpus {gpus} without a launcher")
+    return world, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -310,7 +350,12 @@ def main():
                     help="binary mesh file: loaded if present, else generated and saved (A/B runs)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and not os.environ.get("WORLD_SIZE"):
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, err = check_world(args.gpus, os.environ)
+    if err:
+        log("bench.py:", err)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

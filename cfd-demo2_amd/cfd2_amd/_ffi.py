@@ -74,6 +74,7 @@ class Config(C.Structure):
         ("log_level", C.c_int32),
         ("amg_rebuild_interval", C.c_int32),
         ("amg_local_aggregation", C.c_int32),
+        ("comm_timeout_s", C.c_float),
     ]
 
 
@@ -166,6 +167,7 @@ def default_config(**overrides) -> Config:
         log_level=0,
         amg_rebuild_interval=0,
         amg_local_aggregation=0,
+        comm_timeout_s=180.0,
     )
     for k, v in overrides.items():
         setattr(cfg, k, v)
@@ -188,7 +190,7 @@ EXPORTED = [
     "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_amg_info",
     "cfd_dist_unique_id", "cfd_solver_create_dist", "cfd_solver_create_dist_host", "cfd_group_create",
     "cfd_group_step",
-    "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest", "cfd_dist_comm_stats",
+    "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest", "cfd_debug_comm_watchdog", "cfd_dist_comm_stats",
     "cfd_debug_group_fault", "cfd_debug_group_fault_midstep", "cfd_group_reset", "cfd_group_needs_restore",
     "cfd_comm_timing_enable", "cfd_comm_timing",
 ]

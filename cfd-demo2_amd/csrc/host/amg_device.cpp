@@ -293,6 +293,7 @@ std::vector<std::vector<uint32_t>> Solver::allgatherv_u32(const std::vector<uint
 // rank together (collective decisions) when the host path must build the
 // hierarchy: a Galerkin capacity overflow or rows wider than the u8 layout.
 bool Solver::build_amg_device_dist() {
+  comm->label = -1;  // setup collectives (watchdog reports)
   const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
@@ -861,6 +862,7 @@ void Solver::member_values(const AmgRefreshLevel& F) {
 // distributed level re-runs its member-value gathers and exchange first, and
 // the last one re-gathers the replicated level's values.
 void Solver::refresh_amg() {
+  if (comm) comm->label = -1;
   const size_t slots_s = (size_t)topo.ws * topo.ld;
   CFD_HIP(hipMemcpyAsync(amg_src, sval, slots_s * sizeof(float), hipMemcpyDeviceToDevice, stream));
   for (size_t li = 0; li < amg_refresh.size(); ++li) {

@@ -70,6 +70,7 @@ void cfd_config_default(cfd_config* c) {
   c->log_level = 0;
   c->amg_rebuild_interval = 0;
   c->amg_local_aggregation = 0;
+  c->comm_timeout_s = 180.0f;
 }
 
 cfd_status cfd_solver_create(const cfd_mesh_view* mesh, const cfd_config* cfg, int32_t hip_device,
@@ -313,7 +314,7 @@ cfd_status cfd_solver_create_dist(const cfd_mesh_view* mesh, const cfd_config* c
   cfd2::Solver* sp = nullptr;
   const cfd_status st = guard([&] {
     CFD_HIP(hipSetDevice(hip_device));
-    auto comm = cfd2::make_rccl_comm(nranks, rank, unique_id);
+    auto comm = cfd2::make_rccl_comm(nranks, rank, unique_id, hip_device, c.comm_timeout_s);
     sp = new cfd2::Solver(*mesh, c, hip_device, std::move(comm));
   });
   if (st != CFD_OK) return st;
@@ -334,7 +335,7 @@ cfd_status cfd_solver_create_dist_host(const cfd_mesh_view* mesh, const cfd_conf
   cfd2::Solver* sp = nullptr;
   const cfd_status st = guard([&] {
     CFD_HIP(hipSetDevice(hip_device));
-    auto comm = cfd2::make_host_comm(nranks, rank, exchange, allgather, user);
+    auto comm = cfd2::make_host_comm(nranks, rank, exchange, allgather, user, hip_device, c.comm_timeout_s);
     sp = new cfd2::Solver(*mesh, c, hip_device, std::move(comm));
   });
   if (st != CFD_OK) return st;
@@ -463,6 +464,15 @@ cfd_status cfd_group_state_save(cfd_solver* const* h, int32_t n, const char* pat
     return set_error(CFD_ERR_INVALID, "group state save refused: the group needs restore after a failed step "
                                       "(cfd_state_load on every rank, or cfd_group_reset)");
   return group_run(h, n, [path](cfd2::Solver& s) { s.save_state(path); });
+}
+
+cfd_status cfd_debug_comm_watchdog(float timeout_s, int32_t hang_ms) {
+  return guard([&] {
+    cfd2::Watchdog wd(0, -1, timeout_s, nullptr, nullptr);
+    wd.host_begin("cfd_debug_comm_watchdog host wait", -1);
+    std::this_thread::sleep_for(std::chrono::milliseconds(hang_ms > 0 ? hang_ms : 0));
+    wd.host_end();
+  });
 }
 
 // RCCL plumbing self-test on ONE GPU (RCCL refuses two ranks per device, so

@@ -13,11 +13,16 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
+#include <string>
+#include <thread>
 #include <vector>
 
 namespace cfd2 {
@@ -42,11 +47,72 @@ struct CommStats {
   uint64_t exchanges = 0, allgathers = 0, bytes_sent = 0, bytes_gathered = 0;
 };
 
+// Progress watchdog of a transport (cfd_config.comm_timeout_s).  A stalled
+// collective otherwise hangs the process in its next stream synchronisation
+// with no diagnostic.  Every operation the transport enqueues is followed by
+// a completion event on its stream (note_stream); operations that block the
+// host (the host-staged callbacks, ncclCommInitRank) are bracketed by
+// host_begin / host_end.  A background thread polls them (and the
+// transport's asynchronous error, RCCL: ncclCommGetAsyncError) every 200 ms.
+// When an operation is older than the timeout, or an asynchronous error or
+// a failed event query appears, it prints the rank, device, operation,
+// category and age on stderr, aborts the transport (RCCL: ncclCommAbort)
+// and ends the process with status kCommWatchdogExit.  It never re-execs.
+constexpr int kCommWatchdogExit = 70;
+class Watchdog {
+ public:
+  using AsyncErr = std::function<std::string()>;  // "" while healthy
+  using Abort = std::function<void()>;
+  // timeout_s <= 0: disabled (no thread, every call a no-op)
+  Watchdog(int rank, int device, double timeout_s, AsyncErr err, Abort abort);
+  ~Watchdog();
+  Watchdog(const Watchdog&) = delete;
+  Watchdog& operator=(const Watchdog&) = delete;
+  bool enabled() const { return timeout_s_ > 0.0; }
+  void note_stream(hipStream_t s, const char* op, int label, size_t bytes);
+  void host_begin(const char* op, int label);
+  void host_end();
+  void stop();  // joins the polling thread (idempotent)
+
+ private:
+  struct Pending {
+    hipEvent_t ev;
+    const char* op;
+    int label;
+    size_t bytes;
+    uint64_t seq;
+    std::chrono::steady_clock::time_point t;
+  };
+  void loop();
+  [[noreturn]] void fire(const std::string& why, const char* op, int label, size_t bytes, uint64_t seq, double age);
+  int rank_, device_;
+  double timeout_s_;
+  AsyncErr err_;
+  Abort abort_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  std::deque<Pending> pend_;
+  std::vector<hipEvent_t> free_;
+  uint64_t seq_ = 0;
+  bool host_active_ = false;
+  const char* host_op_ = "";
+  int host_label_ = -1;
+  uint64_t host_seq_ = 0;
+  std::chrono::steady_clock::time_point host_t_;
+  std::thread th_;
+};
+// name of a Comm::label (the solver's communication categories, cfd_comm_timing)
+const char* comm_label_name(int label);
+
 class Comm {
  public:
   virtual ~Comm() = default;
   int rank = 0, size = 1;
   int kind = 0;  // cfd_comm_stats.transport
+  // category of the operations the solver issues next (Solver::CommCat; -1
+  // setup): names the stalled operation in a watchdog report
+  int label = -1;
   CommStats stats;
   // the transport's own view of the communicator (RCCL: ncclCommCount /
   // ncclCommUserRank; the others: size / rank)
@@ -80,13 +146,16 @@ class Comm {
 // ---- RCCL ----
 constexpr int kUniqueIdBytes = 128;
 void rccl_unique_id(uint8_t out[kUniqueIdBytes]);
-std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUniqueIdBytes]);
+// timeout_s: the progress watchdog's limit (<= 0 off); device: the rank's GPU
+std::unique_ptr<Comm> make_rccl_comm(int nranks, int rank, const uint8_t uid[kUniqueIdBytes], int device = 0,
+                                     double timeout_s = 0.0);
 
 // ---- host-staged callbacks (test transport, cfd_solver_create_dist_host) ----
 using HostExchangeFn = int32_t (*)(void* user, int32_t n, const int32_t* peer, void* const* send,
                                    const uint64_t* send_bytes, void* const* recv, const uint64_t* recv_bytes);
 using HostAllgatherFn = int32_t (*)(void* user, void* send, void* recv, uint64_t bytes);
-std::unique_ptr<Comm> make_host_comm(int nranks, int rank, HostExchangeFn ex, HostAllgatherFn ag, void* user);
+std::unique_ptr<Comm> make_host_comm(int nranks, int rank, HostExchangeFn ex, HostAllgatherFn ag, void* user,
+                                     int device = 0, double timeout_s = 0.0);
 
 // ---- in-process group ----
 class LocalGroup {

@@ -439,6 +439,7 @@ void Solver::halo_begin(HaloPlan& plan, std::initializer_list<HField> fields) {
   CFD_HIP(hipEventRecord(hev_pack, stream));
   CFD_HIP(hipStreamWaitEvent(cstream, hev_pack, 0));
   halo_cat = comm_cat;
+  comm->label = halo_cat;
   if (comm_prof) {
     hipEvent_t a = comm_event(), b = comm_event();
     CFD_HIP(hipEventRecord(a, cstream));
@@ -1825,6 +1826,7 @@ void Solver::check_evolution() {
       if (slo < shi) add(q, true, slo, shi);
       if (rlo < rhi) add(q, false, rlo, rhi);
     }
+    comm->label = kCommStateHalo;
     comm->exchange(msgs, stream);
     var = evrec;
     gbase = topo.c0;

@@ -637,6 +637,7 @@ struct Solver {
   // an all-gather on the compute stream, timed when comm_prof is on
   template <class F>
   void timed_gather(int cat, size_t bytes, F&& f) {
+    comm->label = cat;
     if (!comm_prof) {
       f();
       return;

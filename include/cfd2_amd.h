@@ -153,6 +153,14 @@ typedef struct cfd_config {
                                    prolongation need no halo; the hierarchy (and the
                                    bits) then depend on the rank count, and match the
                                    oracle run with the same rank count and mode       */
+  float comm_timeout_s;          /* distributed solver (RCCL and host-staged transports):
+                                   progress watchdog.  An operation of the transport still
+                                   incomplete after this many seconds, or an asynchronous
+                                   RCCL error (ncclCommGetAsyncError), makes a background
+                                   thread print the rank, device, operation and category
+                                   on stderr, abort the communicator (ncclCommAbort) and
+                                   end the process with status 70.  Default 180; <= 0 off.
+                                   No reference counterpart (the reference is one GPU).  */
 } cfd_config;
 
 void cfd_config_default(cfd_config* cfg);
@@ -371,6 +379,11 @@ int32_t cfd_group_needs_restore(cfd_solver* const* handles, int32_t nranks);
  * self and an all-gather through the solver's transport; CFD_OK if the data
  * arrived intact.                                                           */
 cfd_status cfd_debug_rccl_selftest(int32_t hip_device);
+/* Progress-watchdog self-test, no GPU needed: a watchdog with limit
+ * `timeout_s` around a host-blocking operation that takes `hang_ms`.  If
+ * hang_ms exceeds the limit, the watchdog ends the PROCESS with status 70
+ * (as on a stalled collective; run it in a child process); else CFD_OK.    */
+cfd_status cfd_debug_comm_watchdog(float timeout_s, int32_t hang_ms);
 /* Transport of a distributed handle and its traffic since the last reset
  * (bench.py prints these on a --gpus N line).                               */
 typedef struct {

@@ -23,8 +23,14 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     mesh = backwards_step()
     local = int(os.environ.get("CFD_TEST_AMG_LOCAL", "0"))  # partition-aware AMG aggregation
-    s = GpuSolver.create_dist_host(mesh, world, rank, device=0, config=default_config(amg_local_aggregation=local))
+    timeout = float(os.environ.get("CFD_TEST_COMM_TIMEOUT", "180"))  # tests/test_watchdog.py
+    s = GpuSolver.create_dist_host(mesh, world, rank, device=0,
+                                   config=default_config(amg_local_aggregation=local, comm_timeout_s=timeout))
     _setup_amg_test(s, mesh, 1)
+    if rank == int(os.environ.get("CFD_TEST_STALL_RANK", "-1")):
+        import time
+        time.sleep(60)  # a stalled peer: the other ranks' watchdogs must end the job
+        sys.exit(3)
     for _ in range(steps):
         s.step()
     if len(sys.argv) > 3:  # collective checkpoint: every process writes its rows

@@ -32,3 +32,34 @@ def test_comm_timing_summary_per_iteration_and_efficiency():
 def test_comm_timing_summary_empty_ranks():
     s = bench.comm_timing_summary({"iterations": 5, "step_ms_with_timing": 1.0, "ranks": [[], []]})
     assert s["per_iteration"] == {} and s["exposed_us_per_iteration"] == 0.0
+
+
+def test_check_world_matches_launcher():
+    assert bench.check_world(1, {}) == (1, None)
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) == (4, None)
+    w, err = bench.check_world(8, {"WORLD_SIZE": "2"})
+    assert w == 2 and "WORLD_SIZE=2" in err
+    w, err = bench.check_world(1, {"WORLD_SIZE": "2"})
+    assert err is not None
+    assert bench.check_world(0, {})[1] is not None
+
+
+def test_rank_launch_cmd_is_the_driver_launch_line():
+    cmd = bench.rank_launch_cmd(4, ["--gpus", "4", "--steps", "3"], 29511)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_bench_refuses_gpus_world_mismatch_before_gpu():
+    """Under a launcher that started 2 ranks, --gpus 3 exits 2 at once (before
+    any import of torch or the library)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "3"], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr and r.stdout == ""

@@ -36,21 +36,20 @@ def test_bench_json_contract():
 
 
 def test_bench_two_process_launch_contract():
-    """The driver's N > 1 launch (torch.distributed.run, one process per rank,
-    RANK/WORLD_SIZE from the env, 127.0.0.1 rendezvous): rank 0 alone prints
-    one JSON line whose value is the whole job's rate.  The one-GPU box has no
-    second device for RCCL, so both ranks share GPU 0 over the host-staged
-    transport; the line then says so in `parallelism`."""
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    env = dict(os.environ, CFD_DIST_TRANSPORT="host", CFD_BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+    """The N > 1 launch: ``python bench.py --gpus 2`` WITHOUT a launcher starts
+    torch.distributed.run itself (a child process, one process per rank,
+    RANK/WORLD_SIZE from the env, 127.0.0.1 rendezvous) -- the driver's own
+    launch line, bench.rank_launch_cmd; rank 0 alone prints one JSON line
+    whose value is the whole job's rate.  The one-GPU box has no second device
+    for RCCL, so both ranks share GPU 0 over the host-staged transport (DESIGN
+    §7); the line then says so in `parallelism`."""
+    env = dict(os.environ, CFD_DIST_TRANSPORT="host", CFD_BENCH_DEVICE="0")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--config", "c1", "--steps", "1", "--warmup", "1", "--outer", "1", "--inner", "4"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "without a launcher: starting 2 ranks" in r.stderr
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
