@@ -1342,7 +1342,7 @@ void Solver::v_cycle() {
       d.r1 = b;
       d.r2 = a2;
       d.r3 = b2;
-      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream, i == 0 && nt(2));
+      launch_amg_residual(d, Lv.x, Lv.b, Lv.r, stream, (i == 0 && nt(2)) || (i == 1 && nt(64)));
     };
     if (Lv.dist) {
       const CommScope cs(this, amg_cat(i));

@@ -324,7 +324,7 @@ struct Solver {
   // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
   // 1 post-smoother of the split levels, 2 level-0 AMG residual, 4 Schur
   // prediction, 8 SpMV, 16 pre-smoother, 32 the prolongation map of the split
-  // levels.  Same bits either way.  Tried and not kept:
+  // levels, 64 level-1 AMG residual.  Same bits either way.  Tried and not kept:
   // the Schur correction (its lines are the SpMV's Infinity-Cache hits),
   // prepare / assemble (assemble re-reads prepare's face slots), the
   // restriction maps.
