@@ -94,7 +94,7 @@ def cgroup_cpus():
     return None
 
 
-def cpu_baseline(mesh, n_cells, outer_fixed, inner_fixed):
+def cpu_baseline(mesh, n_cells, outer_fixed, inner_fixed, step_ref_bytes=None, step_layout_bytes=None):
     """Oracle (C++ CPU restatement, OpenMP) on a bounded sample of the workload:
     the same mesh, physics and fixed schedule; the trivial t=0 step untimed (it
     also builds the AMG hierarchy), then ONE whole step (all `outer_fixed`
@@ -129,9 +129,21 @@ def cpu_baseline(mesh, n_cells, outer_fixed, inner_fixed):
         o.step()
         runs.append((threads, time.perf_counter() - t0))
     threads, dt = min(runs, key=lambda r: r[1])
+    # BASELINE.md section 2 "Reported": the CPU's achieved GB/s from the same
+    # algorithmic byte counts as the GPU line -- the reference-format count
+    # (the oracle's own CSR layout is that format) and the GPU
+    # library's layout-true bytes -- over the oracle's step time
+    gbs = {
+        "reference_format_gbs": (step_ref_bytes / dt / 1e9) if step_ref_bytes else None,
+        "layout_true_gbs": (step_layout_bytes / dt / 1e9) if step_layout_bytes else None,
+        "step_reference_format_bytes_count": step_ref_bytes,
+        "step_layout_bytes": step_layout_bytes,
+        "seconds_per_step": dt,
+    }
     return {
         "value": n_cells / dt,
         "unit": "cell-updates/sec",
+        "gbs": gbs,
         "cores": threads,
         "kind": "port",
         "host_cpus": total,
@@ -689,7 +701,7 @@ def main():
         }
     if rank == 0 and world == 1 and not inproc and mesh is not None and args.outer > 0 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(mesh, n_cells, args.outer, args.inner)
+            out["cpu_baseline"] = cpu_baseline(mesh, n_cells, args.outer, args.inner, step_bytes, step_layout)
         except Exception as e:  # the baseline is reported, never the target
             log("cpu baseline failed:", e)
             out["cpu_baseline"] = None

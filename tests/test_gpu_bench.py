@@ -33,6 +33,10 @@ def test_bench_json_contract():
     assert rf["traffic"] is None  # PMC traffic is committed for the C2 workload only
     cb = d["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1 and cb["sample"]
+    g = cb["gbs"]  # the CPU GB/s from the same algorithmic byte counts
+    assert g["reference_format_gbs"] > 0 and g["layout_true_gbs"] > 0
+    assert abs(g["reference_format_gbs"] - d["step_reference_format_bytes_count"] / g["seconds_per_step"] / 1e9) \
+        <= 1e-9 * g["reference_format_gbs"]
 
 
 def test_bench_two_process_launch_contract():
