@@ -670,7 +670,7 @@ def main():
             "reference_format_effective_gbs": achieved_ref,
             "avg_launch_us": sm_avg_s * 1e6,
             "launches": sm_n,  # timed sweeps: every sample_stride-th level-0 sweep of the timed steps
-            "sample_stride": max(1, int(os.environ.get("CFD_PROF_STRIDE", "1"))),
+            "sample_stride": 1,  # every level-0 sweep of the timed steps
         },
         "comm": comm_line,
         # hipGraph replay of the FGMRES iteration: captures / replays inside the timed steps

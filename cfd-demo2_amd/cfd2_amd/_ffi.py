@@ -150,7 +150,9 @@ class StateFileHeader(C.Structure):  # cfd_state_file_header (512 bytes)
         ("constants", Constants),
         ("info", StepInfo),
         ("amg_age", C.c_uint32),
-        ("reserved", C.c_uint8 * 172),
+        ("amg_local_aggregation", C.c_int32),
+        ("nranks", C.c_int32),
+        ("reserved", C.c_uint8 * 164),
     ]
 
 

@@ -57,6 +57,8 @@ class SolverState:
     inner_last: float = 0.0
     variance: list = field(default_factory=list)   # [(var_u, var_v)], oldest first, <= 10
     amg_age: int = 0                                # steps since the hierarchy was built
+    amg_local_aggregation: int = 0                  # the saving run's aggregation mode
+    nranks: int = 0                                 # the saving run's rank count (0: not recorded)
     amg_rowptr: np.ndarray | None = None            # uint64 (N+1,) or None
     amg_val: np.ndarray | None = None               # float32 (nnz,)
 
@@ -97,6 +99,7 @@ def read_state(path) -> SolverState:
         x=arr(off["x"], np.float32, 3 * n, (n, 3)),
         have_prev=bool(h.have_prev), inner_has_last=bool(h.inner_has_last), inner_last=float(h.inner_last),
         variance=[(h.variance[k][0], h.variance[k][1]) for k in range(h.n_variance)], amg_age=int(h.amg_age),
+        amg_local_aggregation=int(h.amg_local_aggregation), nranks=int(h.nranks),
         amg_rowptr=arr(off["amg_rowptr"], np.uint64, n + 1) if nnz else None,
         amg_val=arr(off["amg_val"], np.float32, nnz) if nnz else None)
 
@@ -123,6 +126,8 @@ def write_state(path, st: SolverState) -> None:
     h.constants = st.constants
     h.info = st.info
     h.amg_age = int(st.amg_age)
+    h.amg_local_aggregation = int(st.amg_local_aggregation)
+    h.nranks = int(st.nranks)
     tmp = f"{path}.tmp{os.getpid()}"
     with open(tmp, "wb") as f:
         f.write(bytes(h))

@@ -2909,9 +2909,9 @@ void launch_solve_triangular(const float* H, const float* g, float* y, int k, in
   hipLaunchKernelGGL(k_solve_triangular, dim3(1), dim3(256), 0, s, H, g, y, k, m1);
 }
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
-                     hipStream_t s) {
+                     hipStream_t s, bool lat) {
   if (!n) return;
-  if (n / 3 <= CFD_CGS_LAT_MAX_CELLS && k > 2) {
+  if (lat && n / 3 <= CFD_CGS_LAT_MAX_CELLS && k > 2) {
     hipLaunchKernelGGL(k_update_x_lat, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, x, z, stride, y, k, n);
     return;
   }

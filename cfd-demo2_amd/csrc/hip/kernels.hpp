@@ -339,8 +339,9 @@ void launch_precond_correct(const CoupledMatrix& A, const float* w_in, const flo
                             const float* p_sol, const float* dinv_uv, float* z, hipStream_t s);
 void launch_solve_triangular(const float* H, const float* g, float* y, int k, int m1,
                              hipStream_t s);
+// lat: the latency form allowed (small meshes; false = the streaming form)
 void launch_update_x(float* x, const float* z, size_t stride, const float* y, int k, size_t n,
-                     hipStream_t s);
+                     hipStream_t s, bool lat = true);
 // ev0/ev1 (optional): timing events recorded by the GPU at kernel start / end
 // nt: the level matrix, b and the diagonal read with the nontemporal policy
 void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, float* x_out,

@@ -224,8 +224,6 @@ cfd_status cfd_profile_reset(cfd_solver* s) {
     s->s->prof_ms = 0.0;
     s->s->prof_launches = 0;
     s->s->prof_seq = 0;
-    const char* ps = std::getenv("CFD_PROF_STRIDE");
-    s->s->prof_stride = ps ? std::max(1u, (uint32_t)std::strtoul(ps, nullptr, 10)) : 1u;
     s->s->prof_grow(8192);  // 4096 timed launches without growing inside the timed steps
   });
 }

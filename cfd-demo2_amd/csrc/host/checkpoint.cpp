@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdio>
 #include <cstddef>
 #include <cstring>
 
@@ -35,6 +36,7 @@ static_assert(offsetof(cfd_state_file_header, variance) == 64, "cfd_state_file_h
 static_assert(offsetof(cfd_state_file_header, constants) == 224, "cfd_state_file_header layout");
 static_assert(offsetof(cfd_state_file_header, info) == 280, "cfd_state_file_header layout");
 static_assert(offsetof(cfd_state_file_header, amg_age) == 336, "cfd_state_file_header layout");
+static_assert(offsetof(cfd_state_file_header, nranks) == 344, "cfd_state_file_header layout");
 
 namespace {
 
@@ -120,6 +122,8 @@ void Solver::save_state(const char* path) {
         h.constants = constants;
         h.info = info;
         h.amg_age = amg_refresh_pending ? 0 : amg_age;
+        h.amg_local_aggregation = amg_local ? 1 : 0;
+        h.nranks = R;
         pwrite_all(fd, &h, sizeof(h), 0);
       }
       // owned rows of every per-cell array at their global offsets
@@ -249,6 +253,15 @@ void Solver::load_state(const char* path) {
     sync();
   }
   if (amg_built) drop_amg();  // the saved run's hierarchy replaces this solver's
+  // the hierarchy is rebuilt under THIS solver's mode and rank count: the same
+  // as the saving run's unless a partition-aware hierarchy is involved
+  if (h.amg_nnz && h.nranks > 0 && rk == 0 &&
+      ((h.amg_local_aggregation != 0) != amg_local || (amg_local && h.nranks != R)))
+    std::fprintf(stderr,
+                 "cfd_state_load: the file was saved with amg_local_aggregation=%d on %d rank(s); this solver "
+                 "runs amg_local_aggregation=%d on %d: the AMG hierarchy rebuilt from the saved matrix differs, "
+                 "so the continuation is not bit-identical to the saving run\n",
+                 (int)h.amg_local_aggregation, (int)h.nranks, amg_local ? 1 : 0, R);
   amg_src_loaded = h.amg_nnz != 0;
   amg_age = h.amg_age;
   step_index = (h.step_index + 2) % 3;  // rotate() advances it back to the saved slot triple

@@ -1629,19 +1629,30 @@ void Solver::run_iteration(int j, float* pin, int variant) {
     hipGraph_t gr = nullptr;
     CFD_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     capturing = &G;
+    // a failed capture or instantiation leaves no timing pairs behind: they
+    // were never recorded, and a later capture must not append after them
+    auto reset_graph = [&] {
+      for (auto ev : G.ev) (void)hipEventDestroy(ev);
+      G = IterGraph{};
+    };
     try {
       iteration(j, pin);
     } catch (...) {
       capturing = nullptr;
       (void)hipStreamEndCapture(stream, &gr);
       if (gr) (void)hipGraphDestroy(gr);
+      reset_graph();
       throw;
     }
     capturing = nullptr;
-    CFD_HIP(hipStreamEndCapture(stream, &gr));
-    const hipError_t e = hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(gr);
-    CFD_HIP(e);
+    const hipError_t ec = hipStreamEndCapture(stream, &gr);
+    const hipError_t e = ec == hipSuccess ? hipGraphInstantiate(&G.exec, gr, nullptr, nullptr, 0) : ec;
+    if (gr) (void)hipGraphDestroy(gr);
+    if (e != hipSuccess) {
+      G.exec = nullptr;
+      reset_graph();
+      CFD_HIP(e);
+    }
     G.prof = prof;
     graph_captures++;
   }
@@ -1733,7 +1744,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       }
     }
     launch_solve_triangular(H, g, y, basis_size, m1, stream);
-    launch_update_x(x, zvec, stride, y, basis_size, n, stream);
+    launch_update_x(x, zvec, stride, y, basis_size, n, stream, cgs_lat);  // CFD_CGS_LAT=0: streaming form too
     check_launch("FGMRES solution update");
     if (converged) {  // async_reader.flush()
       flush_inner();

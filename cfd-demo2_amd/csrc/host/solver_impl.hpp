@@ -421,13 +421,13 @@ struct Solver {
   size_t prof_used = 0;
   double prof_ms = 0.0;
   uint64_t prof_launches = 0;
-  // every prof_stride-th level-0 sweep is timed (CFD_PROF_STRIDE, default
-  // 1).  An event-bracketed launch is serialised with its neighbours: timing
-  // every sweep costs ~0.7 % of the step, but a sample of them reads ~4 %
-  // slower than the rocprofv3 average of all sweeps, so all are timed.
-  uint32_t prof_stride = 1;
+  // every level-0 sweep is timed while profiling is on.  An event-bracketed
+  // launch is serialised with its neighbours: timing every sweep costs ~0.7 %
+  // of the step, but a sample of them (round 4's CFD_PROF_STRIDE, removed:
+  // under graph replay the sample was frozen into the captured graphs) read
+  // ~4 % slower than the rocprofv3 average of all sweeps.
   uint64_t prof_seq = 0;
-  bool prof_take() { return prof && (prof_seq++ % prof_stride) == 0; }
+  bool prof_take() { return prof && (++prof_seq, true); }
 
   // ---- hipGraph replay of the FGMRES iteration (Solver::run_iteration) ----
   // One executable graph per (basis index j, residual-slot variant): the

@@ -245,7 +245,12 @@ uint32_t cfd_num_faces(const cfd_solver* s);
  *   x f32[3N]  (FGMRES solution = initial guess of the next solve)
  *   if amg_nnz > 0: amg_rowptr u64[N+1], amg_val f32[amg_nnz] -- the scalar
  *   pressure matrix the AMG hierarchy was built from (CSR, columns ascending;
- *   the pattern is the mesh's), so the loader rebuilds the same hierarchy.  */
+ *   the pattern is the mesh's), so the loader rebuilds the same hierarchy --
+ *   under the LOADER's aggregation mode and rank count: the default (global)
+ *   hierarchy is rank-count independent; a partition-aware one
+ *   (amg_local_aggregation = 1) depends on the rank count, so a file saved
+ *   in that mode continues bit-identically only on the same rank count and
+ *   mode.  The loader prints a warning on stderr when they differ.          */
 typedef struct cfd_state_file_header {
   char magic[8];        /* "CFD2STAT" */
   uint32_t version;     /* 1 */
@@ -263,7 +268,9 @@ typedef struct cfd_state_file_header {
   cfd_constants constants;
   cfd_step_info info;
   uint32_t amg_age;     /* steps since the hierarchy was built (amg_rebuild_interval) */
-  uint8_t reserved[172];
+  int32_t amg_local_aggregation; /* cfd_config.amg_local_aggregation of the saving run */
+  int32_t nranks;       /* rank count of the saving run (0: not recorded)             */
+  uint8_t reserved[164];
 } cfd_state_file_header;
 
 /* Writes the state to `path`.  Distributed solver: COLLECTIVE, every rank
@@ -282,8 +289,8 @@ cfd_status cfd_group_state_save(cfd_solver* const* handles, int32_t nranks, cons
  * AMG smoother sweep, on the solver's own stream.                            */
 cfd_status cfd_profile_enable(cfd_solver* s, int32_t enable);
 cfd_status cfd_profile_reset(cfd_solver* s);
-/* total_ms / launches over the TIMED level-0 smoother sweeps (every
- * CFD_PROF_STRIDE-th sweep, default 1, from cfd_profile_reset on); bytes =
+/* total_ms / launches over the level-0 smoother sweeps since
+ * cfd_profile_reset (every sweep timed while profiling is on); bytes =
  * algorithmic bytes per sweep (4(n+1) + 8 nnz + 12 n).       */
 cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t* launches,
                                 double* bytes_per_launch);

@@ -110,12 +110,17 @@ def test_rank_count_independent_file(tmp_path, monkeypatch):
     p2 = str(tmp_path / "r2.bin")
     g2.save_state(p2)
     raw = open(p2, "rb").read()
+    assert read_state(p2).nranks == 2 and read_state(p2).amg_local_aggregation == 0
+
+    def masked(b):  # every byte but the header's record of the saving rank count (offset 344)
+        return b[:344] + b[348:]
     for r in (1, 3, 6):
         h = GpuSolver(mesh) if r == 1 else GpuGroup(mesh, r)
         h.load_state(p2)
         pr = str(tmp_path / f"r{r}.bin")
         h.save_state(pr)
-        assert open(pr, "rb").read() == raw, f"R={r} re-save differs"
+        assert read_state(pr).nranks == r
+        assert masked(open(pr, "rb").read()) == masked(raw), f"R={r} re-save differs"
         h.close()
     g2.step()
     o.step()
@@ -176,3 +181,40 @@ def test_load_into_a_running_solver(tmp_path):
             s.step()
             _same(_snap(s), ref[k], f"replay step {k}")
         assert s.amg_setup_info()[1] == digests
+
+
+def test_partition_aware_file_records_mode_and_rank_count(tmp_path, capfd):
+    """A partition-aware run (amg_local_aggregation=1) records its mode and rank
+    count; loading it under another rank count or mode warns (the hierarchy
+    rebuilt from the saved matrix differs); the same count and mode load
+    silently (include/cfd2_amd.h, cfd_state_file_header)."""
+    import os
+    old = os.environ.get("CFD_AMG_REPLICATE_ROWS")
+    os.environ["CFD_AMG_REPLICATE_ROWS"] = "50"
+    try:
+        mesh = backwards_step()
+        cfg = default_config(amg_local_aggregation=1, fixed_outer=1, fixed_inner=6)
+        g = GpuGroup(mesh, 2, config=cfg)
+        _setup(g, mesh, 1, 1, 0)
+        g.step()
+        p = str(tmp_path / "local2.bin")
+        g.save_state(p)
+        st = read_state(p)
+        assert st.amg_local_aggregation == 1 and st.nranks == 2 and st.amg_val is not None
+        capfd.readouterr()
+        same = GpuGroup(mesh, 2, config=cfg)
+        same.load_state(p)
+        assert "cfd_state_load" not in capfd.readouterr().err
+        other = GpuGroup(mesh, 3, config=cfg)
+        other.load_state(p)
+        assert "amg_local_aggregation=1 on 2 rank(s)" in capfd.readouterr().err
+        glob = GpuGroup(mesh, 2, config=default_config(fixed_outer=1, fixed_inner=6))
+        glob.load_state(p)
+        assert "this solver runs amg_local_aggregation=0" in capfd.readouterr().err
+        for h in (g, same, other, glob):
+            h.close()
+    finally:
+        if old is None:
+            os.environ.pop("CFD_AMG_REPLICATE_ROWS", None)
+        else:
+            os.environ["CFD_AMG_REPLICATE_ROWS"] = old

@@ -21,7 +21,8 @@ def _state(n, nnz, seed=0):
     return SolverState(num_faces=4 * n, step_index=1, constants=c, info=info, slots=[blk(), blk(), blk()],
                        prev=blk(), x=rng.standard_normal((n, 3), dtype=np.float32), have_prev=True,
                        inner_has_last=True, inner_last=0.25, variance=[(1.0, 2.0), (3.0, 4.0)],
-                       amg_rowptr=rp, amg_val=rng.standard_normal(nnz, dtype=np.float32) if nnz else None)
+                       amg_rowptr=rp, amg_val=rng.standard_normal(nnz, dtype=np.float32) if nnz else None,
+                       amg_local_aggregation=1, nranks=4)
 
 
 def test_header_layout_matches_c():
@@ -29,6 +30,7 @@ def test_header_layout_matches_c():
     assert _ffi.StateFileHeader.variance.offset == 64
     assert _ffi.StateFileHeader.constants.offset == 224
     assert _ffi.StateFileHeader.info.offset == 280
+    assert _ffi.StateFileHeader.amg_age.offset == 336 and _ffi.StateFileHeader.nranks.offset == 344
 
 
 @pytest.mark.parametrize("nnz", [0, 37])
@@ -44,6 +46,7 @@ def test_round_trip(tmp_path, nnz):
     assert r.variance == [(1.0, 2.0), (3.0, 4.0)]
     assert r.constants.time == np.float32(0.5) and r.constants.time_scheme == 1
     assert r.info.degenerate_count == 3 and r.info.outer_iterations == 7
+    assert r.amg_local_aggregation == 1 and r.nranks == 4
     for a, b in zip(r.slots + [r.prev], st.slots + [st.prev]):
         for k in a:
             assert np.array_equal(a[k], b[k])
