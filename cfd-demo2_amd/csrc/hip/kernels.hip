@@ -1411,34 +1411,13 @@ __global__ void __launch_bounds__(kRedFinalThreads) k_norm_givens(RedSrc r, int 
 #define CFD_PREDICT_U1 5
 #endif
 
-// relax_pressure (schur_precond.wgsl:52-90), omega = 1.2, live scalar matrix
-__global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t ld, const int32_t* __restrict__ col,
-                                                           const uint32_t* __restrict__ len,
-                                                           const float* __restrict__ sval,
-                                                           const float* __restrict__ dinv_p,
-                                                           const float* __restrict__ temp_p,
-                                                           const float* __restrict__ p_sol,
-                                                           float* p_prev) {
-  const uint32_t i = row_id();
-  if (i >= N) return;
-  float sigma = 0.0f;
-  const uint32_t l = len[i];
-  for (uint32_t r = 0; r < l; ++r) {
-    const size_t slot = (size_t)r * ld + i;
-    const int32_t cc = col[slot];
-    if (cc != (int32_t)i) sigma += sval[slot] * p_sol[cc];
-  }
-  const float hat_x = dinv_p[i] * (temp_p[i] - sigma);
-  p_prev[i] = wmix(p_prev[i], hat_x, 1.2f);
-}
-
 // Every relax_pressure sweep of one preconditioner application in ONE
-// workgroup (small meshes, N < 8192): the p_iters launches of k_relax_pressure
+// workgroup (small meshes, N < 8192): the p_iters launches of k_relax_pressure4
 // (64 at the reference's 8 k-cell benchmark mesh, each a ~4.6 us launch for a
 // few microseconds of work) become one kernel.  Thread t owns rows t + 1024 k;
 // its rows' off-diagonal entries (values + LDS byte addresses of their
 // columns, compacted in slot order: the diagonal is skipped as in
-// k_relax_pressure), temp_p and dinv_p live in registers for all sweeps; the
+// k_relax_pressure4), temp_p and dinv_p live in registers for all sweeps; the
 // two ping-pong iterates live in LDS (P = p_sol at byte 0, T = temp at byte
 // 32768: a sweep's source buffer is an immediate offset; unit-stride rows keep
 // the neighbour reads free of bank conflicts).  Sweep s reads the iterate
@@ -1447,7 +1426,7 @@ __global__ void __launch_bounds__(kBlock) k_relax_pressure(uint32_t N, uint32_t 
 // orders it.  Unused entries point at a zero row with value +0: they add
 // +0 * +0 = +0 to sigma, which starts at +0 and so is never -0 (a
 // round-to-nearest sum is -0 only if both operands are), hence sigma + +0 ==
-// sigma bit for bit -- the f32 result of k_relax_pressure, without a compare
+// sigma bit for bit -- the f32 result of k_relax_pressure4, without a compare
 // and select per entry.
 constexpr int kRelaxThreads = 1024;
 template <int RPT, int OD>
@@ -2106,7 +2085,8 @@ __global__ void __launch_bounds__(kBlock) k_amg_residual(AmgLevelDev L, const fl
 // over the scalar ELL image (16-bit column deltas, u8 lengths / diagonal ranks,
 // the AMG row kernels' slot groups and vector gathers): the diagonal sits in
 // the slots and is skipped by its rank, every other entry is summed in slot
-// order -- k_relax_pressure's f32 operations, row for row.
+// order -- the reference's f32 operations (omega = 1.2, the live scalar
+// matrix), row for row.
 template <bool D16>
 __global__ void __launch_bounds__(kBlock) k_relax_pressure4(AmgLevelDev L, const uint8_t* __restrict__ drank,
                                                             const float* __restrict__ dinv_p,
@@ -2858,13 +2838,6 @@ void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const flo
   auto fn = A.use16 ? (nt ? k_precond_predict2<true, true> : k_precond_predict2<true, false>)
                     : (nt ? k_precond_predict2<false, true> : k_precond_predict2<false, false>);
   hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, A, w_in, binv, j, dinv_uv, dinv_p, temp_p, p_sol, p_prev);
-}
-void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len, const float* sval,
-                           const float* dinv_p, const float* temp_p, const float* p_sol, float* p_prev,
-                           hipStream_t s) {
-  if (N)
-    hipLaunchKernelGGL(k_relax_pressure, dim3(grid_for(N)), dim3(kBlock), 0, s, N, ld, col, len, sval, dinv_p,
-                       temp_p, p_sol, p_prev);
 }
 void launch_relax_pressure4(const AmgLevelDev& L, const uint8_t* drank, const float* dinv_p, const float* temp_p,
                             const float* src, float* dst, hipStream_t s) {

@@ -320,9 +320,6 @@ void launch_norm_givens(const RedSrc& r, int j, float* H, int m1, float* givens,
 void launch_precond_predict(const CoupledMatrix& A, const float* w_in, const float* binv, int j,
                             const float* dinv_uv, const float* dinv_p, float* temp_p, float* p_sol,
                             float* p_prev, hipStream_t s, bool nt = false);
-void launch_relax_pressure(uint32_t N, uint32_t ld, const int32_t* col, const uint32_t* len,
-                           const float* sval, const float* dinv_p, const float* temp_p,
-                           const float* p_sol, float* p_prev, hipStream_t s);
 // one relax_pressure sweep, 4 rows per thread over the scalar ELL image viewed as
 // an AmgLevelDev (val = the live scalar matrix, len / col16 / col32 incl. the
 // diagonal, skipped by `drank`); rows [L.r0, L.r1) + [L.r2, L.r3)

@@ -111,7 +111,7 @@ bool Solver::build_amg_device() {
 // distributed run computes the same replicated levels, so a false return
 // (capacity overflow, wide rows) is the same on every rank.
 bool Solver::device_levels(AmgSetupLevel& cur_in, int li0, const std::vector<uint64_t>& part0) {
-  const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
+  const bool timing = cfg.log_level >= 2 && rk == 0;
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
   auto zeroed = [&](size_t cnt) {
@@ -294,7 +294,7 @@ std::vector<std::vector<uint32_t>> Solver::allgatherv_u32(const std::vector<uint
 // hierarchy: a Galerkin capacity overflow or rows wider than the u8 layout.
 bool Solver::build_amg_device_dist() {
   comm->label = -1;  // setup collectives (watchdog reports)
-  const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
+  const bool timing = cfg.log_level >= 2 && rk == 0;
   using clk = std::chrono::steady_clock;
   auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
   const uint64_t rep = amg_replicate_rows();
@@ -763,11 +763,6 @@ bool Solver::build_amg_device_dist() {
         for (uint32_t i = 0; i < nown; ++i)
           if ((int32_t)aggp[i] < 0 || aggp[i] >= nown_c) G.pf_lo = i + 1;
         G.pf_lo = std::min((G.pf_lo + 3) & ~3u, nown);
-      }
-      const char* ov = std::getenv("CFD_AMG_HALO_OVERLAP");
-      if (ov && ov[0] == '0') {  // everything after the exchange (A/B)
-        G.rc_hi = 0;
-        G.pf_lo = nown;
       }
       G.dev.agg = arena.upload(aggp, stream, kAggSlack);
       G.dev.r_row = arena.upload(r_row, stream);

@@ -130,7 +130,8 @@ void transpose_aggregates(const std::vector<uint32_t>& agg, uint32_t nagg, std::
 }
 
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
-                                               const std::vector<uint64_t>& part0, bool local, uint64_t rep_rows) {
+                                               const std::vector<uint64_t>& part0, bool local, uint64_t rep_rows,
+                                               bool timing) {
   std::vector<AmgHostLevel> levels;
   HostCsr cur = fine;
   // row partition of the current level (distributed solver): coarse rows
@@ -171,7 +172,7 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
         const auto t1 = std::chrono::steady_clock::now();
         HostCsr next = spgemm(RA, P);
         const auto t2 = std::chrono::steady_clock::now();
-        if (std::getenv("CFD_AMG_SETUP_TIMING"))
+        if (timing)
           std::fprintf(stderr, "[amg setup] level %zu: n=%zu nagg=%u  R*A %.3fs  (RA)*P %.3fs\n", li, n, nagg,
                        std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
         L.agg = std::move(agg);

@@ -87,8 +87,6 @@ HaloPlan build_halo_plan_lists(const std::vector<uint64_t>& starts, int rank,
   }
   P.all_direct = true;
   for (const HaloPeer& h : P.peers) P.all_direct = P.all_direct && h.direct >= 0;
-  if (const char* e = std::getenv("CFD_HALO_PACK"))  // 1: always pack (A/B, tests)
-    if (e[0] == '1') P.all_direct = false;
   return P;
 }
 
@@ -144,8 +142,6 @@ HaloPlan build_halo_plan(const std::vector<uint64_t>& starts, int rank, const ui
   }
   P.all_direct = true;
   for (const HaloPeer& h : P.peers) P.all_direct = P.all_direct && h.direct >= 0;
-  if (const char* e = std::getenv("CFD_HALO_PACK"))  // 1: always pack (A/B, tests)
-    if (e[0] == '1') P.all_direct = false;
   return P;
 }
 

@@ -78,38 +78,24 @@ Solver::Solver(const cfd_mesh_view& mesh, const cfd_config& c, int dev, std::uni
   vlen = (size_t)shift + topo.npad + topo.ghi;
   CFD_HIP(hipSetDevice(device));
   lds_budget = init_kernel_attributes(device);
-  if (const char* wl = std::getenv("CFD_AMG_WIDE_LIMIT"))
-    amg_wide_limit = std::max(1, std::min(255, (int)std::strtol(wl, nullptr, 10)));
-  {
-    const char* cs = std::getenv("CFD_CHECK_SYNC");
-    check_sync = cs && cs[0] == '1';
-  }
-  if (const char* rf = std::getenv("CFD_RELAX_FUSED")) relax_fused = rf[0] != '0';
-  if (const char* r4 = std::getenv("CFD_RELAX4")) relax4 = r4[0] != '0';
-  if (const char* cr = std::getenv("CFD_COUPLED_REG")) coupled_reg = cr[0] != '0';
-  if (const char* ne = std::getenv("CFD_NT")) nt_mask = (unsigned)std::strtoul(ne, nullptr, 0);
+  amg_wide_limit = (int)std::max<uint64_t>(1, std::min<uint64_t>(255, knob_u64(Knob::AmgWideLimit, 255)));
+  check_sync = cfg.log_level >= 3;  // debug: synchronise and check after every launch
+  small_forms = knob_on(Knob::SmallMeshForms);
+  nt_mask = (unsigned)knob_u64(Knob::Nt, nt_mask);
   // C1-size meshes: 64 MB of the dots pass kept in the Infinity Cache for a
   // top-down update (profiles/r04/ab_cgskeep2_c1.txt: update 36.5-36.9 ->
   // 32.3 us, dots +0.3 us per iteration); from 2^22 cells on the kept lines
   // cost more than they return (ab_cgskeep_c2.txt: dots 284 -> 293 us)
   cgs_keep_bytes = N < (1u << 22) ? (size_t)64 << 20 : 0;  // (kernels.hip CFD_CGS_SER_MIN_CELLS)
-  if (const char* ck = std::getenv("CFD_CGS_KEEP_MB")) cgs_keep_bytes = (size_t)std::strtoull(ck, nullptr, 10) << 20;
-  if (const char* cu = std::getenv("CFD_CGS_UPDATE_NT")) cgs_update_nt = cu[0] == '1';
-  if (const char* cf = std::getenv("CFD_CGS_FUSE_REDUCE")) cgs_fuse_reduce = cf[0] != '0';
-  if (const char* cl = std::getenv("CFD_CGS_LAT")) cgs_lat = cl[0] != '0';
   CFD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   amg_local = dist() && cfg.amg_local_aggregation != 0;
-  {
-    const char* ge = std::getenv("CFD_GRAPH");
-    // opt-in: replay measured no faster than eager launches on this pool
-    // (profiles/r05/ab_graph_c0_c1.txt: C0 13.36-13.47 vs 13.30-13.51 ms/step,
-    // C1 39.6-39.9 vs 38.8-39.1): the host runs ahead of the GPU either way
-    graph_on = ge && ge[0] == '1';
-    if (dist()) graph_on = false;  // halo exchanges and collectives stay eager
-  }
+  // hipGraph replay: opt-in through cfd_graph_enable (replay measured no faster
+  // than eager launches on this pool, profiles/r05/ab_graph_c0_c1.txt: C0
+  // 13.36-13.47 vs 13.30-13.51 ms/step, C1 39.6-39.9 vs 38.8-39.1); halo
+  // exchanges and collectives stay eager
+  graph_on = false;
   if (dist()) {
-    const char* oe = std::getenv("CFD_OVERLAP_MIN_ROWS");
-    if (oe) overlap_min_rows = (uint32_t)std::strtoul(oe, nullptr, 10);
+    overlap_min_rows = (uint32_t)knob_u64(Knob::OverlapMinRows, overlap_min_rows);
     CFD_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     CFD_HIP(hipEventCreateWithFlags(&hev_pack, hipEventDisableTiming));
     CFD_HIP(hipEventCreateWithFlags(&hev_done, hipEventDisableTiming));
@@ -268,7 +254,7 @@ CoupledMatrix Solver::cmat() const {
   A.cval_a = cval_a;
   A.cval_g = cval_g;
   A.cdiag2 = cdiag2;
-  A.reg = coupled_reg && !topo.tmode.empty() && topo.ws <= kCoupledRegMaxWs ? 1 : 0;
+  A.reg = !topo.tmode.empty() && topo.ws <= kCoupledRegMaxWs ? 1 : 0;
   for (int r = 0; r < 8; ++r) A.tmode[r] = r < (int)topo.tmode.size() ? topo.tmode[r] : 0;
   return A;
 }
@@ -713,7 +699,7 @@ std::vector<uint64_t> Solver::allgather_u64(uint64_t mine) {
 // 50.2 us, level 2 15.1 -> 12.3) and on the small latency-bound levels;
 // predicated loads on ragged big levels.
 void Solver::set_amg_full_policy(AmgGpuLevel& G, int li) {
-  const char* fe = std::getenv("CFD_AMG_FULL");
+  const char* fe = knob(Knob::AmgFull);
   const double n = std::max<double>(G.dev.n, 1.0);
   const double offd = ((double)G.nnz - n) / n;  // mean off-diagonals per row
   const bool regular = G.dev.w > 0 && offd >= 0.75 * G.dev.w;
@@ -738,7 +724,7 @@ void Solver::build_amg_host() {
     A0.row = topo.srow;
     A0.col = topo.scol;
     A0.val = std::move(own);
-    H = build_amg_hierarchy(A0, kMaxAmgLevels);
+    H = build_amg_hierarchy(A0, kMaxAmgLevels, {}, false, 0, cfg.log_level >= 2);
   } else {
     // all-gather the global pattern and the values (row order = global order, rank by rank)
     const std::vector<uint64_t> nz = allgather_u64(topo.scol.size());
@@ -770,7 +756,7 @@ void Solver::build_amg_host() {
     CFD_HIP(hipMemcpyAsync(A0.val.data(), d_vals, nnz_all * 4, hipMemcpyDeviceToHost, stream));
     sync();
     for (uint32_t i = 0; i < NG; ++i) A0.row[i + 1] = A0.row[i] + lens[i];
-    H = build_amg_hierarchy(A0, kMaxAmgLevels, starts, amg_local, amg_replicate_rows());
+    H = build_amg_hierarchy(A0, kMaxAmgLevels, starts, amg_local, amg_replicate_rows(), cfg.log_level >= 2 && rk == 0);
   }
   const int L = (int)H.size();
   // distributed levels [0, amg_g): the rest are replicated (all of them on one GPU)
@@ -924,11 +910,6 @@ void Solver::build_amg_host() {
             if ((int32_t)agg[i] < 0 || agg[i] >= ncl) G.pf_lo = i + 1;
           G.pf_lo = std::min((G.pf_lo + 3) & ~3u, nown);
         }
-        const char* ov = std::getenv("CFD_AMG_HALO_OVERLAP");
-        if (ov && ov[0] == '0') {  // everything after the exchange (A/B)
-          G.rc_hi = 0;
-          G.pf_lo = nown;
-        }
       } else {
         std::copy(HL.agg.begin(), HL.agg.end(), agg.begin());
         r_row = HL.r_row;
@@ -979,9 +960,9 @@ void Solver::ensure_amg() {
     return;
   }
   const Range range("amg setup");
-  const bool timing = std::getenv("CFD_AMG_SETUP_TIMING") != nullptr;
+  const bool timing = cfg.log_level >= 2 && rk == 0;
   const auto t_start = std::chrono::steady_clock::now();
-  const char* se = std::getenv("CFD_AMG_SETUP");
+  const char* se = knob(Knob::AmgSetup);
   const bool device_setup = !(se && std::string(se) == "host");
   const char* how = "device";
   amg_setup_path = 2;
@@ -1014,21 +995,26 @@ void Solver::ensure_amg() {
   }
   const int L = (int)levels.size();
   set_resrestrict_blocks();
+  // post-smoothers with the prolongation fused (single-GPU / replicated
+  // levels of at most CFD_AMG_FUSED_PROLONG_ROWS rows; 0: never)
+  fuse_prolong_rows = knob_u64(Knob::AmgFusedProlongRows, 1ull << 20);
+  // the tail form: blob<K> (default blob2), lds, global
+  {
+    const char* tf = knob(Knob::AmgTail);
+    tail_form = 2;
+    tail_blob_shift = 2;
+    if (tf && std::strncmp(tf, "blob", 4) == 0) {
+      if (tf[4]) tail_blob_shift = std::max(0, (int)std::strtol(tf + 4, nullptr, 10));
+    } else if (tf && std::strcmp(tf, "lds") == 0) {
+      tail_form = 1;
+    } else if (tf && std::strcmp(tf, "global") == 0) {
+      tail_form = 0;
+    } else if (tf) {
+      throw std::invalid_argument(std::string("CFD_AMG_TAIL: expected blob<K>, lds or global, got ") + tf);
+    }
+  }
   // replicated levels from `tail_first` down run inside one single-workgroup kernel
-  const char* fz_env = std::getenv("CFD_AMG_FUSE_PRESMOOTH");
-  fuse_presmooth = !(fz_env && fz_env[0] == '0');
-  // post-smoothers with the prolongation fused (single-GPU / replicated levels
-  // from CFD_AMG_FUSED_PROLONG=<level> on -- "off": never -- with at most
-  // CFD_AMG_FUSED_PROLONG_ROWS rows)
-  const char* fp_env = std::getenv("CFD_AMG_FUSED_PROLONG");
-  fuse_prolong_from = 0;
-  if (fp_env) fuse_prolong_from = (fp_env[0] == 'o') ? kMaxAmgLevels : (int)std::strtol(fp_env, nullptr, 10);
-  const char* fpr_env = std::getenv("CFD_AMG_FUSED_PROLONG_ROWS");
-  fuse_prolong_rows = fpr_env ? std::strtoull(fpr_env, nullptr, 10) : (1ull << 20);
-  const char* tl_env = std::getenv("CFD_AMG_TAIL_LDS");
-  tail_lds = !(tl_env && tl_env[0] == '0');
-  const char* env = std::getenv("CFD_AMG_TAIL_ROWS");
-  const uint32_t tail_rows = env ? (uint32_t)std::strtoul(env, nullptr, 10) : 4096u;
+  const uint32_t tail_rows = (uint32_t)knob_u64(Knob::AmgTailRows, 4096u);
   const int lo = std::max(amg_g, 1);
   tail_first = L;
   while (tail_first > lo && levels[tail_first - 1].dev.n <= tail_rows) --tail_first;
@@ -1061,13 +1047,12 @@ void Solver::ensure_amg() {
   }
   d_tail = arena.upload(tl, stream);
   check_launch("AMG setup");
-  const char* tb_env = std::getenv("CFD_AMG_TAIL_BLOB");
-  if (tail_lds && !(tb_env && tb_env[0] == '0')) {
+  if (tail_form == 2) {
     // The LDS image of the tail (matrices included) is the fast tail; when it
-    // does not fit in one CU's LDS, up to CFD_AMG_BLOB_SHIFT (default 2) more
-    // levels run with the row kernels so that it does (C1: the 3.9 k-row level).
-    const char* sh_env = std::getenv("CFD_AMG_BLOB_SHIFT");
-    const int shift = sh_env ? std::max(0, (int)std::strtol(sh_env, nullptr, 10)) : 2;
+    // does not fit in one CU's LDS, up to tail_blob_shift (CFD_AMG_TAIL=blob<K>,
+    // default 2) more levels run with the row kernels so that it does (C1: the
+    // 3.9 k-row level).
+    const int shift = tail_blob_shift;
     const int t0 = std::max({tail_first, 1, dist() ? amg_g : 0});
     for (int t = t0; t < std::min(L, t0 + 1 + shift) && tail_blob_first < 0; ++t) {
       if (t > t0 && levels[t - 1].wide) break;  // wide levels run only in the tail kernels
@@ -1092,16 +1077,13 @@ void Solver::ensure_amg() {
 // permuted rows only pays on the latency-bound levels: same-box A/B
 // (profiles/r03/ab_log.md) C2 level 0 129 vs 68 + 34 us, level 1 104 vs
 // 56 + 13 us; C1 levels of 125 k rows and fewer 6-8 vs 10-11 us.
-// CFD_AMG_FUSED_RR=0 keeps the two kernels everywhere.
+// CFD_AMG_FUSED_RR_ROWS=0 keeps the two kernels everywhere.
 void Solver::set_resrestrict_blocks() {
-  const char* fe = std::getenv("CFD_AMG_FUSED_RR");
-  const bool on = !(fe && fe[0] == '0');
-  const char* fr = std::getenv("CFD_AMG_FUSED_RR_ROWS");
-  const uint64_t max_rows = fr ? std::strtoull(fr, nullptr, 10) : (1u << 18);
+  const uint64_t max_rows = knob_u64(Knob::AmgFusedRrRows, 1u << 18);
   for (AmgGpuLevel& G : levels) {
     AmgLevelDev& d = G.dev;
     d.rr_agg = 0;
-    if (!on || G.dist || d.nc == 0 || d.n == 0 || d.n > max_rows || !d.r_row) continue;
+    if (max_rows == 0 || G.dist || d.nc == 0 || d.n == 0 || d.n > max_rows || !d.r_row) continue;
     std::vector<uint32_t> rr((size_t)d.nc + 1);
     CFD_HIP(hipMemcpyAsync(rr.data(), d.r_row, rr.size() * 4, hipMemcpyDeviceToHost, stream));
     sync();
@@ -1360,7 +1342,7 @@ void Solver::v_cycle() {
       sm(i, i > 0);  // coarse x was cleared by the restriction (ghosts too)
     AmgGpuLevel& C = levels[i + 1];
     // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
-    presmoothed = fuse_presmooth && (i + 1 < down) && (!Lv.dist || C.dist);
+    presmoothed = (i + 1 < down) && (!Lv.dist || C.dist);
     float* smo = presmoothed ? C.xt : nullptr;
     if (!Lv.dist && Lv.dev.rr_agg) {
       launch_amg_resrestrict(Lv.dev, Lv.x, Lv.b, C.b, C.x, smo, C.dev.de, stream);
@@ -1400,9 +1382,9 @@ void Solver::v_cycle() {
     launch_amg_tail_blob(d_tail, d_tail_desc, d_tail_blob, tail_blob_words, tail_vec_floats, tf, L, levels[tf].b,
                          levels[tf].dev.n, stream);
   } else if (tf < L) {
-    size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL_LDS=0 disables)
+    size_t lds = 0;  // LDS-resident tail when its vectors fit (CFD_AMG_TAIL=global: never)
     for (int l = tf; l < L; ++l) lds += 4 * (((size_t)levels[l].dev.n + 3) & ~(size_t)3) * sizeof(float);
-    if (lds > lds_budget || !tail_lds) lds = 0;
+    if (lds > lds_budget || tail_form == 0) lds = 0;
     launch_amg_tail(d_tail, tf, L, lds, stream);
   } else {
     for (int s = 0; s < 10; ++s) sm(L - 1, s == 0 && L > 1);
@@ -1458,31 +1440,27 @@ void Solver::precondition(int j, float* z) {
     const size_t raw = 20u + (size_t)std::sqrt((float)NG) / 2u;
     const size_t p_iters = std::min<size_t>(raw, 200) == 0 ? 0 : std::min<size_t>(raw, 200) - 1;
     // small meshes: every sweep in one single-workgroup launch (same bits)
-    if (!dist() && relax_fused &&
+    if (!dist() && small_forms &&
         launch_relax_pressure_fused(N, topo.ld, (uint32_t)topo.ws, d_scol, d_slen, sval, dinv_p, temp_p, p_sol, temp,
                                     (uint32_t)p_iters, stream)) {
       if (p_iters & 1) in_sol = false;
     } else {
+      AmgLevelDev rv{};  // the scalar ELL image (diagonal in the slots) as a row-kernel level
+      rv.n = N;
+      rv.r1 = N;
+      rv.stride = topo.ld;
+      rv.w = topo.ws;
+      rv.use16 = topo.use16 ? 1 : 0;
+      rv.full = 1;
+      rv.val = sval;
+      rv.col16 = d_scol16;
+      rv.col32 = d_scol;
+      rv.len = d_slen8;
       for (size_t it = 0; it < p_iters; ++it) {
         float* src = in_sol ? p_sol : temp;
         float* dst = in_sol ? temp : p_sol;
         if (dist()) halo(cell_plan, {{src, 1}});
-        if (relax4) {
-          AmgLevelDev rv{};  // the scalar ELL image (diagonal in the slots) as a row-kernel level
-          rv.n = N;
-          rv.r1 = N;
-          rv.stride = topo.ld;
-          rv.w = topo.ws;
-          rv.use16 = topo.use16 ? 1 : 0;
-          rv.full = 1;
-          rv.val = sval;
-          rv.col16 = d_scol16;
-          rv.col32 = d_scol;
-          rv.len = d_slen8;
-          launch_relax_pressure4(rv, d_sdrank8, dinv_p, temp_p, src, dst, stream);
-        } else {
-          launch_relax_pressure(N, topo.ld, d_scol, d_slen, sval, dinv_p, temp_p, src, dst, stream);
-        }
+        launch_relax_pressure4(rv, d_sdrank8, dinv_p, temp_p, src, dst, stream);
         in_sol = !in_sol;
       }
     }
@@ -1560,10 +1538,10 @@ void Solver::iteration(int j, float* pin) {
     A.r3 = b2;
     launch_spmv(A, zj, w, stream, nullptr, nt(8));
   });
-  const bool lat = cgs_lat && cgs_latency_form(N);
+  const bool lat = small_forms && cgs_latency_form(N);
   launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes, lat);
   const RedSrc dots = combine(partial, j + 1);
-  const bool fuse_reduce = cgs_fuse_reduce && cgs_reduce_fusable(dots);
+  const bool fuse_reduce = small_forms && cgs_reduce_fusable(dots);
   if (!fuse_reduce) launch_cgs_reduce(dots, j, H, m1, stream);
   // the whole restart basis and w within the kept bytes (small meshes): the
   // dots pass already reads every block with the default policy
@@ -1571,7 +1549,7 @@ void Solver::iteration(int j, float* pin) {
   // from the caches.  C0 21.2 -> 12.4 us per launch, -1.3 to -1.6 ms/step;
   // on C1's first iterations alone (the j + 2 vectors fitting) it lost
   // ≈ 0.1-0.2 ms/step, hence the whole-basis test (profiles/r05/ab_log.md).
-  const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes && !cgs_update_nt;
+  const bool basis_kept = (size_t)(m1 + 1) * 12u * N <= cgs_keep_bytes;
   launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0,
                          !basis_kept, fuse_reduce ? &dots : nullptr, lat);
   launch_norm_givens(combine(partial_n, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
@@ -1744,7 +1722,7 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
       }
     }
     launch_solve_triangular(H, g, y, basis_size, m1, stream);
-    launch_update_x(x, zvec, stride, y, basis_size, n, stream, cgs_lat);  // CFD_CGS_LAT=0: streaming form too
+    launch_update_x(x, zvec, stride, y, basis_size, n, stream, small_forms);  // 0: the streaming form
     check_launch("FGMRES solution update");
     if (converged) {  // async_reader.flush()
       flush_inner();
@@ -1889,8 +1867,7 @@ void Solver::step() {  // coupled_solver.rs:33-499
   if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) {
     // numeric re-setup over the kept structure when the device setup built it
     // (CFD_AMG_REFRESH=0: full rebuild; both give the same hierarchy)
-    const char* re = std::getenv("CFD_AMG_REFRESH");
-    if (amg_setup_path == 2 && !amg_refresh.empty() && !(re && re[0] == '0'))
+    if (amg_setup_path == 2 && !amg_refresh.empty() && knob_on(Knob::AmgRefresh))
       amg_refresh_pending = true;
     else
       drop_amg();
@@ -2175,7 +2152,7 @@ double Solver::layout_step_bytes() const {
       const double nc = levels[i + 1].dev.n;
       // pre-smoother (coarse: zero-x, elementwise; not launched when fused into
       // the previous level's restriction, whose 12 nc term counts it)
-      const bool presmoothed = i > 0 && fuse_presmooth && (!levels[i - 1].dist || levels[i].dist);
+      const bool presmoothed = i > 0 && (!levels[i - 1].dist || levels[i].dist);
       vc += (i == 0 ? smooth : (presmoothed ? 0.0 : 12 * n));
       if (d.rr_agg && !levels[i].dist)
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction

@@ -17,6 +17,7 @@
 #include "../hip/kernels.hpp"
 #include "comm.hpp"
 #include "dist.hpp"
+#include "tuning.hpp"
 
 namespace cfd2 {
 
@@ -128,8 +129,8 @@ struct Topology {
   // missing neighbours (walls) leave gaps instead of shifting the rest of the
   // row, and 4 consecutive rows keep 4 consecutive columns per slot.  Gaps and
   // trailing slots hold the virtual column row + tmode[r] (clamped into the
-  // vectors' range; never accumulated).  Position layout when ws > 8 or
-  // CFD_TYPED_ELL=0.
+  // vectors' range; never accumulated).  Position layout when ws > 8 (the
+  // Voronoi meshes).
   std::vector<int32_t> tmode;
   std::vector<uint8_t> tslot;    // [nnz] slot of CSR entry k
   std::vector<int32_t> tcol;     // [r*ld + i]
@@ -154,9 +155,10 @@ struct AmgHostLevel {
 };
 // local: partition-aware aggregation of the row-partitioned levels (those of
 // more than rep_rows rows from level 0 on; cfd_config.amg_local_aggregation)
+// timing: per-level SpGEMM times on stderr (cfg.log_level >= 2)
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
                                                const std::vector<uint64_t>& part = {}, bool local = false,
-                                               uint64_t rep_rows = 0);
+                                               uint64_t rep_rows = 0, bool timing = false);
 // Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
 // n rows; returns the aggregate count, agg[i] = aggregate of row i, and
 // cpart = the aggregate partition induced by the row partition `part` (an
@@ -204,10 +206,7 @@ struct AmgSetupLevel;  // amg_device.cpp
 // all-gather of its rhs cost less than the four un-overlapped halos per
 // V-cycle that keeping it row-partitioned costs (C4: level 4, 650 k rows).
 constexpr uint64_t kAmgReplicateRowsDefault = 1u << 20;
-inline uint64_t amg_replicate_rows() {
-  const char* ev = std::getenv("CFD_AMG_REPLICATE_ROWS");
-  return ev ? std::strtoull(ev, nullptr, 10) : kAmgReplicateRowsDefault;
-}
+inline uint64_t amg_replicate_rows() { return knob_u64(Knob::AmgReplicateRows, kAmgReplicateRowsDefault); }
 
 struct Solver {
   cfd_config cfg{};
@@ -311,15 +310,22 @@ struct Solver {
   bool amg_built = false;
   int amg_setup_path = 0;          // 0 not built, 1 host, 2 device (build_amg_device)
   int tail_first = 1;              // first AMG level handled by k_amg_tail
-  bool tail_lds = true;            // LDS-resident tail kernel when it fits
+  // tail kernel form (CFD_AMG_TAIL): 2 the LDS image of matrices + vectors
+  // (k_amg_tail_blob, starting up to tail_blob_shift levels lower to fit),
+  // 1 vectors in LDS (k_amg_tail_lds), 0 global memory (k_amg_tail); the
+  // weaker forms are also the fallbacks when the LDS does not hold the image
+  int tail_form = 2;
+  int tail_blob_shift = 2;
   // rows with more off-diagonals than this use the 16-bit layout (<= 255;
   // CFD_AMG_WIDE_LIMIT lowers it so that tests exercise the wide path)
   int amg_wide_limit = 255;
   size_t lds_budget = 0;           // dynamic LDS of the tail kernels on this device (init_kernel_attributes)
-  bool coupled_reg = true;         // regular coupled rows: derived columns (CFD_COUPLED_REG=0: always load)
-  bool relax4 = true;              // Jacobi sweeps: 4 rows per thread on the 16-bit scalar image (CFD_RELAX4=0: one row per thread)
-  bool relax_fused = true;         // Jacobi path: all sweeps in one launch on small meshes (CFD_RELAX_FUSED=0: off)
-  bool fuse_presmooth = true;      // coarse zero-x pre-smoother fused into the restriction
+  // small-mesh kernel forms (CFD_SMALL_MESH_FORMS=0: the large-mesh forms on
+  // every mesh): the CGS dots / update in their latency form (<= 2^17 cells,
+  // several basis vectors per load round trip), the CGS totals reduced inside
+  // the update kernel (<= 256 reduction units), every Jacobi relaxation sweep
+  // in one single-workgroup launch (<= 8191 cells)
+  bool small_forms = true;
   // nontemporal loads of the matrix streams (kernels.hip ldx), per kernel, for
   // the last readers of a matrix before the cycle moves on (CFD_NT, bit mask):
   // 1 post-smoother of the split levels, 2 level-0 AMG residual, 4 Schur
@@ -340,23 +346,13 @@ struct Solver {
   bool nt(unsigned bit) const { return (nt_mask & bit) != 0; }
   // CGS: bytes of the dots pass's last blocks read with the default policy
   // (kept in the Infinity Cache for the top-down update after it); 0: every
-  // basis read nontemporal, both passes bottom-up (CFD_CGS_KEEP_MB; default
-  // set in the constructor: 64 MB below 2^22 cells, else 0)
+  // basis read nontemporal, both passes bottom-up (set in the constructor:
+  // 64 MB below 2^22 cells, else 0)
   size_t cgs_keep_bytes = 0;
-  // CGS update: nontemporal basis loads / new-vector store even when the
-  // whole basis fits the kept bytes (CFD_CGS_UPDATE_NT=1; A/B)
-  bool cgs_update_nt = false;
-  // small meshes: the CGS totals reduced inside the update kernel
-  // (CFD_CGS_FUSE_REDUCE=0: k_cgs_reduce launched as on large meshes)
-  bool cgs_fuse_reduce = true;
-  // small meshes: the CGS dots / update in their latency form (several basis
-  // vectors per load round trip; CFD_CGS_LAT=0: the streaming form)
-  bool cgs_lat = true;
-  int fuse_prolong_from = 0;       // post-smoothers of levels >= this read x + P xc (no prolong launch) ...
-  uint64_t fuse_prolong_rows = 1ull << 20;  // ... when the level has at most this many rows
-  bool fused_prolong(int li) const {
-    return li >= fuse_prolong_from && !levels[li].dist && levels[li].dev.n <= fuse_prolong_rows;
-  }
+  // post-smoothers of single-GPU / replicated levels of at most this many
+  // rows read x + P xc (no prolongation launch; CFD_AMG_FUSED_PROLONG_ROWS)
+  uint64_t fuse_prolong_rows = 1ull << 20;
+  bool fused_prolong(int li) const { return !levels[li].dist && levels[li].dev.n <= fuse_prolong_rows; }
   AmgTailLevel* d_tail = nullptr;  // device copy of the level descriptors
   // k_amg_tail_blob: LDS image of the tail levels [tail_blob_first, L) (-1: none)
   int tail_blob_first = -1;
@@ -440,7 +436,7 @@ struct Solver {
   // being timed (prof) its launches in the graph are bracketed by event nodes
   // owned by the graph; every replay's times are harvested before the next
   // replay of that graph (graph_harvest) or when the profile is read.
-  // CFD_GRAPH=1 (or cfd_graph_enable) turns it on for one GPU (R = 1); off by
+  // cfd_graph_enable turns it on for one GPU (R = 1); off by
   // default: the same-box A/B found replay no faster than eager launches at
   // C0 and C1 -- the GPU's kernel boundaries, not the host's launch rate,
   // bound the small-mesh iteration.
@@ -517,7 +513,7 @@ struct Solver {
   void sync() { CFD_HIP(hipStreamSynchronize(stream)); }
  public:
   // Launch-error check: hipGetLastError after each phase of the step (a host
-  // call, no synchronisation); with CFD_CHECK_SYNC=1 the stream is also
+  // call, no synchronisation); with cfg.log_level >= 3 the stream is also
   // synchronised there, so an asynchronous kernel fault is reported at the
   // phase that caused it (debug runs).
   void check_launch(const char* where) {

@@ -139,8 +139,9 @@ void build_topology(const cfd_mesh_view& m, Topology& t, uint32_t c0, uint32_t c
   }
   // coupled-matrix ELL with aligned slots (Topology::tslot)
   {
-    const char* te = std::getenv("CFD_TYPED_ELL");
-    const bool typed = ws <= 8 && !(te && te[0] == '0');
+    // aligned slots up to 8 slots per row (the gap mask is 8 bits); wider
+    // meshes (the Voronoi meshes: up to 9 neighbours) keep the positional layout
+    const bool typed = ws <= 8;
     t.tmode.assign(ws, 0);
     if (typed) {
       const uint32_t step = N > (1u << 20) ? 7u : 1u;  // a sample is enough for a mode

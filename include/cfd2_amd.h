@@ -138,7 +138,9 @@ typedef struct cfd_config {
   float fgmres_atol;          /* 1e-7                                                   */
   int32_t log_level;          /* 0 silent; 1 the reference's println! progress lines
                                  (coupled_solver.rs, coupled_solver_fgmres.rs) on stderr,
-                                 rank 0 only                                             */
+                                 rank 0 only; 2 also AMG setup timings; 3 also a stream
+                                 synchronisation + error check after every kernel phase
+                                 (debug: a fault is reported where it happened)          */
   int32_t amg_rebuild_interval; /* 0: AMG hierarchy frozen after the first AMG solve
                                    (reference, amg.rs); k > 0: rebuilt from the current
                                    matrix every k steps (opt-in deviation) */

@@ -183,15 +183,15 @@ def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
     _three_way(mesh, nranks, cfg, setup, 2, f"overlapped {which}", oracle=(which != "c1"))
 
 
-@pytest.mark.parametrize("env", [{"CFD_HALO_PACK": "1"}, {"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"},
-                                 {"CFD_AMG_FUSED_PROLONG": "off"},
-                                 # every level split around its exchanges, but the restriction /
-                                 # prolongation of straddling aggregates all after them
-                                 {"CFD_OVERLAP_MIN_ROWS": "64", "CFD_AMG_HALO_OVERLAP": "0"}],
+@pytest.mark.parametrize("env", [{"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"},
+                                 {"CFD_AMG_FUSED_PROLONG_ROWS": "0"}, {"CFD_SMALL_MESH_FORMS": "0"},
+                                 # every level split around its exchanges
+                                 {"CFD_OVERLAP_MIN_ROWS": "64", "CFD_AMG_TAIL": "global"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_group_variants_parity(env, replicate_rows, monkeypatch):
-    """Distributed runs through the packed halo path and the alternative AMG
-    kernel paths: bit-exact."""
+    """Distributed runs through the alternative AMG kernel paths: bit-exact.
+    (The packed halo path -- non-contiguous send lists -- is the Voronoi
+    meshes' own: tests/test_voronoi.py test_voronoi_group_parity.)"""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     replicate_rows(50)

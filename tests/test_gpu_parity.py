@@ -501,22 +501,18 @@ def test_log_level_reference_lines(capfd):
 VARIANTS = [
     {"CFD_AMG_FULL": "0"},            # predicated slot loads (production: coarse levels > 2^19 rows)
     {"CFD_AMG_FULL": "1"},            # unconditional slot loads on every level
-    {"CFD_AMG_TAIL_BLOB": "0"},       # LDS tail with vectors only
-    {"CFD_AMG_TAIL_LDS": "0"},        # global-memory single-workgroup tail
+    {"CFD_AMG_TAIL": "lds"},          # LDS tail with vectors only (fallback when the image does not fit)
+    {"CFD_AMG_TAIL": "global"},       # global-memory single-workgroup tail (fallback when the vectors do not fit)
     {"CFD_AMG_TAIL_ROWS": "0"},       # no tail kernel: every level launched
-    {"CFD_AMG_FUSE_PRESMOOTH": "0"},  # coarse pre-smoother as its own sweep
-    {"CFD_COUPLED_REG": "0"},         # coupled-matrix kernels always load their columns
-    {"CFD_CGS_KEEP_MB": "1"},         # CGS dots' last blocks default-policy, update top-down
-    {"CFD_CGS_FUSE_REDUCE": "0"},     # k_cgs_reduce launched (production: meshes past 256 reduction units)
-    {"CFD_CGS_UPDATE_NT": "1"},       # nontemporal CGS update although the basis is cache-kept
-    {"CFD_CGS_LAT": "0"},             # CGS dots / update in the streaming form (production: > 131 k cells)
-    {"CFD_AMG_FUSED_RR": "0"},        # separate residual + restriction kernels on every level
+    {"CFD_SMALL_MESH_FORMS": "0"},    # streaming CGS dots / update / update_x, k_cgs_reduce launched,
+                                      # per-sweep Jacobi relaxation (production: > 131 k cells)
+    {"CFD_AMG_FUSED_RR_ROWS": "0"},   # separate residual + restriction kernels on every level
     {"CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused residual-restriction on every level, predicated loads
     {"CFD_AMG_FUSED_RR_ROWS": "4000000000"},          # fused residual-restriction on the big levels too
-    {"CFD_AMG_FUSED_PROLONG": "off"},                 # separate prolongation + post-smoother launches
-    {"CFD_AMG_FUSED_PROLONG": "0", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused, every level, predicated loads
-    {"CFD_NT": "63", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG": "off"},  # nontemporal loads everywhere
-    {"CFD_NT": "63", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR": "0"},             # ... with predicated slot loads
+    {"CFD_AMG_FUSED_PROLONG_ROWS": "0"},              # separate prolongation + post-smoother launches
+    {"CFD_AMG_FUSED_PROLONG_ROWS": "4000000000", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FULL": "0"},  # fused, every level
+    {"CFD_NT": "127", "CFD_AMG_TAIL_ROWS": "0", "CFD_AMG_FUSED_PROLONG_ROWS": "0"},  # nontemporal loads everywhere
+    {"CFD_NT": "127", "CFD_AMG_FULL": "0", "CFD_AMG_FUSED_RR_ROWS": "0"},            # ... with predicated slot loads
 ]
 
 
@@ -545,17 +541,18 @@ def test_amg_kernel_variants_parity(env, mesh_name, monkeypatch):
 
 @pytest.mark.parametrize("shift", ["0", "1", "4"])
 def test_amg_blob_shift_parity(shift, monkeypatch, capfd):
-    """CFD_AMG_BLOB_SHIFT: how many levels the LDS-image tail may start below
+    """CFD_AMG_TAIL=blob<K>: how many levels the LDS-image tail may start below
     the first tail level when that level's image does not fit one CU's LDS
-    (production: C1's 3.9 k-row level).  Forced here by a tail from level 1
-    (CFD_AMG_TAIL_ROWS) on a mesh whose level 1 is too large for the image:
-    shift 0 runs the vectors-only LDS tail, larger shifts the image tail from a
-    lower level -- GPU == oracle bit-exact either way."""
+    (production: C1's 3.9 k-row level; default K = 2).  Forced here by a tail
+    from level 1 (CFD_AMG_TAIL_ROWS) on a mesh whose level 1 is too large for
+    the image: K = 0 runs the vectors-only LDS tail, larger K the image tail
+    from a lower level -- GPU == oracle bit-exact either way.  The setup line
+    comes with cfg.log_level 2."""
     monkeypatch.setenv("CFD_AMG_TAIL_ROWS", "1000000")
-    monkeypatch.setenv("CFD_AMG_BLOB_SHIFT", shift)
-    monkeypatch.setenv("CFD_AMG_SETUP_TIMING", "1")
+    monkeypatch.setenv("CFD_AMG_TAIL", "blob" + shift)
     mesh = channel_obstacle(h=0.012)
-    g, o = _pair(mesh, fixed_outer=2, fixed_inner=8)
+    g = GpuSolver(mesh, config=default_config(fixed_outer=2, fixed_inner=8, log_level=2))
+    o = OracleSolver(mesh, config=default_config(fixed_outer=2, fixed_inner=8))
     for s in (g, o):
         _setup_amg_test(s, mesh, 1)
     capfd.readouterr()

@@ -62,14 +62,11 @@ def test_relax_fused_parity(name, rpt, wmax, monkeypatch):
         assert n > 8191, n
     cfg = dict(fixed_outer=3, fixed_inner=12)
     fused = GpuSolver(mesh, config=default_config(**cfg))
-    monkeypatch.setenv("CFD_RELAX_FUSED", "0")
+    monkeypatch.setenv("CFD_SMALL_MESH_FORMS", "0")  # one launch per sweep, as on large meshes
     per_sweep4 = GpuSolver(mesh, config=default_config(**cfg))
-    monkeypatch.setenv("CFD_RELAX4", "0")
-    per_sweep1 = GpuSolver(mesh, config=default_config(**cfg))
-    monkeypatch.delenv("CFD_RELAX_FUSED")
-    monkeypatch.delenv("CFD_RELAX4")
+    monkeypatch.delenv("CFD_SMALL_MESH_FORMS")
     o = OracleSolver(mesh, config=default_config(**cfg))
-    gpus = {"fused": fused, "per-sweep 4-row": per_sweep4, "per-sweep 1-row": per_sweep1}
+    gpus = {"fused": fused, "per-sweep 4-row": per_sweep4}
     for s in (*gpus.values(), o):
         _setup_amg_test(s, mesh, 0)
     for k in range(2):

@@ -55,14 +55,14 @@ def test_nan_state_diverges_like_reference(precond, at_step):
     assert ("linear residual" in mg) == ("linear residual" in mo)
 
 
-@pytest.mark.parametrize("tail_lds", ["1", "0"])
-def test_wide_amg_rows_take_the_16bit_path_bitexact(monkeypatch, tail_lds):
+@pytest.mark.parametrize("tail", ["blob2", "global"])
+def test_wide_amg_rows_take_the_16bit_path_bitexact(monkeypatch, tail):
     """Coarse levels wider than the (lowered) layout limit: host setup path,
     16-bit row lengths, the whole coarse cycle in the tail kernel (LDS-resident
     or global-memory); fields and step statistics bit-exact vs the oracle."""
     mesh = backwards_step()
     monkeypatch.setenv("CFD_AMG_WIDE_LIMIT", "5")  # level 0: 4, coarse levels: 6
-    monkeypatch.setenv("CFD_AMG_TAIL_LDS", tail_lds)
+    monkeypatch.setenv("CFD_AMG_TAIL", tail)
     g = GpuSolver(mesh, config=default_config())
     o = OracleSolver(mesh, config=default_config())
     for s in (g, o):
@@ -81,14 +81,12 @@ def test_wide_amg_rows_take_the_16bit_path_bitexact(monkeypatch, tail_lds):
     assert g2.amg_setup_info()[0] == 2, "without wide rows the device setup runs"
 
 
-@pytest.mark.parametrize("typed", ["1", "0"])
-def test_aligned_slot_ell_bitexact(monkeypatch, typed):
+def test_aligned_slot_ell_bitexact():
     """Coupled-matrix ELL with aligned slots (gaps where a wall removes a
-    neighbour; Topology::tslot) and the plain positional layout
-    (CFD_TYPED_ELL=0): both give the oracle's bits (amg_test setup, Jacobi and
-    AMG preconditioners)."""
+    neighbour; Topology::tslot) on a quad mesh: the oracle's bits (amg_test
+    setup, Jacobi and AMG preconditioners).  The positional layout of wider
+    meshes (ws > 8) is the Voronoi meshes' own (tests/test_voronoi.py)."""
     mesh = backwards_step()
-    monkeypatch.setenv("CFD_TYPED_ELL", typed)
     for precond in (0, 1):
         g = GpuSolver(mesh, config=default_config())
         o = OracleSolver(mesh, config=default_config())
@@ -97,6 +95,6 @@ def test_aligned_slot_ell_bitexact(monkeypatch, typed):
         for k in range(3):
             g.step()
             o.step()
-            _assert_same_fields(g, o, f"typed={typed} precond={precond} step {k}")
-            _assert_same_info(g, o, f"typed={typed} precond={precond} step {k}")
+            _assert_same_fields(g, o, f"precond={precond} step {k}")
+            _assert_same_info(g, o, f"precond={precond} step {k}")
         g.close()
