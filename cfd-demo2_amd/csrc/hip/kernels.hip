@@ -2259,6 +2259,144 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
     cx[I] = 0.0f;
 }
 
+// The down-leg of two adjacent single-GPU / replicated levels (i, i+1) in one
+// launch (AmgPairImage, kernels.hpp): the two k_amg_resrestrict launches'
+// arithmetic, operation for operation.  Phase 1: one level-i member residual
+// per thread (k_amg_resrestrict's loop) into LDS; phase 2: every S row's rhs
+// (0 + r_1 + r_2 ... in R order) and its zero-x pre-smoother
+// mix(0, (b - 0) / de, 0.8), the block's own rows stored; phase 3: the level-
+// (i+1) residual of the block's rows from the LDS values (diagonal at its rank
+// among the off-diagonals, as k_amg_resrestrict); phase 4: the level-(i+2)
+// rhs per aggregate and its pre-smoother (or x = 0).  The level-(i+1) slots,
+// row headers and the aggregate ranges are loaded before phase 1, so the
+// second level costs LDS round trips only; the ring rows' level-i residuals
+// are the redundant work (amg_fusion_ratio.py).
+template <bool D16>
+__global__ void __launch_bounds__(kPairThreads) k_amg_resrestrict_pair(AmgLevelDev Lf, AmgLevelDev Lm,
+                                                                     AmgPairImage P, const float* __restrict__ x,
+                                                                     const float* __restrict__ b,
+                                                                     float* __restrict__ bm, float* __restrict__ xm,
+                                                                     float* __restrict__ cb, float* __restrict__ cx,
+                                                                     float* __restrict__ sm_out,
+                                                                     const float* __restrict__ sm_de) {
+  __shared__ float rl[kPairThreads];  // level-i residuals of the block's f rows
+  __shared__ float bs[kPairThreads];  // level-(i+1) rhs of the block's s rows
+  __shared__ float xs[kPairThreads];  // their pre-smoothed x
+  __shared__ float r2[kPairThreads];  // level-(i+1) residuals of the block's own rows
+  const uint32_t blk = xcd_block<kRevResidual>();
+  if (blk >= P.nblocks) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t s0 = P.sb[blk], s1 = P.sb[blk + 1];
+  const uint32_t J0 = P.jb[blk], J1 = P.jb[blk + 1];
+  const uint32_t m0 = Lm.r_row[J0], nm = Lm.r_row[J1] - m0;
+  const uint32_t fb = P.fo[s0], fe = P.fo[s1];
+  // phase-2 / phase-3 / phase-4 operands, independent of phase 1
+  uint32_t sr = 0, k0 = 0, k1 = 0, mlen = 0, mdr = 0, a0 = 0, a1 = 0;
+  float des = 1.0f, mdv = 0.0f, dec = 1.0f;
+  float mv[kPairW];
+  uint32_t mc[kPairW];
+  if (s0 + t < s1) {
+    sr = P.s[s0 + t];
+    k0 = P.fo[s0 + t];
+    k1 = P.fo[s0 + t + 1];
+    des = Lm.de[sr];
+  }
+  if (t < nm) {
+    mlen = Lm.len[sr];
+    mdr = Lm.drank[sr];
+    mdv = Lm.dv[sr];
+    const uint32_t wm = (uint32_t)max(Lm.w, 1);
+#pragma unroll
+    for (int r = 0; r < kPairW; ++r) {
+      const size_t off = (size_t)min((uint32_t)r, wm - 1u) * Lm.stride + sr;
+      mv[r] = Lm.val[off];
+      mc[r] = P.lc[off];
+    }
+  }
+  if (J0 + t < J1) {
+    a0 = Lm.r_row[J0 + t];
+    a1 = Lm.r_row[J0 + t + 1];
+    if (sm_out) dec = sm_de[J0 + t];
+  }
+  // phase 1: level-i residuals (k_amg_resrestrict's row loop)
+  const uint32_t w = (uint32_t)max(Lf.w, 1);
+  for (uint32_t p = fb + t; p < fe; p += kPairThreads) {
+    const uint32_t f = P.f[p];
+    const uint32_t len = Lf.len[f], dr = Lf.drank[f];
+    const float xf = x[f], dvf = Lf.dv[f];
+    float ax = 0.0f;
+    uint32_t r0 = 0;
+    for (; r0 < len; r0 += 4) {
+      float v[4], xg[4];
+      int c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t off = (size_t)min(r0 + u, w - 1u) * Lf.stride + f;
+        v[u] = Lf.val[off];
+        c[u] = D16 ? (int)f + (int)Lf.col16[off] : Lf.col32[off];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xg[u] = x[c[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t r = r0 + u;
+        if (r == dr) ax += dvf * xf;
+        if (r < len) ax += v[u] * xg[u];
+      }
+    }
+    if (dr >= r0) ax += dvf * xf;
+    rl[p - fb] = b[f] - ax;
+  }
+  __syncthreads();
+  // phase 2: level-(i+1) rhs (restriction) and zero-x pre-smoother of every s row
+  if (s0 + t < s1) {
+    float sum = 0.0f;
+    for (uint32_t k = k0; k < k1; ++k) sum += 1.0f * rl[k - fb];
+    const float xv = wmix(0.0f, (sum - 0.0f) / des, 0.8f);
+    bs[t] = sum;
+    xs[t] = xv;
+    if (t < nm) {  // the block's own rows (every level-(i+1) row is one block's)
+      bm[sr] = sum;
+      xm[sr] = xv;
+    }
+  }
+  __syncthreads();
+  // phase 3: level-(i+1) residual of the block's rows
+  if (t < nm) {
+    const float xf = xs[t];
+    float ax = 0.0f;
+    uint32_t r = 0;
+    for (; r < mlen; ++r) {
+      float v;
+      uint32_t c;
+      if (r < (uint32_t)kPairW) {
+        v = mv[r];
+        c = mc[r];
+      } else {
+        const size_t off = (size_t)r * Lm.stride + sr;
+        v = Lm.val[off];
+        c = P.lc[off];
+      }
+      if (r == mdr) ax += mdv * xf;
+      ax += v * xs[c];
+    }
+    if (mdr >= r) ax += mdv * xf;  // a diagonal ranked after every off-diagonal comes last
+    r2[t] = bs[t] - ax;
+  }
+  __syncthreads();
+  // phase 4: level-(i+2) rhs (restriction) and its pre-smoother / cleared x
+  if (J0 + t < J1) {
+    const uint32_t J = J0 + t;
+    float sum = 0.0f;
+    for (uint32_t k = a0; k < a1; ++k) sum += 1.0f * r2[k - m0];
+    cb[J] = sum;
+    if (sm_out)
+      sm_out[J] = wmix(0.0f, (sum - 0.0f) / dec, 0.8f);
+    else
+      cx[J] = 0.0f;
+  }
+}
+
 // prolongate_op (amg.wgsl:56-75): x += (0 + 1 * xc[agg]), 4 rows per thread.
 // agg is a signed local index on a distributed level (aggregates seeded on a
 // lower rank are ghosts of xc below 0).
@@ -2944,6 +3082,17 @@ void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b
     hipLaunchKernelGGL(k_amg_resrestrict<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
   else
     hipLaunchKernelGGL(k_amg_resrestrict<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
+}
+void launch_amg_resrestrict_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lm, const AmgPairImage& P,
+                                 const float* x, const float* b, float* bm, float* xm, float* cb, float* cx,
+                                 float* sm_out, const float* sm_de, hipStream_t s) {
+  if (!P.nblocks) return;
+  if (Lf.use16)
+    hipLaunchKernelGGL(k_amg_resrestrict_pair<true>, dim3(P.nblocks), dim3(kPairThreads), 0, s, Lf, Lm, P, x, b, bm, xm,
+                       cb, cx, sm_out, sm_de);
+  else
+    hipLaunchKernelGGL(k_amg_resrestrict_pair<false>, dim3(P.nblocks), dim3(kPairThreads), 0, s, Lf, Lm, P, x, b, bm,
+                       xm, cb, cx, sm_out, sm_de);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1, bool nt) {
   if (f1 == 0) f1 = L.n;

@@ -233,6 +233,25 @@ struct AmgLevelDev {
   uint32_t rr_agg;
 };
 constexpr uint32_t kRRCap = 2048;  // residuals per block of k_amg_resrestrict (LDS floats)
+
+// k_amg_resrestrict_pair: the down-leg of two adjacent single-GPU / replicated
+// levels (i, i+1) in one launch.  A block owns level-(i+2) aggregates
+// [jb[k], jb[k+1]); its level-(i+1) rows S = the members of those aggregates
+// (R order, written by the block) then their off-diagonal columns outside
+// them (the ring, recomputed redundantly); f lists the level-i members of every
+// S row (R order).  Built at AMG setup (Solver::build_rr_pairs) so that every
+// block's S, f and aggregates fit kPairThreads.
+constexpr uint32_t kPairThreads = 1024;
+constexpr int kPairW = 8;  // level-(i+1) slots prefetched before the level-i phase
+struct AmgPairImage {
+  uint32_t nblocks;
+  const uint32_t* jb;  // [nblocks + 1] level-(i+2) aggregate ranges
+  const uint32_t* sb;  // [nblocks + 1] ranges in s
+  const uint32_t* s;   // level-(i+1) rows: each block's members first, then its ring
+  const uint32_t* fo;  // [|s| + 1] ranges in f of each s row's level-i members
+  const uint32_t* f;   // level-i rows
+  const uint16_t* lc;  // [r * stride_{i+1} + row] block-local index (in s) of slot r's column
+};
 // zeroed entries after every level's agg array: the fused prolongation reads
 // agg with 16-byte loads from any column (as the x gathers, whose vectors
 // carry the same slack)
@@ -380,6 +399,13 @@ void launch_amg_tail_blob(const AmgTailLevel* tail, const TailBlobLevel* desc, c
 // coarse zero-x pre-smoother written to sm_out (as launch_amg_restrict)
 void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b, float* coarse_b, float* coarse_x,
                             float* sm_out, const float* sm_de, hipStream_t s);
+// levels i (Lf: x, b) and i+1 (Lm) down-leg in one launch: writes level
+// i+1's rhs bm and pre-smoothed x xm (as k_amg_resrestrict with sm_out), then
+// level i+2's rhs cb and either its pre-smoothed x (sm_out, diagonal sm_de)
+// or cx = 0 -- the bits of the two k_amg_resrestrict launches
+void launch_amg_resrestrict_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lm, const AmgPairImage& P,
+                                 const float* x, const float* b, float* bm, float* xm, float* cb, float* cx,
+                                 float* sm_out, const float* sm_de, hipStream_t s);
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* coarse_x, hipStream_t s, uint32_t f0 = 0,
                         uint32_t f1 = 0, bool nt = false);
 // Sets the tail kernels' dynamic-LDS attribute on `device` (once per device,

@@ -1060,13 +1060,20 @@ void Solver::ensure_amg() {
       if (tail_blob_first >= 0) tail_first = t;
     }
   }
+  build_rr_pairs();
   sync();
   amg_built = true;
   if (!from_checkpoint) amg_age = 0;
-  if (timing)
-    std::fprintf(stderr, "[amg setup] %s path: %d levels in %.3f s, tail from level %d (LDS image from level %d)\n",
+  if (timing) {
+    std::string pairs;
+    for (int li = 0; li < (int)rr_pair.size(); ++li)
+      if (rr_pair[li].nblocks) pairs += " " + std::to_string(li) + "+" + std::to_string(li + 1);
+    std::fprintf(stderr,
+                 "[amg setup] %s path: %d levels in %.3f s, tail from level %d (LDS image from level %d), "
+                 "down-leg pairs:%s\n",
                  how, L, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
-                 tail_first, tail_blob_first);
+                 tail_first, tail_blob_first, pairs.empty() ? " none" : pairs.c_str());
+  }
 }
 
 // Aggregates per block of k_amg_resrestrict for the single-GPU / replicated
@@ -1095,6 +1102,136 @@ void Solver::set_resrestrict_blocks() {
     }
     d.rr_agg = a;
   }
+}
+
+// Down-leg pairs (k_amg_resrestrict_pair): greedily from the top, two
+// adjacent levels that both take k_amg_resrestrict and whose second level is
+// pre-smoothed inside the V-cycle's down loop run as one launch.
+void Solver::build_rr_pairs() {
+  const int L = (int)levels.size();
+  rr_pair.assign(L, AmgPairImage{});
+  if (!knob_on(Knob::AmgFusedPair)) return;
+  const int D = dist() ? amg_g : 0;
+  const int down = std::min(std::max({tail_first, 1, D}), L - 1);
+  for (int i = 0; i + 1 < down;) {
+    const AmgGpuLevel &F = levels[i], &M = levels[i + 1];
+    const bool ok = !F.dist && !M.dist && !F.wide && !M.wide && F.dev.rr_agg && M.dev.rr_agg && M.dev.w >= 1;
+    i += (ok && build_rr_pair(i)) ? 2 : 1;
+  }
+}
+
+// The pair image of levels (i, i+1): blocks of level-(i+2) aggregates whose
+// level-(i+1) rows (members + ring: S) and level-i members of S each fit
+// kPairThreads.  False (no pair) when one aggregate alone does not fit.
+bool Solver::build_rr_pair(int i) {
+  const AmgLevelDev &F = levels[i].dev, &M = levels[i + 1].dev;
+  const uint32_t nm = M.n, nc = M.nc;
+  auto down_u32 = [&](const uint32_t* d, size_t n) {
+    std::vector<uint32_t> h(n);
+    CFD_HIP(hipMemcpyAsync(h.data(), d, n * 4, hipMemcpyDeviceToHost, stream));
+    return h;
+  };
+  const std::vector<uint32_t> fr_row = down_u32(F.r_row, (size_t)F.nc + 1), fr_col = down_u32(F.r_col, F.n);
+  const std::vector<uint32_t> mr_row = down_u32(M.r_row, (size_t)nc + 1), mr_col = down_u32(M.r_col, nm);
+  std::vector<uint8_t> mlen(nm);
+  CFD_HIP(hipMemcpyAsync(mlen.data(), M.len, nm, hipMemcpyDeviceToHost, stream));
+  const size_t slots = (size_t)M.w * M.stride;
+  std::vector<int32_t> mcol(slots);
+  if (M.use16) {
+    std::vector<int16_t> c16(slots);
+    CFD_HIP(hipMemcpyAsync(c16.data(), M.col16, slots * 2, hipMemcpyDeviceToHost, stream));
+    sync();
+    for (size_t k = 0; k < slots; ++k) mcol[k] = (int32_t)(k % M.stride) + c16[k];
+  } else {
+    CFD_HIP(hipMemcpyAsync(mcol.data(), M.col32, slots * 4, hipMemcpyDeviceToHost, stream));
+    sync();
+  }
+  if (F.nc != nm) return false;
+  auto nfine = [&](uint32_t g) { return fr_row[g + 1] - fr_row[g]; };
+  auto col = [&](uint32_t g, uint32_t r) { return (uint32_t)mcol[(size_t)r * M.stride + g]; };
+  // greedy partition of the aggregates; stamp[g] = block that holds row g in S
+  std::vector<int32_t> stamp(nm, -1);
+  std::vector<uint32_t> jb{0};
+  uint32_t nS = 0, nF = 0, nJ = 0;
+  int blk = 0;
+  std::vector<uint32_t> added;
+  for (uint32_t J = 0; J < nc;) {
+    added.clear();
+    uint32_t dS = 0, dF = 0;
+    auto take = [&](uint32_t g) {
+      if (stamp[g] == blk) return;
+      stamp[g] = blk;
+      added.push_back(g);
+      ++dS;
+      dF += nfine(g);
+    };
+    for (uint32_t k = mr_row[J]; k < mr_row[J + 1]; ++k) {
+      const uint32_t g = mr_col[k];
+      take(g);
+      for (uint32_t r = 0; r < mlen[g]; ++r) take(col(g, r));
+    }
+    if (nS + dS <= kPairThreads && nF + dF <= kPairThreads && nJ + 1 <= kPairThreads) {
+      nS += dS;
+      nF += dF;
+      ++nJ;
+      ++J;
+      continue;
+    }
+    for (uint32_t g : added) stamp[g] = -1;  // J opens the next block
+    if (nJ == 0) return false;               // one aggregate alone does not fit
+    jb.push_back(J);
+    ++blk;
+    nS = nF = nJ = 0;
+  }
+  if (nJ) jb.push_back(nc);
+  const uint32_t nb = (uint32_t)jb.size() - 1;
+  // per block: S = members (R order) then the ring (ascending); f, local columns
+  std::vector<uint32_t> sb{0}, sv, fo{0}, fv;
+  std::vector<uint16_t> lc(slots, 0);
+  std::vector<int32_t> loc(nm, -1);
+  std::vector<uint32_t> ring;
+  for (uint32_t k = 0; k < nb; ++k) {
+    const uint32_t base = (uint32_t)sv.size();
+    for (uint32_t q = mr_row[jb[k]]; q < mr_row[jb[k + 1]]; ++q) {
+      loc[mr_col[q]] = (int32_t)(sv.size() - base);
+      sv.push_back(mr_col[q]);
+    }
+    const size_t own_end = sv.size();
+    ring.clear();
+    for (size_t q = base; q < own_end; ++q)
+      for (uint32_t r = 0; r < mlen[sv[q]]; ++r) {
+        const uint32_t c = col(sv[q], r);
+        if (loc[c] < 0) {
+          loc[c] = -2;  // queued
+          ring.push_back(c);
+        }
+      }
+    std::sort(ring.begin(), ring.end());
+    for (uint32_t c : ring) {
+      loc[c] = (int32_t)(sv.size() - base);
+      sv.push_back(c);
+    }
+    for (size_t q = base; q < own_end; ++q)
+      for (uint32_t r = 0; r < mlen[sv[q]]; ++r) lc[(size_t)r * M.stride + sv[q]] = (uint16_t)loc[col(sv[q], r)];
+    for (size_t q = base; q < sv.size(); ++q) {
+      for (uint32_t e = fr_row[sv[q]]; e < fr_row[sv[q] + 1]; ++e) fv.push_back(fr_col[e]);
+      fo.push_back((uint32_t)fv.size());
+    }
+    for (size_t q = base; q < sv.size(); ++q) loc[sv[q]] = -1;
+    if (sv.size() - base > kPairThreads || fo.back() - fo[base] > kPairThreads)
+      throw std::logic_error("AMG pair image: block over capacity");
+    sb.push_back((uint32_t)sv.size());
+  }
+  AmgPairImage& P = rr_pair[i];
+  P.nblocks = nb;
+  P.jb = arena.upload(jb, stream);
+  P.sb = arena.upload(sb, stream);
+  P.s = arena.upload(sv, stream);
+  P.fo = arena.upload(fo, stream);
+  P.f = arena.upload(fv, stream);
+  P.lc = arena.upload(lc, stream);
+  sync();
+  return true;
 }
 
 // LDS image of the tail levels [tf, L) for k_amg_tail_blob: every array the
@@ -1344,6 +1481,18 @@ void Solver::v_cycle() {
     // the next level is pre-smoothed by this loop: fuse its zero-x sweep into the restriction
     presmoothed = (i + 1 < down) && (!Lv.dist || C.dist);
     float* smo = presmoothed ? C.xt : nullptr;
+    if (presmoothed && (size_t)i < rr_pair.size() && rr_pair[i].nblocks && i + 2 <= down) {
+      // levels i and i + 1 in one launch; level i + 1 ends pre-smoothed (as
+      // the next iteration's swap leaves it) and level i + 2 gets its rhs
+      AmgGpuLevel& C2 = levels[i + 2];
+      const bool pre2 = i + 2 < down;  // both replicated / single-GPU: as `presmoothed` below
+      launch_amg_resrestrict_pair(Lv.dev, C.dev, rr_pair[i], Lv.x, Lv.b, C.b, C.xt, C2.b, C2.x,
+                                  pre2 ? C2.xt : nullptr, C2.dev.de, stream);
+      std::swap(C.x, C.xt);
+      presmoothed = pre2;
+      ++i;  // level i + 1 is done
+      continue;
+    }
     if (!Lv.dist && Lv.dev.rr_agg) {
       launch_amg_resrestrict(Lv.dev, Lv.x, Lv.b, C.b, C.x, smo, C.dev.de, stream);
     } else if (!Lv.dist) {
@@ -2156,6 +2305,8 @@ double Solver::layout_step_bytes() const {
       vc += (i == 0 ? smooth : (presmoothed ? 0.0 : 12 * n));
       if (d.rr_agg && !levels[i].dist)
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
+      if (i > 0 && (size_t)i <= rr_pair.size() && rr_pair[i - 1].nblocks)
+        vc -= 8 * n;  // second level of a k_amg_resrestrict_pair: its b and x stay in LDS
       else
         vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
       if (fused_prolong(i))

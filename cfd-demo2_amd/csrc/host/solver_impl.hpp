@@ -361,6 +361,12 @@ struct Solver {
   uint32_t tail_blob_words = 0, tail_vec_floats = 0;
   void build_tail_blob(int tf, bool reuse = false);  // reuse: rewrite the existing blob in place
   void set_resrestrict_blocks();
+  // down-leg pairs (k_amg_resrestrict_pair): rr_pair[i].nblocks > 0 when levels
+  // i and i+1 run as one launch (single-GPU / replicated levels that both take
+  // k_amg_resrestrict, level i+1 pre-smoothed)
+  std::vector<AmgPairImage> rr_pair;
+  void build_rr_pairs();
+  bool build_rr_pair(int i);
   std::vector<AmgGpuLevel> levels;
   // the scalar matrix (ELL image, like sval) the hierarchy was built from:
   // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)

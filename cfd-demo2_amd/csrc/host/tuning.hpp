@@ -27,6 +27,7 @@ enum class Knob : int {
   AmgFusedRrRows,      // CFD_AMG_FUSED_RR_ROWS
   AmgWideLimit,        // CFD_AMG_WIDE_LIMIT
   SmallMeshForms,      // CFD_SMALL_MESH_FORMS
+  AmgFusedPair,        // CFD_AMG_FUSED_PAIR
   Count
 };
 

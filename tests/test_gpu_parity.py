@@ -642,3 +642,39 @@ def test_fixed_schedule_early_exits(inlet):
         o.step()
         _assert_same_fields(g, o, f"inlet={inlet} step {k}")
         _assert_same_info(g, o, f"inlet={inlet} step {k}")
+
+
+@pytest.mark.parametrize("mesh_name", ["amg_test", "graded", "channel_012"])
+@pytest.mark.parametrize("pair", ["1", "0"])
+def test_amg_resrestrict_pair_parity(mesh_name, pair, monkeypatch, capfd):
+    """k_amg_resrestrict_pair: two adjacent down-leg levels in one launch
+    (CFD_AMG_FUSED_PAIR; production: C1's levels 2+3 and 4+5).  With the tail
+    off every level pair of these meshes is a candidate; GPU == oracle
+    bit-exact with the pairs on and off, and the setup line names the pairs."""
+    monkeypatch.setenv("CFD_AMG_TAIL_ROWS", "0")
+    monkeypatch.setenv("CFD_AMG_FUSED_PAIR", pair)
+    if mesh_name == "amg_test":
+        mesh = backwards_step()
+    elif mesh_name == "graded":
+        from cfd2_amd.mesh import ChannelWithObstacle, generate_cut_cell_mesh
+        geo = ChannelWithObstacle(length=3.0, height=1.0, obstacle_center=(1.0, 0.5), obstacle_radius=0.15)
+        mesh = generate_cut_cell_mesh(geo, 0.02, 0.08, 1.2, (3.0, 1.0))
+    else:
+        mesh = channel_obstacle(h=0.012)
+    cfg = dict(fixed_outer=2, fixed_inner=8)
+    g = GpuSolver(mesh, config=default_config(log_level=2, **cfg))
+    o = OracleSolver(mesh, config=default_config(**cfg))
+    for s in (g, o):
+        _setup_amg_test(s, mesh, 1)
+    capfd.readouterr()
+    for k in range(2):
+        g.step()
+        o.step()
+        _assert_same_fields(g, o, f"pair={pair} {mesh_name} step {k}")
+        _assert_same_info(g, o, f"pair={pair} {mesh_name} step {k}")
+    import re
+    m = re.search(r"down-leg pairs:(.*)\n", capfd.readouterr().err)
+    assert m, "no AMG setup line"
+    pairs = [] if m.group(1).strip() == "none" else m.group(1).split()
+    assert (len(pairs) > 0) == (pair == "1"), pairs
+    g.close()
