@@ -195,3 +195,93 @@ std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_le
 }
 
 }  // namespace cfd2
+
+namespace cfd2 {
+
+bool build_pair_partition(const std::vector<uint32_t>& fr_row, const std::vector<uint32_t>& fr_col,
+                          const std::vector<uint32_t>& mr_row, const std::vector<uint32_t>& mr_col,
+                          const std::vector<uint32_t>& mrow, const std::vector<uint32_t>& mcol, uint32_t cap,
+                          PairPartition& out) {
+  const uint32_t nm = (uint32_t)mrow.size() - 1, nc = (uint32_t)mr_row.size() - 1;
+  if (fr_row.size() != (size_t)nm + 1 || mr_col.size() != nm) return false;
+  auto nfine = [&](uint32_t g) { return fr_row[g + 1] - fr_row[g]; };
+  out = PairPartition{};
+  out.jb.push_back(0);
+  // greedy: stamp[g] = block whose S holds row g
+  std::vector<int32_t> stamp(nm, -1);
+  std::vector<uint32_t> added;
+  uint32_t nS = 0, nF = 0, nJ = 0;
+  int32_t blk = 0;
+  for (uint32_t J = 0; J < nc;) {
+    added.clear();
+    uint32_t dS = 0, dF = 0;
+    auto take = [&](uint32_t g) {
+      if (stamp[g] == blk) return;
+      stamp[g] = blk;
+      added.push_back(g);
+      ++dS;
+      dF += nfine(g);
+    };
+    for (uint32_t k = mr_row[J]; k < mr_row[J + 1]; ++k) {
+      const uint32_t g = mr_col[k];
+      take(g);
+      for (uint32_t e = mrow[g]; e < mrow[g + 1]; ++e) take(mcol[e]);
+    }
+    if (nS + dS <= cap && nF + dF <= cap && nJ + 1 <= cap) {
+      nS += dS;
+      nF += dF;
+      ++nJ;
+      ++J;
+      continue;
+    }
+    for (uint32_t g : added) stamp[g] = -1;  // J opens the next block
+    if (nJ == 0) return false;               // one aggregate alone does not fit
+    out.jb.push_back(J);
+    ++blk;
+    nS = nF = nJ = 0;
+  }
+  if (nJ) out.jb.push_back(nc);
+  const uint32_t nb = (uint32_t)out.jb.size() - 1;
+  out.sb.assign(1, 0);
+  out.fo.assign(1, 0);
+  out.s.clear();
+  out.f.clear();
+  out.lc.assign(mcol.size(), 0);
+  std::vector<int32_t> loc(nm, -1);
+  std::vector<uint32_t> ring;
+  for (uint32_t k = 0; k < nb; ++k) {
+    const size_t base = out.s.size();
+    for (uint32_t q = mr_row[out.jb[k]]; q < mr_row[out.jb[k + 1]]; ++q) {
+      loc[mr_col[q]] = (int32_t)(out.s.size() - base);
+      out.s.push_back(mr_col[q]);
+    }
+    const size_t own_end = out.s.size();
+    ring.clear();
+    for (size_t q = base; q < own_end; ++q)
+      for (uint32_t e = mrow[out.s[q]]; e < mrow[out.s[q] + 1]; ++e)
+        if (loc[mcol[e]] == -1) {
+          loc[mcol[e]] = -2;  // queued
+          ring.push_back(mcol[e]);
+        }
+    std::sort(ring.begin(), ring.end());
+    for (uint32_t c : ring) {
+      loc[c] = (int32_t)(out.s.size() - base);
+      out.s.push_back(c);
+    }
+    for (size_t q = base; q < own_end; ++q)
+      for (uint32_t e = mrow[out.s[q]]; e < mrow[out.s[q] + 1]; ++e) out.lc[e] = (uint16_t)loc[mcol[e]];
+    for (size_t q = base; q < out.s.size(); ++q) {
+      for (uint32_t e = fr_row[out.s[q]]; e < fr_row[out.s[q] + 1]; ++e) out.f.push_back(fr_col[e]);
+      out.fo.push_back((uint32_t)out.f.size());
+    }
+    for (size_t q = base; q < out.s.size(); ++q) loc[out.s[q]] = -1;
+    if (out.s.size() - base > cap || out.fo.back() - out.fo[base] > cap)
+      throw std::logic_error("AMG pair partition: block " + std::to_string(k) + " over capacity (S " +
+                             std::to_string(out.s.size() - base) + ", f " +
+                             std::to_string(out.fo.back() - out.fo[base]) + ", cap " + std::to_string(cap) + ")");
+    out.sb.push_back((uint32_t)out.s.size());
+  }
+  return true;
+}
+
+}  // namespace cfd2

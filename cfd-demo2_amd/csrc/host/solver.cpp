@@ -1147,81 +1147,19 @@ bool Solver::build_rr_pair(int i) {
     sync();
   }
   if (F.nc != nm) return false;
-  auto nfine = [&](uint32_t g) { return fr_row[g + 1] - fr_row[g]; };
-  auto col = [&](uint32_t g, uint32_t r) { return (uint32_t)mcol[(size_t)r * M.stride + g]; };
-  // greedy partition of the aggregates; stamp[g] = block that holds row g in S
-  std::vector<int32_t> stamp(nm, -1);
-  std::vector<uint32_t> jb{0};
-  uint32_t nS = 0, nF = 0, nJ = 0;
-  int blk = 0;
-  std::vector<uint32_t> added;
-  for (uint32_t J = 0; J < nc;) {
-    added.clear();
-    uint32_t dS = 0, dF = 0;
-    auto take = [&](uint32_t g) {
-      if (stamp[g] == blk) return;
-      stamp[g] = blk;
-      added.push_back(g);
-      ++dS;
-      dF += nfine(g);
-    };
-    for (uint32_t k = mr_row[J]; k < mr_row[J + 1]; ++k) {
-      const uint32_t g = mr_col[k];
-      take(g);
-      for (uint32_t r = 0; r < mlen[g]; ++r) take(col(g, r));
-    }
-    if (nS + dS <= kPairThreads && nF + dF <= kPairThreads && nJ + 1 <= kPairThreads) {
-      nS += dS;
-      nF += dF;
-      ++nJ;
-      ++J;
-      continue;
-    }
-    for (uint32_t g : added) stamp[g] = -1;  // J opens the next block
-    if (nJ == 0) return false;               // one aggregate alone does not fit
-    jb.push_back(J);
-    ++blk;
-    nS = nF = nJ = 0;
-  }
-  if (nJ) jb.push_back(nc);
-  const uint32_t nb = (uint32_t)jb.size() - 1;
-  // per block: S = members (R order) then the ring (ascending); f, local columns
-  std::vector<uint32_t> sb{0}, sv, fo{0}, fv;
+  // the off-diagonal pattern of level i + 1 as CSR in slot order
+  std::vector<uint32_t> mrow(nm + 1, 0), mcsr;
+  for (uint32_t g = 0; g < nm; ++g) mrow[g + 1] = mrow[g] + mlen[g];
+  mcsr.resize(mrow[nm]);
+  for (uint32_t g = 0; g < nm; ++g)
+    for (uint32_t r = 0; r < mlen[g]; ++r) mcsr[mrow[g] + r] = (uint32_t)mcol[(size_t)r * M.stride + g];
+  PairPartition pp;
+  if (!build_pair_partition(fr_row, fr_col, mr_row, mr_col, mrow, mcsr, kPairThreads, pp)) return false;
   std::vector<uint16_t> lc(slots, 0);
-  std::vector<int32_t> loc(nm, -1);
-  std::vector<uint32_t> ring;
-  for (uint32_t k = 0; k < nb; ++k) {
-    const uint32_t base = (uint32_t)sv.size();
-    for (uint32_t q = mr_row[jb[k]]; q < mr_row[jb[k + 1]]; ++q) {
-      loc[mr_col[q]] = (int32_t)(sv.size() - base);
-      sv.push_back(mr_col[q]);
-    }
-    const size_t own_end = sv.size();
-    ring.clear();
-    for (size_t q = base; q < own_end; ++q)
-      for (uint32_t r = 0; r < mlen[sv[q]]; ++r) {
-        const uint32_t c = col(sv[q], r);
-        if (loc[c] < 0) {
-          loc[c] = -2;  // queued
-          ring.push_back(c);
-        }
-      }
-    std::sort(ring.begin(), ring.end());
-    for (uint32_t c : ring) {
-      loc[c] = (int32_t)(sv.size() - base);
-      sv.push_back(c);
-    }
-    for (size_t q = base; q < own_end; ++q)
-      for (uint32_t r = 0; r < mlen[sv[q]]; ++r) lc[(size_t)r * M.stride + sv[q]] = (uint16_t)loc[col(sv[q], r)];
-    for (size_t q = base; q < sv.size(); ++q) {
-      for (uint32_t e = fr_row[sv[q]]; e < fr_row[sv[q] + 1]; ++e) fv.push_back(fr_col[e]);
-      fo.push_back((uint32_t)fv.size());
-    }
-    for (size_t q = base; q < sv.size(); ++q) loc[sv[q]] = -1;
-    if (sv.size() - base > kPairThreads || fo.back() - fo[base] > kPairThreads)
-      throw std::logic_error("AMG pair image: block over capacity");
-    sb.push_back((uint32_t)sv.size());
-  }
+  for (uint32_t g = 0; g < nm; ++g)
+    for (uint32_t r = 0; r < mlen[g]; ++r) lc[(size_t)r * M.stride + g] = pp.lc[mrow[g] + r];
+  const uint32_t nb = (uint32_t)pp.jb.size() - 1;
+  const std::vector<uint32_t>&jb = pp.jb, &sb = pp.sb, &sv = pp.s, &fo = pp.fo, &fv = pp.f;
   AmgPairImage& P = rr_pair[i];
   P.nblocks = nb;
   P.jb = arena.upload(jb, stream);

@@ -159,6 +159,23 @@ struct AmgHostLevel {
 std::vector<AmgHostLevel> build_amg_hierarchy(const HostCsr& fine, size_t max_levels,
                                                const std::vector<uint64_t>& part = {}, bool local = false,
                                                uint64_t rep_rows = 0, bool timing = false);
+// Block partition of a down-leg level pair (k_amg_resrestrict_pair,
+// kernels.hpp AmgPairImage).  fr_row / fr_col: R of level i (its aggregates
+// are the level-(i+1) rows); mr_row / mr_col: R of level i+1; mrow / mcol:
+// the off-diagonal pattern of level i+1 (CSR, entries in the level image's
+// slot order).  Each block takes consecutive level-(i+2) aggregates while its
+// S rows (their members, then the ring of the members' columns) and those
+// rows' level-i members each stay <= cap and its aggregates <= cap.  lc[k]:
+// the block-local index (in S) of entry k of mcol, for the rows the block owns.
+// False when one aggregate alone exceeds cap.
+struct PairPartition {
+  std::vector<uint32_t> jb, sb, s, fo, f;
+  std::vector<uint16_t> lc;
+};
+bool build_pair_partition(const std::vector<uint32_t>& fr_row, const std::vector<uint32_t>& fr_col,
+                          const std::vector<uint32_t>& mr_row, const std::vector<uint32_t>& mr_col,
+                          const std::vector<uint32_t>& mrow, const std::vector<uint32_t>& mcol, uint32_t cap,
+                          PairPartition& out);
 // Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
 // n rows; returns the aggregate count, agg[i] = aggregate of row i, and
 // cpart = the aggregate partition induced by the row partition `part` (an

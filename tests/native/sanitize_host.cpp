@@ -107,6 +107,57 @@ void run(const char* name, const cfd2::Mesh& m) {
     }
     for (size_t l = 0; l + 1 < H.size(); ++l)
       check(H[l].has_op && H[l + 1].A.rows == H[l].nc, "level sizes");
+    // down-leg pair partitions (k_amg_resrestrict_pair) of every level pair
+    // with a coarser level, at the kernel's capacity and at a small one
+    for (size_t l = 0; l + 2 < H.size(); ++l)
+      for (uint32_t cap : {1024u, 96u}) {
+        const cfd2::HostCsr& M = H[l + 1].A;
+        const uint32_t nm = (uint32_t)M.rows;
+        std::vector<uint32_t> mrow(nm + 1, 0), mcol;
+        for (uint32_t g = 0; g < nm; ++g) {
+          for (uint32_t k = M.row[g]; k < M.row[g + 1]; ++k)
+            if (M.col[k] != g) mcol.push_back(M.col[k]);
+          mrow[g + 1] = (uint32_t)mcol.size();
+        }
+        cfd2::PairPartition pp;
+        if (!cfd2::build_pair_partition(H[l].r_row, H[l].r_col, H[l + 1].r_row, H[l + 1].r_col, mrow, mcol, cap, pp))
+          continue;  // an aggregate alone over the capacity: no pair here
+        std::vector<int> owner(nm, -1);
+        const uint32_t nb = (uint32_t)pp.jb.size() - 1;
+        check(pp.jb.back() == H[l + 1].nc && pp.sb.size() == nb + 1, "pair partition blocks");
+        for (uint32_t b = 0; b < nb; ++b) {
+          const uint32_t m0 = H[l + 1].r_row[pp.jb[b]], m1 = H[l + 1].r_row[pp.jb[b + 1]];
+          const uint32_t s0 = pp.sb[b], s1 = pp.sb[b + 1];
+          check(s1 - s0 <= cap && pp.fo[s1] - pp.fo[s0] <= cap && m1 - m0 <= s1 - s0, "pair block capacity");
+          std::vector<int> in_s(nm, -1);
+          for (uint32_t q = s0; q < s1; ++q) {
+            check(in_s[pp.s[q]] < 0, "pair S row twice");
+            in_s[pp.s[q]] = (int)(q - s0);
+            const uint32_t g = pp.s[q];
+            check(pp.fo[q + 1] - pp.fo[q] == H[l].r_row[g + 1] - H[l].r_row[g], "pair member count");
+            for (uint32_t e = 0; e < pp.fo[q + 1] - pp.fo[q]; ++e)
+              check(pp.f[pp.fo[q] + e] == H[l].r_col[H[l].r_row[g] + e], "pair members in R order");
+          }
+          for (uint32_t q = 0; q < m1 - m0; ++q) {
+            const uint32_t g = pp.s[s0 + q];
+            check(g == H[l + 1].r_col[m0 + q], "pair owned rows in R order");
+            check(owner[g] < 0, "pair row owned twice");
+            owner[g] = (int)b;
+            for (uint32_t e = mrow[g]; e < mrow[g + 1]; ++e)
+              check(in_s[mcol[e]] >= 0 && pp.lc[e] == (uint16_t)in_s[mcol[e]], "pair local column");
+          }
+          for (uint32_t q = m1 - m0; q < s1 - s0; ++q) {  // ring rows: columns of owned rows
+            bool used = false;
+            const uint32_t c = pp.s[s0 + q];
+            for (uint32_t r = 0; r < m1 - m0 && !used; ++r) {
+              const uint32_t g = pp.s[s0 + r];
+              for (uint32_t e = mrow[g]; e < mrow[g + 1]; ++e) used = used || mcol[e] == c;
+            }
+            check(used, "pair ring row not a column of an owned row");
+          }
+        }
+        for (uint32_t g = 0; g < nm; ++g) check(owner[g] >= 0, "pair row not owned");
+      }
     for (size_t l = 0; l < H.size(); ++l) {  // coarse rows follow their seeds: a partition in rank order
       check(H[l].part.size() == (size_t)R + 1 && H[l].part[0] == 0 && H[l].part[R] == H[l].A.rows, "level partition");
       for (int q = 0; q < R; ++q) check(H[l].part[q] <= H[l].part[q + 1], "level partition order");
