@@ -2271,18 +2271,18 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
 // row headers and the aggregate ranges are loaded before phase 1, so the
 // second level costs LDS round trips only; the ring rows' level-i residuals
 // are the redundant work (amg_fusion_ratio.py).
-template <bool D16>
-__global__ void __launch_bounds__(kPairThreads) k_amg_resrestrict_pair(AmgLevelDev Lf, AmgLevelDev Lm,
+template <bool D16, uint32_t NTH>
+__global__ void __launch_bounds__(NTH) k_amg_resrestrict_pair(AmgLevelDev Lf, AmgLevelDev Lm,
                                                                      AmgPairImage P, const float* __restrict__ x,
                                                                      const float* __restrict__ b,
                                                                      float* __restrict__ bm, float* __restrict__ xm,
                                                                      float* __restrict__ cb, float* __restrict__ cx,
                                                                      float* __restrict__ sm_out,
                                                                      const float* __restrict__ sm_de) {
-  __shared__ float rl[kPairThreads];  // level-i residuals of the block's f rows
-  __shared__ float bs[kPairThreads];  // level-(i+1) rhs of the block's s rows
-  __shared__ float xs[kPairThreads];  // their pre-smoothed x
-  __shared__ float r2[kPairThreads];  // level-(i+1) residuals of the block's own rows
+  __shared__ float rl[NTH];  // level-i residuals of the block's f rows
+  __shared__ float bs[NTH];  // level-(i+1) rhs of the block's s rows
+  __shared__ float xs[NTH];  // their pre-smoothed x
+  __shared__ float r2[NTH];  // level-(i+1) residuals of the block's own rows
   const uint32_t blk = xcd_block<kRevResidual>();
   if (blk >= P.nblocks) return;
   const uint32_t t = threadIdx.x;
@@ -2320,7 +2320,7 @@ __global__ void __launch_bounds__(kPairThreads) k_amg_resrestrict_pair(AmgLevelD
   }
   // phase 1: level-i residuals (k_amg_resrestrict's row loop)
   const uint32_t w = (uint32_t)max(Lf.w, 1);
-  for (uint32_t p = fb + t; p < fe; p += kPairThreads) {
+  for (uint32_t p = fb + t; p < fe; p += NTH) {
     const uint32_t f = P.f[p];
     const uint32_t len = Lf.len[f], dr = Lf.drank[f];
     const float xf = x[f], dvf = Lf.dv[f];
@@ -3087,12 +3087,10 @@ void launch_amg_resrestrict_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lm, c
                                  const float* x, const float* b, float* bm, float* xm, float* cb, float* cx,
                                  float* sm_out, const float* sm_de, hipStream_t s) {
   if (!P.nblocks) return;
-  if (Lf.use16)
-    hipLaunchKernelGGL(k_amg_resrestrict_pair<true>, dim3(P.nblocks), dim3(kPairThreads), 0, s, Lf, Lm, P, x, b, bm, xm,
-                       cb, cx, sm_out, sm_de);
-  else
-    hipLaunchKernelGGL(k_amg_resrestrict_pair<false>, dim3(P.nblocks), dim3(kPairThreads), 0, s, Lf, Lm, P, x, b, bm,
-                       xm, cb, cx, sm_out, sm_de);
+  auto fn = P.threads == 256 ? (Lf.use16 ? k_amg_resrestrict_pair<true, 256> : k_amg_resrestrict_pair<false, 256>)
+                             : (Lf.use16 ? k_amg_resrestrict_pair<true, kPairThreads>
+                                         : k_amg_resrestrict_pair<false, kPairThreads>);
+  hipLaunchKernelGGL(fn, dim3(P.nblocks), dim3(P.threads), 0, s, Lf, Lm, P, x, b, bm, xm, cb, cx, sm_out, sm_de);
 }
 void launch_amg_prolong(const AmgLevelDev& L, float* x, const float* xc, hipStream_t s, uint32_t f0, uint32_t f1, bool nt) {
   if (f1 == 0) f1 = L.n;

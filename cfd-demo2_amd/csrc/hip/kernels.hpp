@@ -245,6 +245,7 @@ constexpr uint32_t kPairThreads = 1024;
 constexpr int kPairW = 8;  // level-(i+1) slots prefetched before the level-i phase
 struct AmgPairImage {
   uint32_t nblocks;
+  uint32_t threads;    // block size = per-block capacity (256 or kPairThreads)
   const uint32_t* jb;  // [nblocks + 1] level-(i+2) aggregate ranges
   const uint32_t* sb;  // [nblocks + 1] ranges in s
   const uint32_t* s;   // level-(i+1) rows: each block's members first, then its ring

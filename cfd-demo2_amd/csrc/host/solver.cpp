@@ -1153,8 +1153,14 @@ bool Solver::build_rr_pair(int i) {
   mcsr.resize(mrow[nm]);
   for (uint32_t g = 0; g < nm; ++g)
     for (uint32_t r = 0; r < mlen[g]; ++r) mcsr[mrow[g] + r] = (uint32_t)mcol[(size_t)r * M.stride + g];
+  // 256-thread blocks (one CU each, like the k_amg_resrestrict launches they
+  // replace) while the ring's redundant level-i rows stay within 25 %:
+  // 1,024-thread blocks (less redundancy, a quarter of the CUs) lost on both
+  // C1 pairs (profiles/r06/ab_log.md)
   PairPartition pp;
-  if (!build_pair_partition(fr_row, fr_col, mr_row, mr_col, mrow, mcsr, kPairThreads, pp)) return false;
+  const uint32_t threads = 256;
+  if (!build_pair_partition(fr_row, fr_col, mr_row, mr_col, mrow, mcsr, threads, pp)) return false;
+  if ((double)pp.f.size() > 1.25 * (double)F.n) return false;
   std::vector<uint16_t> lc(slots, 0);
   for (uint32_t g = 0; g < nm; ++g)
     for (uint32_t r = 0; r < mlen[g]; ++r) lc[(size_t)r * M.stride + g] = pp.lc[mrow[g] + r];
@@ -1162,6 +1168,7 @@ bool Solver::build_rr_pair(int i) {
   const std::vector<uint32_t>&jb = pp.jb, &sb = pp.sb, &sv = pp.s, &fo = pp.fo, &fv = pp.f;
   AmgPairImage& P = rr_pair[i];
   P.nblocks = nb;
+  P.threads = threads;
   P.jb = arena.upload(jb, stream);
   P.sb = arena.upload(sb, stream);
   P.s = arena.upload(sv, stream);
