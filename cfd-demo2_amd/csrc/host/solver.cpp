@@ -1110,7 +1110,8 @@ void Solver::set_resrestrict_blocks() {
 void Solver::build_rr_pairs() {
   const int L = (int)levels.size();
   rr_pair.assign(L, AmgPairImage{});
-  if (!knob_on(Knob::AmgFusedPair)) return;
+  pair_mode = (int)knob_u64(Knob::AmgFusedPair, 1);  // 0 off, 1 where cheap, 2 every candidate (tests)
+  if (pair_mode == 0) return;
   const int D = dist() ? amg_g : 0;
   const int down = std::min(std::max({tail_first, 1, D}), L - 1);
   for (int i = 0; i + 1 < down;) {
@@ -1160,7 +1161,7 @@ bool Solver::build_rr_pair(int i) {
   PairPartition pp;
   const uint32_t threads = 256;
   if (!build_pair_partition(fr_row, fr_col, mr_row, mr_col, mrow, mcsr, threads, pp)) return false;
-  if ((double)pp.f.size() > 1.25 * (double)F.n) return false;
+  if (pair_mode < 2 && (double)pp.f.size() > 1.25 * (double)F.n) return false;
   std::vector<uint16_t> lc(slots, 0);
   for (uint32_t g = 0; g < nm; ++g)
     for (uint32_t r = 0; r < mlen[g]; ++r) lc[(size_t)r * M.stride + g] = pp.lc[mrow[g] + r];

@@ -382,6 +382,7 @@ struct Solver {
   // i and i+1 run as one launch (single-GPU / replicated levels that both take
   // k_amg_resrestrict, level i+1 pre-smoothed)
   std::vector<AmgPairImage> rr_pair;
+  int pair_mode = 1;
   void build_rr_pairs();
   bool build_rr_pair(int i);
   std::vector<AmgGpuLevel> levels;

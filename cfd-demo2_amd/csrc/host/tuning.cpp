@@ -41,7 +41,8 @@ constexpr KnobInfo kKnobs[] = {
      "1: small-mesh kernel forms (CGS latency forms <= 2^17 cells, in-kernel CGS reduction <= 256 units, "
      "single-launch Jacobi relaxation <= 8191 cells); 0: the large-mesh forms everywhere"},
     {Knob::AmgFusedPair, "CFD_AMG_FUSED_PAIR",
-     "1: two adjacent k_amg_resrestrict levels of the down-leg in one launch (k_amg_resrestrict_pair); 0 off"},
+     "1: two adjacent k_amg_resrestrict levels of the down-leg in one launch (k_amg_resrestrict_pair) where "
+     "the ring's redundant rows stay within 25 %; 2: every candidate pair; 0 off"},
 };
 static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == (size_t)Knob::Count, "one table entry per knob");
 
