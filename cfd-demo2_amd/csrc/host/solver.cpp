@@ -1155,13 +1155,14 @@ bool Solver::build_rr_pair(int i) {
   for (uint32_t g = 0; g < nm; ++g)
     for (uint32_t r = 0; r < mlen[g]; ++r) mcsr[mrow[g] + r] = (uint32_t)mcol[(size_t)r * M.stride + g];
   // 256-thread blocks (one CU each, like the k_amg_resrestrict launches they
-  // replace) while the ring's redundant level-i rows stay within 25 %:
-  // 1,024-thread blocks (less redundancy, a quarter of the CUs) lost on both
-  // C1 pairs (profiles/r06/ab_log.md)
+  // replace) while the ring's redundant level-i rows stay within 50 %
+  // (profiles/r06/ab_log.md, C1: levels 4+5 at 1.41x rows 7.8 us against
+  // 5.5 + 5.1; levels 2+3 at 2.9x 16.1 us against 7.1 + 6.3; 1,024-thread
+  // blocks -- less redundancy, a quarter of the CUs -- lost on both pairs)
   PairPartition pp;
   const uint32_t threads = 256;
   if (!build_pair_partition(fr_row, fr_col, mr_row, mr_col, mrow, mcsr, threads, pp)) return false;
-  if (pair_mode < 2 && (double)pp.f.size() > 1.25 * (double)F.n) return false;
+  if (pair_mode < 2 && (double)pp.f.size() > 1.5 * (double)F.n) return false;
   std::vector<uint16_t> lc(slots, 0);
   for (uint32_t g = 0; g < nm; ++g)
     for (uint32_t r = 0; r < mlen[g]; ++r) lc[(size_t)r * M.stride + g] = pp.lc[mrow[g] + r];

@@ -42,7 +42,7 @@ constexpr KnobInfo kKnobs[] = {
      "single-launch Jacobi relaxation <= 8191 cells); 0: the large-mesh forms everywhere"},
     {Knob::AmgFusedPair, "CFD_AMG_FUSED_PAIR",
      "1: two adjacent k_amg_resrestrict levels of the down-leg in one launch (k_amg_resrestrict_pair) where "
-     "the ring's redundant rows stay within 25 %; 2: every candidate pair; 0 off"},
+     "the ring's redundant rows stay within 50 %; 2: every candidate pair; 0 off"},
 };
 static_assert(sizeof(kKnobs) / sizeof(kKnobs[0]) == (size_t)Knob::Count, "one table entry per knob");
 
