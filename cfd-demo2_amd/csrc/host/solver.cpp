@@ -963,6 +963,8 @@ void Solver::ensure_amg() {
   const bool timing = cfg.log_level >= 2 && rk == 0;
   const auto t_start = std::chrono::steady_clock::now();
   const char* se = knob(Knob::AmgSetup);
+  if (se && std::strcmp(se, "host") && std::strcmp(se, "device") && std::strcmp(se, "rebuild"))
+    throw std::invalid_argument(std::string("CFD_AMG_SETUP: expected device, host or rebuild, got ") + se);
   const bool device_setup = !(se && std::string(se) == "host");
   const char* how = "device";
   amg_setup_path = 2;
@@ -1962,8 +1964,9 @@ void Solver::step() {  // coupled_solver.rs:33-499
   // opt-in deviation from the frozen hierarchy
   if (cfg.amg_rebuild_interval > 0 && amg_built && amg_age >= (uint32_t)cfg.amg_rebuild_interval) {
     // numeric re-setup over the kept structure when the device setup built it
-    // (CFD_AMG_REFRESH=0: full rebuild; both give the same hierarchy)
-    if (amg_setup_path == 2 && !amg_refresh.empty() && knob_on(Knob::AmgRefresh))
+    // (CFD_AMG_SETUP=rebuild: full rebuild; both give the same hierarchy)
+    const char* se = knob(Knob::AmgSetup);  // "rebuild": a full setup instead of the refresh
+    if (amg_setup_path == 2 && !amg_refresh.empty() && !(se && std::strcmp(se, "rebuild") == 0))
       amg_refresh_pending = true;
     else
       drop_amg();

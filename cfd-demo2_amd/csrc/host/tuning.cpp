@@ -20,9 +20,9 @@ struct KnobInfo {
 constexpr KnobInfo kKnobs[] = {
     {Knob::AmgReplicateRows, "CFD_AMG_REPLICATE_ROWS",
      "2^20: distributed AMG levels of at most this many rows are replicated on every rank"},
-    {Knob::AmgSetup, "CFD_AMG_SETUP", "device: AMG setup on the GPU; 'host': the host setup (same hierarchy)"},
-    {Knob::AmgRefresh, "CFD_AMG_REFRESH",
-     "1: amg_rebuild_interval re-setup refreshes the values over the kept structure; 0: full rebuild"},
+    {Knob::AmgSetup, "CFD_AMG_SETUP",
+     "device: AMG setup on the GPU (amg_rebuild_interval re-setups refresh the values over the kept "
+     "structure); host: the host setup; rebuild: device setup, every re-setup a full one (same hierarchy)"},
     {Knob::OverlapMinRows, "CFD_OVERLAP_MIN_ROWS",
      "2^20: halo'd launches of at least this many rows split interior / boundary around the exchange"},
     {Knob::Nt, "CFD_NT", "47: nontemporal-load mask per kernel (Solver::nt_mask)"},
@@ -54,6 +54,7 @@ constexpr const char* kRemoved[] = {
     "CFD_GRAPH",          "CFD_PROF_STRIDE",      "CFD_CHECK_SYNC",          "CFD_AMG_SETUP_TIMING",
     "CFD_AMG_TAIL_LDS",   "CFD_AMG_TAIL_BLOB",    "CFD_AMG_BLOB_SHIFT",      "CFD_AMG_FUSED_PROLONG",
     "CFD_AMG_FUSED_RR",   "CFD_CGS_LAT",          "CFD_CGS_FUSE_REDUCE",     "CFD_RELAX_FUSED",
+    "CFD_AMG_REFRESH",
 };
 
 void warn_removed_once() {

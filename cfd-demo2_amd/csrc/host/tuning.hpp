@@ -17,7 +17,6 @@ namespace cfd2 {
 enum class Knob : int {
   AmgReplicateRows,    // CFD_AMG_REPLICATE_ROWS
   AmgSetup,            // CFD_AMG_SETUP
-  AmgRefresh,          // CFD_AMG_REFRESH
   OverlapMinRows,      // CFD_OVERLAP_MIN_ROWS
   Nt,                  // CFD_NT
   AmgFull,             // CFD_AMG_FULL

@@ -153,7 +153,7 @@ def test_group_hierarchy_is_the_global_one(replicate_rows):
 def test_group_amg_rebuild_interval(refresh, replicate_rows, monkeypatch):
     """Re-setting up the hierarchy every step (a distributed run rebuilds its
     global hierarchy; the single GPU refreshes or rebuilds): bit-exact."""
-    monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
+    monkeypatch.setenv("CFD_AMG_SETUP", "device" if refresh == "1" else "rebuild")
     replicate_rows(50)
     mesh = backwards_step()
     _three_way(mesh, 2, dict(amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8),
@@ -361,7 +361,7 @@ def test_group_local_aggregation_fewer_exchanges(replicate_rows):
 def test_group_local_aggregation_rebuild(refresh, replicate_rows, monkeypatch):
     """Partition-aware mode with the AMG re-setup every step (numeric refresh
     over the per-rank structure, or a full rebuild): == oracle(R, local)."""
-    monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
+    monkeypatch.setenv("CFD_AMG_SETUP", "device" if refresh == "1" else "rebuild")
     replicate_rows(50)
     mesh = backwards_step()
     cfg = dict(amg_local_aggregation=1, amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8)

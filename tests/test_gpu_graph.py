@@ -55,20 +55,12 @@ def test_graph_replay_parity(precond, cfg):
     assert eager.graph_stats() == (False, 0, 0)
 
 
-def test_graph_preconditioner_switch_and_rebuild():
+def test_graph_preconditioner_switch_and_rebuild(monkeypatch):
     """Jacobi <-> AMG switches and a full AMG rebuild every 2 steps (the
     graphs hold the hierarchy's pointers: dropped and captured again)."""
-    import os
-    old = os.environ.get("CFD_AMG_REFRESH")
-    os.environ["CFD_AMG_REFRESH"] = "0"  # full rebuild, new allocations
-    try:
-        mesh = channel_obstacle(h=0.04)
-        eager, graph, o = _three(mesh, fixed_outer=2, fixed_inner=8, amg_rebuild_interval=2)
-    finally:
-        if old is None:
-            os.environ.pop("CFD_AMG_REFRESH", None)
-        else:
-            os.environ["CFD_AMG_REFRESH"] = old
+    monkeypatch.setenv("CFD_AMG_SETUP", "rebuild")  # every re-setup a full rebuild, new allocations
+    mesh = channel_obstacle(h=0.04)
+    eager, graph, o = _three(mesh, fixed_outer=2, fixed_inner=8, amg_rebuild_interval=2)
     for s in (eager, graph, o):
         _setup_amg_test(s, mesh, 1)
     caps = []

@@ -458,7 +458,7 @@ def test_amg_refresh_matches_full_rebuild(monkeypatch):
     mesh = channel_obstacle(h=0.03)
     runs = {}
     for refresh in ("1", "0"):
-        monkeypatch.setenv("CFD_AMG_REFRESH", refresh)
+        monkeypatch.setenv("CFD_AMG_SETUP", "device" if refresh == "1" else "rebuild")
         g = GpuSolver(mesh, config=default_config(amg_rebuild_interval=1, fixed_outer=2, fixed_inner=8))
         _setup_amg_test(g, mesh, 1)
         out = []
