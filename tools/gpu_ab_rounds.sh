@@ -10,7 +10,7 @@ CFG=${CFG:-c2}
 ROUNDS=${ROUNDS:-3}
 ROOT=$GRAFT_REPO_ROOT
 names=()
-for spec in "$@"; do names+=("${spec%%:*}"); done
+for spec in "$@"; do names+=("${spec%%:*}"); rm -f gpurun_out/ab_${spec%%:*}_r*.json; done
 for k in $(seq 1 $ROUNDS); do
   for spec in "$@"; do
     v=${spec%%:*}; envs=${spec#*:}; [ "$envs" = "-" ] && envs=""
