@@ -2259,6 +2259,93 @@ __global__ void __launch_bounds__(kBlock) k_amg_resrestrict(AmgLevelDev L, const
     cx[I] = 0.0f;
 }
 
+// The up-leg of two adjacent single-GPU / replicated levels (c, c-1) in one
+// launch (AmgUpPairImage, kernels.hpp): phase 1 smooths the level-c rows T
+// the block needs with their prolongation from level c+1 applied to every
+// read (k_amg_smooth<..., PRO>'s operations: x' = x + (0 + 1 x_c+1[agg]),
+// sigma over the off-diagonals in slot order, mix(x', (b - sigma) / de,
+// 0.8)) into LDS; phase 2 smooths the block's fine rows the same way with
+// x_f + (0 + 1 x_c[agg]) read from that LDS image.  The fine rows' slots,
+// columns, local indices and x gathers are loaded before phase 1.
+template <bool D16F, bool D16C>
+__global__ void __launch_bounds__(kUpPairRows) k_amg_prolong_smooth_pair(AmgLevelDev Lf, AmgLevelDev Lc,
+                                                                       AmgUpPairImage P,
+                                                                       const float* __restrict__ xf,
+                                                                       const float* __restrict__ bf,
+                                                                       float* __restrict__ xf_out,
+                                                                       const float* __restrict__ xc,
+                                                                       const float* __restrict__ bc,
+                                                                       const float* __restrict__ xcc) {
+  __shared__ float xs[kUpPairCap];
+  const uint32_t blk = xcd_block<kRevSmooth>();
+  if (blk >= P.nblocks) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t f = blk * kUpPairRows + t;
+  const bool own = f < Lf.n;
+  // fine row operands (independent of phase 1)
+  constexpr int W = kPairW;
+  uint32_t flen = 0, flo = 0;
+  float fx = 0.0f, fb = 0.0f, fde = 1.0f;
+  float fv[W], fg[W];
+  uint32_t fl[W];
+  const uint32_t wf = (uint32_t)max(Lf.w, 1);
+  if (own) {
+    flen = Lf.len[f];
+    flo = P.lto[f];
+    fx = xf[f];
+    fb = bf[f];
+    fde = Lf.de[f];
+#pragma unroll
+    for (int r = 0; r < W; ++r) {
+      const size_t off = (size_t)min((uint32_t)r, wf - 1u) * Lf.stride + f;
+      fv[r] = Lf.val[off];
+      fl[r] = P.lt[off];
+      const int c = D16F ? (int)f + (int)Lf.col16[off] : Lf.col32[off];
+      fg[r] = xf[c];
+    }
+  }
+  // phase 1: post-smoothed level-c rows of T (prolongation from c+1 in the reads)
+  const uint32_t t0 = P.tb[blk], nt = P.tb[blk + 1] - t0;
+  const uint32_t wc = (uint32_t)max(Lc.w, 1);
+  for (uint32_t q = t; q < nt; q += kUpPairRows) {
+    const uint32_t g = P.t[t0 + q];
+    const uint32_t len = Lc.len[g];
+    float sg = 0.0f;
+    for (uint32_t r = 0; r < len; ++r) {
+      const size_t off = (size_t)min(r, wc - 1u) * Lc.stride + g;
+      const int c = D16C ? (int)g + (int)Lc.col16[off] : Lc.col32[off];
+      const float xg = prolonged(xc[c], xcc[Lc.agg[c]]);
+      sg += Lc.val[off] * xg;
+    }
+    float xx = xc[g];
+    float pc = 0.0f;
+    pc += 1.0f * xcc[Lc.agg[g]];
+    xx += pc;
+    xs[q] = wmix(xx, (bc[g] - sg) / Lc.de[g], 0.8f);
+  }
+  __syncthreads();
+  // phase 2: the block's fine rows, x_f + P x_c read through the LDS image
+  if (!own) return;
+  float sg = 0.0f;
+  for (uint32_t r = 0; r < flen; ++r) {
+    float v, xg;
+    if (r < (uint32_t)W) {
+      v = fv[r];
+      xg = prolonged(fg[r], xs[fl[r]]);
+    } else {
+      const size_t off = (size_t)r * Lf.stride + f;
+      const int c = D16F ? (int)f + (int)Lf.col16[off] : Lf.col32[off];
+      v = Lf.val[off];
+      xg = prolonged(xf[c], xs[P.lt[off]]);
+    }
+    sg += v * xg;
+  }
+  float pc = 0.0f;
+  pc += 1.0f * xs[flo];
+  fx += pc;
+  xf_out[f] = wmix(fx, (fb - sg) / fde, 0.8f);
+}
+
 // The down-leg of two adjacent single-GPU / replicated levels (i, i+1) in one
 // launch (AmgPairImage, kernels.hpp): the two k_amg_resrestrict launches'
 // arithmetic, operation for operation.  Phase 1: one level-i member residual
@@ -3082,6 +3169,14 @@ void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b
     hipLaunchKernelGGL(k_amg_resrestrict<true>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
   else
     hipLaunchKernelGGL(k_amg_resrestrict<false>, dim3(nb), dim3(kBlock), 0, s, L, x, b, cb, cx, sm_out, sm_de);
+}
+void launch_amg_prolong_smooth_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lc, const AmgUpPairImage& P,
+                                    const float* xf, const float* bf, float* xf_out, const float* xc,
+                                    const float* bc, const float* xcc, hipStream_t s) {
+  if (!P.nblocks) return;
+  auto fn = Lf.use16 ? (Lc.use16 ? k_amg_prolong_smooth_pair<true, true> : k_amg_prolong_smooth_pair<true, false>)
+                     : (Lc.use16 ? k_amg_prolong_smooth_pair<false, true> : k_amg_prolong_smooth_pair<false, false>);
+  hipLaunchKernelGGL(fn, dim3(P.nblocks), dim3(kUpPairRows), 0, s, Lf, Lc, P, xf, bf, xf_out, xc, bc, xcc);
 }
 void launch_amg_resrestrict_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lm, const AmgPairImage& P,
                                  const float* x, const float* b, float* bm, float* xm, float* cb, float* cx,

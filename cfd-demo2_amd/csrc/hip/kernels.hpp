@@ -253,6 +253,22 @@ struct AmgPairImage {
   const uint32_t* f;   // level-i rows
   const uint16_t* lc;  // [r * stride_{i+1} + row] block-local index (in s) of slot r's column
 };
+
+// k_amg_prolong_smooth_pair: the up-leg of two adjacent single-GPU /
+// replicated levels in one launch -- the post-smoother of coarse level c (its
+// prolongation from c+1 applied to its reads, k_amg_smooth<..., PRO>) for the
+// rows T the block needs, kept in LDS, then the post-smoother of fine level
+// c-1 reading x_f + P x_c.  A block owns kUpPairRows consecutive fine rows;
+// level c's smoothed x is never stored (nothing reads it after the up-leg).
+constexpr uint32_t kUpPairRows = 256;
+constexpr uint32_t kUpPairCap = 1024;  // T rows per block (LDS floats)
+struct AmgUpPairImage {
+  uint32_t nblocks;
+  const uint32_t* tb;   // [nblocks + 1] ranges in t
+  const uint32_t* t;    // level-c rows of each block (ascending)
+  const uint16_t* lt;   // [r * stride_f + row] T-local index of agg_f[col] of fine slot r
+  const uint16_t* lto;  // [stride_f] T-local index of agg_f[row]
+};
 // zeroed entries after every level's agg array: the fused prolongation reads
 // agg with 16-byte loads from any column (as the x gathers, whose vectors
 // carry the same slack)
@@ -404,6 +420,12 @@ void launch_amg_resrestrict(const AmgLevelDev& L, const float* x, const float* b
 // i+1's rhs bm and pre-smoothed x xm (as k_amg_resrestrict with sm_out), then
 // level i+2's rhs cb and either its pre-smoothed x (sm_out, diagonal sm_de)
 // or cx = 0 -- the bits of the two k_amg_resrestrict launches
+// levels c (Lc: x xc, b bc; coarse x xcc of level c+1) and c-1 (Lf: x xf, b
+// bf): writes only the fine level's post-smoothed x into xf_out -- the bits of
+// the two k_amg_smooth<..., PRO> launches for the fine level
+void launch_amg_prolong_smooth_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lc, const AmgUpPairImage& P,
+                                    const float* xf, const float* bf, float* xf_out, const float* xc,
+                                    const float* bc, const float* xcc, hipStream_t s);
 void launch_amg_resrestrict_pair(const AmgLevelDev& Lf, const AmgLevelDev& Lm, const AmgPairImage& P,
                                  const float* x, const float* b, float* bm, float* xm, float* cb, float* cx,
                                  float* sm_out, const float* sm_de, hipStream_t s);

@@ -284,4 +284,43 @@ bool build_pair_partition(const std::vector<uint32_t>& fr_row, const std::vector
   return true;
 }
 
+bool build_up_pair_partition(const std::vector<uint32_t>& frow, const std::vector<uint32_t>& fcol,
+                             const std::vector<uint32_t>& agg, uint32_t nc, uint32_t rows, uint32_t cap,
+                             UpPairPartition& out) {
+  const uint32_t nf = (uint32_t)frow.size() - 1;
+  if (agg.size() < nf || rows == 0) return false;
+  out = UpPairPartition{};
+  out.tb.assign(1, 0);
+  out.lt.assign(fcol.size(), 0);
+  out.lto.assign(nf, 0);
+  std::vector<int32_t> loc(nc, -1);
+  std::vector<uint32_t> tl;
+  for (uint32_t r0 = 0; r0 < nf; r0 += rows) {
+    const uint32_t r1 = std::min(nf, r0 + rows);
+    tl.clear();
+    auto add = [&](uint32_t c) {
+      if (c >= nc) throw std::logic_error("AMG up pair: aggregate out of range");
+      if (loc[c] == -1) {
+        loc[c] = -2;
+        tl.push_back(c);
+      }
+    };
+    for (uint32_t f = r0; f < r1; ++f) {
+      add(agg[f]);
+      for (uint32_t e = frow[f]; e < frow[f + 1]; ++e) add(agg[fcol[e]]);
+    }
+    std::sort(tl.begin(), tl.end());
+    if (tl.size() > cap) return false;
+    for (size_t q = 0; q < tl.size(); ++q) loc[tl[q]] = (int32_t)q;
+    for (uint32_t f = r0; f < r1; ++f) {
+      out.lto[f] = (uint16_t)loc[agg[f]];
+      for (uint32_t e = frow[f]; e < frow[f + 1]; ++e) out.lt[e] = (uint16_t)loc[agg[fcol[e]]];
+    }
+    for (uint32_t c : tl) loc[c] = -1;
+    out.t.insert(out.t.end(), tl.begin(), tl.end());
+    out.tb.push_back((uint32_t)out.t.size());
+  }
+  return true;
+}
+
 }  // namespace cfd2

@@ -1070,11 +1070,14 @@ void Solver::ensure_amg() {
     std::string pairs;
     for (int li = 0; li < (int)rr_pair.size(); ++li)
       if (rr_pair[li].nblocks) pairs += " " + std::to_string(li) + "+" + std::to_string(li + 1);
+    std::string ups;
+    for (int li = 0; li < (int)up_pair.size(); ++li)
+      if (up_pair[li].nblocks) ups += " " + std::to_string(li) + "+" + std::to_string(li - 1);
     std::fprintf(stderr,
                  "[amg setup] %s path: %d levels in %.3f s, tail from level %d (LDS image from level %d), "
-                 "down-leg pairs:%s\n",
+                 "down-leg pairs:%s, up-leg pairs:%s\n",
                  how, L, std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
-                 tail_first, tail_blob_first, pairs.empty() ? " none" : pairs.c_str());
+                 tail_first, tail_blob_first, pairs.empty() ? " none" : pairs.c_str(), ups.empty() ? " none" : ups.c_str());
   }
 }
 
@@ -1112,6 +1115,7 @@ void Solver::set_resrestrict_blocks() {
 void Solver::build_rr_pairs() {
   const int L = (int)levels.size();
   rr_pair.assign(L, AmgPairImage{});
+  up_pair.assign(L, AmgUpPairImage{});
   pair_mode = (int)knob_u64(Knob::AmgFusedPair, 1);  // 0 off, 1 where cheap, 2 every candidate (tests)
   if (pair_mode == 0) return;
   const int D = dist() ? amg_g : 0;
@@ -1121,6 +1125,59 @@ void Solver::build_rr_pairs() {
     const bool ok = !F.dist && !M.dist && !F.wide && !M.wide && F.dev.rr_agg && M.dev.rr_agg && M.dev.w >= 1;
     i += (ok && build_rr_pair(i)) ? 2 : 1;
   }
+  // up-leg: from the bottom, post-smoothers of levels c and c - 1 that both
+  // take the fused prolongation, fine level at most 2^18 rows
+  for (int c = down - 1; c >= 1;) {
+    const AmgGpuLevel &C = levels[c], &F = levels[c - 1];
+    const bool ok = fused_prolong(c) && fused_prolong(c - 1) && !C.wide && !F.wide && F.dev.n <= (1u << 18) &&
+                    F.dev.w >= 1 && C.dev.agg;
+    c -= (ok && build_up_pair(c)) ? 2 : 1;
+  }
+}
+
+// The up-leg pair image of levels (c, c - 1): blocks of kUpPairRows fine rows
+// and the level-c rows T they need (kUpPairCap at most), with the T-local
+// index of every fine slot's column aggregate.  Mode 1 pairs only while T
+// recomputes at most 50 % more level-c rows than the level has.
+bool Solver::build_up_pair(int c) {
+  const AmgLevelDev &F = levels[c - 1].dev, &C = levels[c].dev;
+  const uint32_t nf = F.n;
+  const size_t slots = (size_t)F.w * F.stride;
+  std::vector<uint8_t> flen(nf);
+  std::vector<uint32_t> agg(nf);
+  std::vector<int32_t> fc(slots);
+  CFD_HIP(hipMemcpyAsync(flen.data(), F.len, nf, hipMemcpyDeviceToHost, stream));
+  CFD_HIP(hipMemcpyAsync(agg.data(), F.agg, (size_t)nf * 4, hipMemcpyDeviceToHost, stream));
+  if (F.use16) {
+    std::vector<int16_t> c16(slots);
+    CFD_HIP(hipMemcpyAsync(c16.data(), F.col16, slots * 2, hipMemcpyDeviceToHost, stream));
+    sync();
+    for (size_t k = 0; k < slots; ++k) fc[k] = (int32_t)(k % F.stride) + c16[k];
+  } else {
+    CFD_HIP(hipMemcpyAsync(fc.data(), F.col32, slots * 4, hipMemcpyDeviceToHost, stream));
+    sync();
+  }
+  std::vector<uint32_t> frow(nf + 1, 0), fcol;
+  for (uint32_t g = 0; g < nf; ++g) frow[g + 1] = frow[g] + flen[g];
+  fcol.resize(frow[nf]);
+  for (uint32_t g = 0; g < nf; ++g)
+    for (uint32_t r = 0; r < flen[g]; ++r) fcol[frow[g] + r] = (uint32_t)fc[(size_t)r * F.stride + g];
+  UpPairPartition up;
+  if (!build_up_pair_partition(frow, fcol, agg, C.n, kUpPairRows, kUpPairCap, up)) return false;
+  if (pair_mode < 2 && (double)up.t.size() > 1.5 * (double)C.n) return false;
+  std::vector<uint16_t> lt(slots, 0), lto(F.stride, 0);
+  for (uint32_t g = 0; g < nf; ++g) {
+    lto[g] = up.lto[g];
+    for (uint32_t r = 0; r < flen[g]; ++r) lt[(size_t)r * F.stride + g] = up.lt[frow[g] + r];
+  }
+  AmgUpPairImage& P = up_pair[c];
+  P.nblocks = (uint32_t)up.tb.size() - 1;
+  P.tb = arena.upload(up.tb, stream);
+  P.t = arena.upload(up.t, stream);
+  P.lt = arena.upload(lt, stream);
+  P.lto = arena.upload(lto, stream);
+  sync();
+  return true;
 }
 
 // The pair image of levels (i, i+1): blocks of level-(i+2) aggregates whose
@@ -1500,6 +1557,16 @@ void Solver::v_cycle() {
       if (split < F.dev.n) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, split, F.dev.n, nt(32));
       halo_end();
       if (split > 0) launch_amg_prolong(F.dev, F.x, levels[ii + 1].x, stream, 0, split, nt(32));
+    } else if (ii >= 1 && (size_t)ii < up_pair.size() && up_pair[ii].nblocks) {
+      // levels ii and ii - 1 post-smoothed in one launch; level ii's smoothed x
+      // lives only in the kernel's LDS (nothing reads it after the up-leg), its
+      // buffers swap as the separate launch would leave them
+      AmgGpuLevel &Cl = levels[ii], &F = levels[ii - 1];
+      launch_amg_prolong_smooth_pair(F.dev, Cl.dev, up_pair[ii], F.x, F.b, F.xt, Cl.x, Cl.b, levels[ii + 1].x, stream);
+      std::swap(Cl.x, Cl.xt);
+      std::swap(F.x, F.xt);
+      --ii;  // level ii - 1 is done
+      continue;
     } else if (fused_prolong(ii)) {
       // the prolongation applied inside the post-smoother's reads (x stays un-prolonged)
       AmgGpuLevel& F = levels[ii];
@@ -2257,6 +2324,8 @@ double Solver::layout_step_bytes() const {
         vc += 4 * nc + 4 * n + 2 * st + img + 14 * n + 12 * nc;       // fused residual + restriction
       if (i > 0 && (size_t)i <= rr_pair.size() && rr_pair[i - 1].nblocks)
         vc -= 8 * n;  // second level of a k_amg_resrestrict_pair: its b and x stay in LDS
+      if ((size_t)i < up_pair.size() && up_pair[i].nblocks)
+        vc -= 8 * n;  // coarse level of a k_amg_prolong_smooth_pair: its smoothed x stays in LDS
       else
         vc += (2 * st + img + 16 * n) + (16 * nc + 4 * n + 12 * nc);  // residual, restriction
       if (fused_prolong(i))

@@ -176,6 +176,19 @@ bool build_pair_partition(const std::vector<uint32_t>& fr_row, const std::vector
                           const std::vector<uint32_t>& mr_row, const std::vector<uint32_t>& mr_col,
                           const std::vector<uint32_t>& mrow, const std::vector<uint32_t>& mcol, uint32_t cap,
                           PairPartition& out);
+// Block partition of an up-leg level pair (k_amg_prolong_smooth_pair,
+// kernels.hpp AmgUpPairImage): blocks of `rows` consecutive fine rows; each
+// block's T = the coarse rows its fine rows and their columns aggregate into
+// (ascending).  frow / fcol: the fine level's off-diagonal pattern (CSR, slot
+// order); agg: fine -> coarse.  lt[k]: T-local index of agg[fcol[k]] for
+// entry k, lto[f]: of agg[f].  False when a block's T exceeds cap.
+struct UpPairPartition {
+  std::vector<uint32_t> tb, t;
+  std::vector<uint16_t> lt, lto;
+};
+bool build_up_pair_partition(const std::vector<uint32_t>& frow, const std::vector<uint32_t>& fcol,
+                             const std::vector<uint32_t>& agg, uint32_t nc, uint32_t rows, uint32_t cap,
+                             UpPairPartition& out);
 // Greedy index-order aggregation (amg.rs:84-116) of the pattern (row, col) of
 // n rows; returns the aggregate count, agg[i] = aggregate of row i, and
 // cpart = the aggregate partition induced by the row partition `part` (an
@@ -385,6 +398,10 @@ struct Solver {
   int pair_mode = 1;
   void build_rr_pairs();
   bool build_rr_pair(int i);
+  // up-leg pairs (k_amg_prolong_smooth_pair): up_pair[c].nblocks > 0 when the
+  // post-smoothers of levels c and c-1 run as one launch
+  std::vector<AmgUpPairImage> up_pair;
+  bool build_up_pair(int c);
   std::vector<AmgGpuLevel> levels;
   // the scalar matrix (ELL image, like sval) the hierarchy was built from:
   // snapshot at setup, or a checkpoint's (amg_src_loaded: ensure_amg builds from it)

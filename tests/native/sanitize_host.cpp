@@ -158,6 +158,31 @@ void run(const char* name, const cfd2::Mesh& m) {
         }
         for (uint32_t g = 0; g < nm; ++g) check(owner[g] >= 0, "pair row not owned");
       }
+    // up-leg pair partitions (k_amg_prolong_smooth_pair): fine level l, coarse l + 1
+    for (size_t l = 0; l + 1 < H.size(); ++l)
+      for (uint32_t rows : {256u, 64u}) {
+        const cfd2::HostCsr& Fm = H[l].A;
+        const uint32_t nf = (uint32_t)Fm.rows, nc = H[l].nc;
+        std::vector<uint32_t> frow(nf + 1, 0), fcol;
+        for (uint32_t g = 0; g < nf; ++g) {
+          for (uint32_t k = Fm.row[g]; k < Fm.row[g + 1]; ++k)
+            if (Fm.col[k] != g) fcol.push_back(Fm.col[k]);
+          frow[g + 1] = (uint32_t)fcol.size();
+        }
+        cfd2::UpPairPartition up;
+        if (!cfd2::build_up_pair_partition(frow, fcol, H[l].agg, nc, rows, 1024, up)) continue;
+        const uint32_t nb = (nf + rows - 1) / rows;
+        check(up.tb.size() == nb + 1, "up pair blocks");
+        for (uint32_t b = 0; b < nb; ++b) {
+          const uint32_t t0 = up.tb[b], t1 = up.tb[b + 1];
+          for (uint32_t q = t0 + 1; q < t1; ++q) check(up.t[q - 1] < up.t[q], "up pair T ascending");
+          for (uint32_t f = b * rows; f < std::min(nf, (b + 1) * rows); ++f) {
+            check(up.t[t0 + up.lto[f]] == H[l].agg[f], "up pair own aggregate");
+            for (uint32_t e = frow[f]; e < frow[f + 1]; ++e)
+              check(up.t[t0 + up.lt[e]] == H[l].agg[fcol[e]], "up pair column aggregate");
+          }
+        }
+      }
     for (size_t l = 0; l < H.size(); ++l) {  // coarse rows follow their seeds: a partition in rank order
       check(H[l].part.size() == (size_t)R + 1 && H[l].part[0] == 0 && H[l].part[R] == H[l].A.rows, "level partition");
       for (int q = 0; q < R; ++q) check(H[l].part[q] <= H[l].part[q + 1], "level partition order");

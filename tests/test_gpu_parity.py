@@ -647,9 +647,10 @@ def test_fixed_schedule_early_exits(inlet):
 @pytest.mark.parametrize("mesh_name", ["amg_test", "graded", "channel_012"])
 @pytest.mark.parametrize("pair", ["2", "0"])
 def test_amg_resrestrict_pair_parity(mesh_name, pair, monkeypatch, capfd):
-    """k_amg_resrestrict_pair: two adjacent down-leg levels in one launch
-    (CFD_AMG_FUSED_PAIR; production: C1's levels 4+5, where the ring adds
-    under 25 % rows).  With the tail off every level pair of these meshes is a
+    """k_amg_resrestrict_pair / k_amg_prolong_smooth_pair: two adjacent
+    down-leg levels, and two adjacent up-leg post-smoothers, in one launch
+    (CFD_AMG_FUSED_PAIR; production: C1's levels 4+5 where the ring adds
+    under 50 % rows).  With the tail off every level pair of these meshes is a
     candidate and mode 2 pairs them all; GPU == oracle bit-exact with the
     pairs on and off, and the setup line names the pairs."""
     monkeypatch.setenv("CFD_AMG_TAIL_ROWS", "0")
@@ -674,8 +675,9 @@ def test_amg_resrestrict_pair_parity(mesh_name, pair, monkeypatch, capfd):
         _assert_same_fields(g, o, f"pair={pair} {mesh_name} step {k}")
         _assert_same_info(g, o, f"pair={pair} {mesh_name} step {k}")
     import re
-    m = re.search(r"down-leg pairs:(.*)\n", capfd.readouterr().err)
+    m = re.search(r"down-leg pairs:(.*), up-leg pairs:(.*)\n", capfd.readouterr().err)
     assert m, "no AMG setup line"
-    pairs = [] if m.group(1).strip() == "none" else m.group(1).split()
-    assert (len(pairs) > 0) == (pair == "2"), pairs  # 2: every candidate pair, whatever its redundancy
+    for grp in (1, 2):  # 2: every candidate pair of either leg, whatever its redundancy
+        pairs = [] if m.group(grp).strip() == "none" else m.group(grp).split()
+        assert (len(pairs) > 0) == (pair == "2"), (grp, pairs)
     g.close()
