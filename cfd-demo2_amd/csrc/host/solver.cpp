@@ -1137,8 +1137,10 @@ void Solver::build_rr_pairs() {
 
 // The up-leg pair image of levels (c, c - 1): blocks of kUpPairRows fine rows
 // and the level-c rows T they need (kUpPairCap at most), with the T-local
-// index of every fine slot's column aggregate.  Mode 1 pairs only while T
-// recomputes at most 50 % more level-c rows than the level has.
+// index of every fine slot's column aggregate.  Mode 1 pairs only while the
+// blocks' T rows total at most 2.5x the level's rows (profiles/r06/ab_log.md,
+// C1: levels 5+4 9.1 us against 7.5 + 6.3, in; 3+2 13.1 against 6.8 + 6.7,
+// out).
 bool Solver::build_up_pair(int c) {
   const AmgLevelDev &F = levels[c - 1].dev, &C = levels[c].dev;
   const uint32_t nf = F.n;
@@ -1164,7 +1166,7 @@ bool Solver::build_up_pair(int c) {
     for (uint32_t r = 0; r < flen[g]; ++r) fcol[frow[g] + r] = (uint32_t)fc[(size_t)r * F.stride + g];
   UpPairPartition up;
   if (!build_up_pair_partition(frow, fcol, agg, C.n, kUpPairRows, kUpPairCap, up)) return false;
-  if (pair_mode < 2 && (double)up.t.size() > 1.5 * (double)C.n) return false;
+  if (pair_mode < 2 && (double)up.t.size() > 2.5 * (double)C.n) return false;
   std::vector<uint16_t> lt(slots, 0), lto(F.stride, 0);
   for (uint32_t g = 0; g < nf; ++g) {
     lto[g] = up.lto[g];
