@@ -346,7 +346,7 @@ def main():
     ap.add_argument("--outer", type=int, default=5)
     ap.add_argument("--inner", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--ref-workloads", type=int, default=1,
                     help="1: also time the reference's own criterion workloads (natural convergence) as extra keys")
     ap.add_argument("--inproc-ranks", type=int, default=0,
