@@ -44,5 +44,5 @@ for m in (47, 111):
     mb = (2 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) / 1e3  # KB -> MB
     us = statistics.fmean(durs[g1])
     wc = max(c.get("SQ_WAVE_CYCLES", 1.0), 1.0)
-    print(f"{m:5d} {g1:9d} {len(durs[g1]):4d} {us:8.2f} {mb:10.1f} {mb / us / 1e3 * 1e3 / 1e3:6.2f} "
+    print(f"{m:5d} {g1:9d} {len(durs[g1]):4d} {us:8.2f} {mb:10.1f} {mb / us:6.2f} "
           f"{c.get('SQ_WAIT_ANY', 0.0) / wc:5.2f} {c.get('SQ_WAIT_INST_ANY', 0.0) / wc:9.2f}")
