@@ -299,7 +299,7 @@ cfd_status cfd_profile_smoother(const cfd_solver* s, double* total_ms, uint64_t*
 /* hipGraph replay of the FGMRES iteration (one executable graph per basis
  * index, captured on first use, replayed by every later solve; DESIGN.md
  * section 5).  enable: 1 on, 0 off (the launches are issued one by one);
- * default from CFD_GRAPH (1 on), else off: replay measured no faster than
+ * default off: replay measured no faster than
  * eager launches.  One GPU only.  Same bits either
  * way.  Stats: graphs captured and iterations replayed so far.             */
 cfd_status cfd_graph_enable(cfd_solver* s, int32_t enable);
