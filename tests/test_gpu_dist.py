@@ -185,6 +185,8 @@ def test_group_overlapped_halo_path(nranks, which, replicate_rows, monkeypatch):
 
 @pytest.mark.parametrize("env", [{"CFD_AMG_FULL": "0"}, {"CFD_AMG_TAIL_ROWS": "0"},
                                  {"CFD_AMG_FUSED_PROLONG_ROWS": "0"}, {"CFD_SMALL_MESH_FORMS": "0"},
+                                 # every level pair of the replicated levels in one launch
+                                 {"CFD_AMG_FUSED_PAIR": "2", "CFD_AMG_TAIL_ROWS": "0"},
                                  # every level split around its exchanges
                                  {"CFD_OVERLAP_MIN_ROWS": "64", "CFD_AMG_TAIL": "global"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))

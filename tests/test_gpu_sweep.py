@@ -67,7 +67,10 @@ def _case(seed):
     if rng.random() < 0.35:
         cfg.update(amg_local_aggregation=1)
     graph = rng.random() < 0.3
-    return kind, mesh, cfg, phys, nranks, useed, graph
+    # round 6: every candidate AMG level pair in one launch, the tail off (so
+    # that these small meshes have candidate pairs)
+    pairs = rng.random() < 0.3
+    return kind, mesh, cfg, phys, nranks, useed, graph, pairs
 
 
 def _setup(s, mesh, phys, useed):
@@ -91,10 +94,13 @@ def _setup(s, mesh, phys, useed):
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
-    kind, mesh, cfg, phys, nranks, useed, graph = _case(seed)
+    kind, mesh, cfg, phys, nranks, useed, graph, pairs = _case(seed)
     # ranks own whole reduction segments (>= 256 cells): small meshes take fewer ranks
     nranks = min(nranks, max_ranks(mesh.num_cells()))
     monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "200")  # distributed coarse levels on these small meshes
+    if pairs:
+        monkeypatch.setenv("CFD_AMG_FUSED_PAIR", "2")
+        monkeypatch.setenv("CFD_AMG_TAIL_ROWS", "0")
     c = default_config(**cfg)
     g = GpuSolver(mesh, config=c) if nranks == 1 else GpuGroup(mesh, nranks, config=c)
     if nranks == 1 and graph:
@@ -102,7 +108,7 @@ def test_random_case_parity(seed, monkeypatch):
     o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
     for s in (g, o):
         _setup(s, mesh, phys, useed)
-    ctx = f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}, graph={graph}"
+    ctx = f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}, graph={graph}, pairs={pairs}"
     for k in range(3):
         g.step()
         o.step()
