@@ -941,6 +941,8 @@ void Solver::drop_amg() {
   d_tail_desc = nullptr;
   tail_blob_words = tail_vec_floats = 0;
   amg_refresh.clear();
+  rr_pair.clear();  // their block images lived in amg_arena
+  up_pair.clear();
   amg_setup_flag = nullptr;
   amg_refresh_pending = false;
   amg_arena.release();
