@@ -1,4 +1,4 @@
-// CPU oracle — TEST INFRASTRUCTURE ONLY (see oracle.h).  PARITY UNPINNED.
+// CPU oracle — TEST INFRASTRUCTURE ONLY (see oracle.h).  Pinned to the reference's WGSL kernels (oracle.h).
 //
 // Literal f32 restatement of the reference hot path (TSultanov/cfd-demo2):
 //   prepare_coupled.wgsl:63-348          -> prepare()

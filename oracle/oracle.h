@@ -5,11 +5,15 @@
  * load this library, and only as the checker / reported CPU baseline.  The
  * product (cfd-demo2_amd/) never links or calls it.
  *
- * PARITY UNPINNED: the reference (Rust + wgpu, TSultanov/cfd-demo2) cannot be
- * built here (no cargo/rustc, needs a wgpu adapter) and its own tests hold no
- * golden field values.  The oracle is a literal f32 restatement
- * of the reference WGSL + Rust control flow with the deterministic choices of
- * SURVEY §0.1, checked against the reference tests' behavioural assertions.
+ * Parity pinned to the reference's own kernels (round 6): the reference's
+ * WGSL shaders, executed on the CPU from its source (oracle/wgsl/, driven by
+ * tests/wgsl_ref.py; fixtures tests/golden/wgsl_ref.npz), reproduce this
+ * oracle bit for bit with reference-semantics flags 15 (workgroups in order,
+ * Restrict policy) and 4 (whole dispatch resident, ReadZeroSkipWrite); the
+ * canonical mode (flags 0, what the HIP path reproduces) differs from the
+ * latter only by its reduction tree.  The Rust host sequence (dispatch order,
+ * AMG setup, readbacks) is restated, not executed: the reference program
+ * itself (Rust + wgpu) cannot be built here.
  */
 #ifndef CFD2_ORACLE_H
 #define CFD2_ORACLE_H

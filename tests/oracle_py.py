@@ -2,7 +2,8 @@
 
 TEST INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py.  Mirrors the GpuSolver API so parity tests can
-drive both with the same script.  PARITY UNPINNED (see oracle/oracle.h).
+drive both with the same script.  Pinned to the reference's own WGSL kernels
+(tests/test_wgsl_pin.py; see oracle/oracle.h).
 """
 from __future__ import annotations
 
