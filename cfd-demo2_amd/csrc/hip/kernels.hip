@@ -310,11 +310,45 @@ __device__ __forceinline__ T total_tree(const T* a, uint32_t P, T* b) {
   return tot;
 }
 
+// The 64-wide halving tree of the reference's workgroup reductions (stride
+// 32 .. 1: lane l adds lane l + stride, gmres_ops.wgsl:177-182) as one
+// wavefront's shuffles -- the same pairs, lane 0 holds the result.
+template <class T>
+__device__ __forceinline__ T ref_tree64(T v) {
+  for (int st = 32; st > 0; st >>= 1) v = v + __shfl_down(v, st);
+  return v;
+}
+
+// Reference reduction order (RedSrcT::order, test mode): the total of vector v
+// from the reference's 64-DOF group partials.  Every thread returns it.
+template <class T, int NT>
+__device__ __forceinline__ T ref_total(const RedSrcT<T>& r, uint32_t v, T* b) {
+  const T* p = r.p + (size_t)v * r.stride;
+  __syncthreads();
+  if (r.order == 1) {  // reduce_final: one thread, the partials in order
+    if (threadIdx.x == 0) {
+      T s = T(0);
+      for (uint32_t k = 0; k < r.nchunks; ++k) s += p[k];
+      b[64] = s;
+    }
+  } else if (threadIdx.x < 64) {  // reduce_dots_cgs: strided lane sums, then the tree
+    T s = T(0);
+    for (uint32_t k = threadIdx.x; k < r.nchunks; k += 64) s += p[k];
+    s = ref_tree64(s);
+    if (threadIdx.x == 0) b[64] = s;
+  }
+  __syncthreads();
+  const T tot = b[64];
+  __syncthreads();  // the caller may reuse the LDS
+  return tot;
+}
+
 // Total of vector v of reduction r by the whole block (NT threads): the
 // segment values into LDS a[0, P) (+0 padding to P = pow2 >= nseg), then the
 // pairwise tree over them.  Every thread returns the total.
 template <class T, int NT>
 __device__ __forceinline__ T red_total(const RedSrcT<T>& r, uint32_t v, T* a, T* b) {
+  if (r.order) return ref_total<T, NT>(r, v, b);
   const uint32_t P = pow2_ceil(r.nseg);
   if (r.seg_src) {  // distributed: gathered segment values
     const size_t blk = (size_t)r.nvec * r.stride;
@@ -803,6 +837,34 @@ __global__ void __launch_bounds__(kBlock) k_dot_partial(const float* __restrict_
   __syncthreads();
   const uint32_t UB = 4 / U, unit = blockIdx.x * UB + threadIdx.x;
   if (threadIdx.x < UB && (size_t)unit * U * kRedChunkCells < N) partial[unit] = unit_value_q(lds, U, threadIdx.x);
+}
+
+// Reference-order group partials (test mode, launch_ref_norm_partials /
+// launch_ref_cgs_dots): one wavefront per 64-DOF group, four per block.
+__global__ void __launch_bounds__(256) k_ref_norm_partials(const float* __restrict__ v, uint32_t n3,
+                                                          float* partial, uint32_t ng) {
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  const size_t i = (size_t)g * 64 + l;
+  float x = 0.0f;
+  if (i < n3) {
+    const float a = v[i];
+    x = a * a;  // norm_sq_partial: val * val
+  }
+  x = ref_tree64(x);
+  if (l == 0 && g < ng) partial[g] = x;
+}
+__global__ void __launch_bounds__(256) k_ref_cgs_dots(const float* __restrict__ w, const float* __restrict__ basis,
+                                                     const float* __restrict__ binv, size_t stride, uint32_t n3,
+                                                     float* partial, uint32_t pstride, uint32_t ng) {
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63, ii = blockIdx.y;
+  const size_t i = (size_t)g * 64 + l;
+  float x = 0.0f;
+  if (i < n3) {
+    const float vv = binv[ii] * basis[(size_t)ii * stride + i];  // V_ii as the reference's scale stored it
+    x = vv * w[i];                                               // calc_dots_cgs: v * w_val
+  }
+  x = ref_tree64(x);
+  if (l == 0 && g < ng) partial[(size_t)ii * pstride + g] = x;
 }
 
 // norm outputs of a finished dot: mode 1: out = sqrt(s); mode 2: also inv, g0
@@ -2991,6 +3053,17 @@ inline unsigned red_blocks(uint32_t N) {  // 4 chunks of 256 cells per 256-threa
 }
 void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s) {
   if (N) hipLaunchKernelGGL(k_dot_partial, dim3(red_blocks(N)), dim3(kBlock), 0, s, x, y, N, U, partial);
+}
+void launch_ref_norm_partials(const float* v, uint32_t n3, float* partial, hipStream_t s) {
+  const uint32_t ng = (n3 + 63) / 64;
+  if (ng) hipLaunchKernelGGL(k_ref_norm_partials, dim3((ng + 3) / 4), dim3(256), 0, s, v, n3, partial, ng);
+}
+void launch_ref_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t n3,
+                         float* partial, uint32_t pstride, hipStream_t s) {
+  const uint32_t ng = (n3 + 63) / 64;
+  if (ng)
+    hipLaunchKernelGGL(k_ref_cgs_dots, dim3((ng + 3) / 4, (unsigned)(j + 1)), dim3(256), 0, s, w, basis, binv, stride,
+                       n3, partial, pstride, ng);
 }
 void launch_reduce_final(const RedSrc& r, int mode, float* out, float* inv, float* g0, int g_len, float* host_out,
                          hipStream_t s) {

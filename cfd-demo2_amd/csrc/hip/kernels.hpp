@@ -89,6 +89,11 @@ struct RedSrcT {
   uint32_t nseg = 0;
   uint32_t nvec = 1;
   const uint32_t* seg_src = nullptr;
+  // 0: the canonical tree.  Reference order (test mode, Solver::ref_red): 1
+  // one thread adds the nchunks group partials in order (reduce_final,
+  // gmres_ops.wgsl:257-262); 2 lanes t < 64 add partials t, t + 64, ...,
+  // then the 64-wide halving tree (reduce_dots_cgs, gmres_cgs.wgsl:97-118)
+  uint32_t order = 0;
 };
 using RedSrc = RedSrcT<float>;
 using RedSrcD = RedSrcT<double>;
@@ -319,6 +324,14 @@ void launch_update_fields(uint32_t N, float alpha_u, float alpha_p, const float*
                           float* p, uint32_t* blockmax, uint32_t* maxbits, uint32_t* host_out, hipStream_t s);
 // unit partials (U chunks of 256 cells each) of dot(x, y) over 3-component cells
 void launch_dot_partial(const float* x, const float* y, uint32_t N, uint32_t U, float* partial, hipStream_t s);
+// Reference reduction order (test mode): partial[g] = the 64-wide halving tree
+// of v[i] * v[i] over DOFs i in [64 g, 64 g + 64) of the 3N (norm_sq_partial,
+// gmres_ops.wgsl:195-223); ng = ceil(n3 / 64) groups
+void launch_ref_norm_partials(const float* v, uint32_t n3, float* partial, hipStream_t s);
+// partial[ii * pstride + g] = the same tree of V_ii[i] * w[i], V_ii = binv[ii] *
+// W_ii, ii = 0..j (calc_dots_cgs, gmres_cgs.wgsl:28-82)
+void launch_ref_cgs_dots(const float* w, const float* basis, const float* binv, size_t stride, int j, uint32_t n3,
+                         float* partial, uint32_t pstride, hipStream_t s);
 // total of the reduction r (one vector): mode 1: out[0] = sqrt(total); mode 2:
 // also *inv = 1.0f / sqrt (host-style) and g0 (if non-null) = sqrt
 // g0 (mode 2): g0[0] = norm, g0[1..g_len) = 0; host_out (device view of pinned host memory, or null) = norm

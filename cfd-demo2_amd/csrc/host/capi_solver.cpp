@@ -294,6 +294,11 @@ cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble) {
   return guard([&] { s->s->debug_prepare_assemble(assemble != 0); });
 }
 
+cfd_status cfd_debug_reference_reductions(cfd_solver* s, int32_t on) {
+  CHECK_S(s);
+  return guard([&] { s->s->set_reference_reductions(on != 0); });
+}
+
 // ---------------------------------------------------------------- multi-GPU
 cfd_status cfd_dist_unique_id(uint8_t out[128]) {
   if (!out) return set_error(CFD_ERR_INVALID, "null out");

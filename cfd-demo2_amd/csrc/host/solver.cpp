@@ -1646,7 +1646,24 @@ void Solver::precondition(int j, float* z) {
   });
 }
 
+void Solver::set_reference_reductions(bool on) {
+  if (on && dist()) throw std::invalid_argument("reference reduction order: one GPU only");
+  if (on && !ref_part) {
+    ref_ng = (uint32_t)((3 * (uint64_t)N + 63) / 64);
+    ref_part = arena.alloc<float>((size_t)(m1 + 1) * ref_ng + 1);
+    ref_norm = arena.alloc<float>((size_t)ref_ng + 1);
+  }
+  drop_graphs();  // captured iterations hold the other order's launches
+  ref_red = on;
+}
+
 void Solver::norm_launch(const float* v, int mode, int slot) {
+  if (ref_red) {  // gpu_norm: norm_sq_partial + reduce_final (coupled_solver_fgmres.rs:1444-1588)
+    launch_ref_norm_partials(v, 3 * N, ref_norm, stream);
+    launch_reduce_final(ref_src(ref_norm, 1), mode, dsc + slot, binv, mode == 2 ? g : nullptr, m1, d_pin + slot,
+                        stream);
+    return;
+  }
   launch_dot_partial(v, v, N, red.U, partial_n, stream);
   // the norm also lands in h_pin[slot] (mapped pinned memory): a blocking read needs no copy
   launch_reduce_final(combine(partial_n, 1), mode, dsc + slot, binv, mode == 2 ? g : nullptr, m1, d_pin + slot,
@@ -1708,6 +1725,16 @@ void Solver::iteration(int j, float* pin) {
     launch_spmv(A, zj, w, stream, nullptr, nt(8));
   });
   const bool lat = small_forms && cgs_latency_form(N);
+  if (ref_red) {  // calc_dots_cgs / reduce_dots_cgs / update_w_cgs, then norm_sq_partial + finish
+    launch_ref_cgs_dots(w, basis, binv, stride, j, 3 * N, ref_part, ref_ng, stream);
+    launch_cgs_reduce(ref_src(ref_part, 2), j, H, m1, stream);
+    launch_cgs_update_norm(w, basis, binv, stride, j, H, m1, N, red.U, partial_n, stream, cgs_keep_bytes > 0, true,
+                           nullptr, lat);
+    launch_ref_norm_partials(basis + (size_t)(j + 1) * stride, 3 * N, ref_norm, stream);
+    launch_norm_givens(ref_src(ref_norm, 1), j, H, m1, givens, g, binv, resid_hist, pin, stream);
+    check_launch("FGMRES iteration (reference reduction order)");
+    return;
+  }
   launch_cgs_dots(w, basis, binv, stride, j, N, red.U, partial, pstride, stream, cgs_keep_bytes, lat);
   const RedSrc dots = combine(partial, j + 1);
   const bool fuse_reduce = small_forms && cgs_reduce_fusable(dots);
@@ -1939,6 +1966,54 @@ cfd_linear_stats Solver::solve() {  // coupled_solver_fgmres.rs:1728-2448
   return st;
 }
 
+// Reference reduction order (test mode): coupled_solver.rs:504-545 literally,
+// on the host -- the AoS FluidState view (8 floats per cell: u, v, p, d_p,
+// grad_p, grad_component = 0) read at floats 2i, 2i + 1 (the stride bug) and
+// serial f64 loops.  tot: evolution, sum u, sum v, sum u^2, sum v^2.
+void Solver::evolution_reference(double tot[5]) {
+  auto aos = [&](const StateView& v, std::vector<float>& out) {
+    std::vector<float2> u(N), gp(N);
+    std::vector<float> p(N), dp(N);
+    CFD_HIP(hipMemcpyAsync(u.data(), v.u, N * sizeof(float2), hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(p.data(), v.p, N * sizeof(float), hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(dp.data(), v.dp, N * sizeof(float), hipMemcpyDeviceToHost, stream));
+    CFD_HIP(hipMemcpyAsync(gp.data(), v.gp, N * sizeof(float2), hipMemcpyDeviceToHost, stream));
+    sync();
+    out.assign(8 * (size_t)N, 0.0f);
+    for (size_t c = 0; c < N; ++c) {
+      float* r = out.data() + 8 * c;
+      r[0] = u[c].x;
+      r[1] = u[c].y;
+      r[2] = p[c];
+      r[3] = dp[c];
+      r[4] = gp[c].x;
+      r[5] = gp[c].y;
+    }
+  };
+  std::vector<float> cur, old;
+  aos(S(), cur);
+  double e = 0.0, a = 0.0, b = 0.0, aa = 0.0, bb = 0.0;
+  if (have_prev) {
+    aos(prev, old);
+    for (size_t k = 0; k < cur.size(); ++k) {
+      const float d = cur[k] - old[k];
+      e += (double)(d * d);
+    }
+  }
+  for (size_t c = 0; c < N; ++c) {
+    const double u = (double)cur[2 * c], v = (double)cur[2 * c + 1];
+    a += u;
+    b += v;
+    aa += u * u;
+    bb += v * v;
+  }
+  tot[0] = e;
+  tot[1] = a;
+  tot[2] = b;
+  tot[3] = aa;
+  tot[4] = bb;
+}
+
 // check_evolution (coupled_solver.rs:501-580), statistics on the GPU.  The
 // stride bug (§0.1-12) makes index i read record i >> 2: a distributed rank
 // first fetches the records [ev_a, ev_b) its indices read from their owners.
@@ -1990,12 +2065,16 @@ void Solver::check_evolution() {
     gbase = topo.c0;
     rec0 = ev_a;
   }
-  launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, red.U, partial_d, pstride, stream);
-  double* out5 = partial_d + 5 * (size_t)pstride;
-  launch_evolution_final(combine_d(partial_d, 5), out5, stream);
-  check_launch("check_evolution");
   double tot[5];
-  CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
+  if (ref_red) {
+    evolution_reference(tot);
+  } else {
+    launch_evolution_partial(S(), prev, have_prev ? 1 : 0, N, var, gbase, rec0, red.U, partial_d, pstride, stream);
+    double* out5 = partial_d + 5 * (size_t)pstride;
+    launch_evolution_final(combine_d(partial_d, 5), out5, stream);
+    check_launch("check_evolution");
+    CFD_HIP(hipMemcpyAsync(tot, out5, sizeof(tot), hipMemcpyDeviceToHost, stream));
+  }
   copy_state(S(), prev, 0, N, stream);
   sync();
   const double nn = (double)NG;

@@ -321,6 +321,24 @@ struct Solver {
   uint32_t pstride = 0;          // unit partials per vector (nunits rounded up to 4: 16-byte loads)
   float* partial = nullptr;      // [(m+1) * pstride] chunk partials (256 cells each)
   float* partial_n = nullptr;    // [nchunks]
+  // reference reduction order (test mode, cfd_debug_reference_reductions): the
+  // reference's 64-DOF group partials and finishing orders instead of the
+  // canonical tree, one GPU only -- the bits of the reference's own kernels
+  // (tests/test_gpu_wgsl_pin.py)
+  bool ref_red = false;
+  uint32_t ref_ng = 0;           // ceil(3N / 64) groups
+  float* ref_part = nullptr;     // [(m+1) * ref_ng] CGS dot group partials
+  float* ref_norm = nullptr;     // [ref_ng] norm group partials
+  void set_reference_reductions(bool on);
+  void evolution_reference(double tot[5]);
+  RedSrc ref_src(const float* part, int order) const {
+    RedSrc r;
+    r.p = part;
+    r.stride = ref_ng;
+    r.nchunks = ref_ng;
+    r.order = (uint32_t)order;
+    return r;
+  }
   double* partial_d = nullptr;   // [5 * pstride] check_evolution
   float* dsc = nullptr;          // device scalars
   float* H = nullptr;

@@ -1,4 +1,4 @@
-"""HIP kernels vs the REFERENCE'S OWN SHADERS (tests/golden/wgsl_ref.npz).
+"""The HIP path vs the REFERENCE'S OWN SHADERS (tests/golden/wgsl_ref.npz).
 
 prepare_coupled.wgsl + coupled_assembly_merged.wgsl, executed on the CPU from
 the reference's source (tests/golden/make_wgsl_golden.py, schedule B: the
@@ -6,7 +6,12 @@ whole dispatch resident -- prepare's neighbour reads see the pre-kernel
 state), on a random state for every scheme / time scheme: k_prepare and
 k_assemble through the C ABI must give the same bits in every output buffer
 (fluxes, gradients, d_p, the coupled CSR values in the reference's order, rhs,
-the scalar pressure matrix, the diagonal inverses).  No oracle in between."""
+the scalar pressure matrix, the diagonal inverses).  No oracle in between.
+
+Whole steps: with cfd_debug_reference_reductions the HIP path sums like the
+reference (64-DOF workgroup trees, serial / strided finishing sums, serial
+f64 check_evolution) and must then give, step by step, the bits of the
+reference's shaders under schedule B -- again with no oracle in between."""
 import os
 
 import numpy as np
@@ -49,3 +54,48 @@ def test_hip_kernels_equal_reference_shaders(scheme, time_scheme):
             ref = z[f"{key}/{k}"]
             assert v.shape == ref.shape, k
             assert np.array_equal(v, ref), f"{key} {k}: max diff {np.abs(v - ref).max()}"
+
+
+def _b_cases():
+    from tests.golden.make_wgsl_golden import cases
+    return [c for c in cases() if "B" in c[5]]
+
+
+@pytest.mark.parametrize("name", [c[0] for c in _b_cases()])
+def test_hip_reference_order_equals_reference_kernels(name):
+    """Whole steps: the HIP path with the reference's reduction order
+    (cfd_debug_reference_reductions) == the reference's eight shaders run
+    with the whole dispatch resident (fixture schedule B), bit for bit at
+    every step -- fields (SHA-256 of the f32 bytes), FGMRES iteration counts,
+    outer residuals, the linear residual and the stop counters -- on the
+    reference's own tests (amg_test, coupled_schemes), the fixed 3 x 10
+    schedule and the 10 k-cell Voronoi channel (BASELINE configs[0])."""
+    from cfd2_amd import default_config
+    from tests.golden.make_wgsl_golden import digest, info_vec
+    _, mk, setup, kw, steps, _ = [c for c in _b_cases() if c[0] == name][0]
+    mesh = mk()
+    g = GpuSolver(mesh, config=default_config(**kw))
+    g.debug_reference_reductions(True)
+    setup(g, mesh)
+    with np.load(FIX) as z:
+        for k in range(steps):
+            g.step()
+            assert digest(g) == str(z[f"{name}/B/digests"][k]), f"{name} step {k}: fields differ from the reference"
+            np.testing.assert_array_equal(info_vec(g), z[f"{name}/B/info"][k], err_msg=f"{name} step {k}")
+
+
+def test_reference_order_switches_back_to_canonical():
+    """the canonical mode stays the default; switching back restores it"""
+    from tests.meshes import backwards_step
+    from tests.oracle_py import OracleSolver
+    from tests.test_oracle import setup_amg_test
+    mesh = backwards_step()
+    g = GpuSolver(mesh)
+    o = OracleSolver(mesh)
+    for s in (g, o):
+        setup_amg_test(s, mesh, 1)
+    g.debug_reference_reductions(True)
+    g.debug_reference_reductions(False)
+    for s in (g, o):
+        s.step()
+    assert np.array_equal(g.get_p(), o.get_p()) and np.array_equal(g.get_u(), o.get_u())
