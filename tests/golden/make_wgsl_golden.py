@@ -19,7 +19,8 @@ Plus the kernel-level case: prepare_coupled + coupled_assembly_merged under
 B on a random state, every output buffer (no reduction inside: equal to the
 oracle's canonical mode, flags 0).
 
-Run:  python -m tests.golden.make_wgsl_golden   (a few minutes)
+Run:  python -m tests.golden.make_wgsl_golden        (≈ 20 min)
+      python -m tests.golden.make_wgsl_golden --c1   (BASELINE configs[1]: wgsl_ref_c1.npz)
 """
 import hashlib
 import os
@@ -141,6 +142,39 @@ def kernel_case(scheme, time_scheme):
                 diag_v_inv=r.diag_v.f.copy(), diag_p_inv=r.diag_p.f.copy())
 
 
+def c1_setup(s, mesh):  # tests/test_gpu_parity.py::test_c1_scale_parity_and_true_residual
+    s.set_dt(1e-3)
+    s.set_viscosity(0.01)
+    s.set_density(1.0)
+    s.set_alpha_u(0.7)
+    s.set_alpha_p(0.3)
+    s.set_precond_type(1)
+    s.initialize_history()
+
+
+def c1_mesh():
+    from tests.meshes import bench_mesh
+    return bench_mesh(0.001723, 100)
+
+
+# BASELINE configs[1] (1.0 M cells, the bench geometry and physics), schedule B
+# only, 3 steps of 2 Picard x 6 FGMRES: every C1-only kernel form of the HIP
+# path (paired AMG levels, the blob tail, 16-bit ELL levels) against the
+# reference's kernels.  Digests and statistics only (the fields are 16 MB).
+C1 = ("c1", c1_mesh, c1_setup, dict(convergence_lag=0, fixed_outer=2, fixed_inner=6), 3)
+
+
+def main_c1():
+    from tests import wgsl_ref
+    if not wgsl_ref.available():
+        raise SystemExit("the reference (/root/reference) is not present: fixtures cannot be regenerated here")
+    name, mk, setup, kw, steps = C1
+    t = time.time()
+    res = run_wgsl(name, mk, setup, kw, steps, "B")
+    print(f"{name} B: {time.time() - t:.1f} s, info {res['info'][-1].tolist()}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "wgsl_ref_c1.npz"), **{f"{name}/B/{k}": v for k, v in res.items()})
+
+
 def main():
     from tests import wgsl_ref
     if not wgsl_ref.available():
@@ -161,4 +195,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main_c1() if "--c1" in sys.argv else main()

@@ -99,3 +99,22 @@ def test_reference_order_switches_back_to_canonical():
     for s in (g, o):
         s.step()
     assert np.array_equal(g.get_p(), o.get_p()) and np.array_equal(g.get_u(), o.get_u())
+
+
+def test_hip_reference_order_equals_reference_kernels_c1():
+    """BASELINE configs[1] scale: the C1-only kernel forms (the paired AMG
+    levels down and up, the blob tail, 16-bit ELL levels, the nontemporal
+    variants) in the reference reduction order == the reference's kernels
+    (tests/golden/wgsl_ref_c1.npz) at every step"""
+    from cfd2_amd import default_config
+    from tests.golden.make_wgsl_golden import C1, digest, info_vec
+    name, mk, setup, kw, steps = C1
+    mesh = mk()
+    g = GpuSolver(mesh, config=default_config(**kw))
+    g.debug_reference_reductions(True)
+    setup(g, mesh)
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "wgsl_ref_c1.npz")) as z:
+        for k in range(steps):
+            g.step()
+            assert digest(g) == str(z[f"{name}/B/digests"][k]), f"C1 step {k}"
+            np.testing.assert_array_equal(info_vec(g), z[f"{name}/B/info"][k], err_msg=f"C1 step {k}")

@@ -284,3 +284,23 @@ def test_digest_is_field_bytes():
     for a in (np.ones((2, 2), F), np.zeros(2, F), np.zeros(2, F)):
         h.update(a.tobytes())
     assert digest(S()) == h.hexdigest()
+
+
+FIX_C1 = os.path.join(os.path.dirname(__file__), "golden", "wgsl_ref_c1.npz")
+
+
+def test_oracle_equals_reference_kernels_c1():
+    """BASELINE configs[1] (1.0 M cells, bench geometry and physics, 2 Picard
+    x 6 FGMRES, AMG with its 9-level hierarchy): oracle flags 4 == the
+    reference's kernels under B at every step"""
+    from tests.golden.make_wgsl_golden import C1
+    name, mk, setup, kw, steps = C1
+    mesh = mk()
+    o = OracleSolver(mesh, config=default_config(**kw))
+    o.set_semantics(4)
+    setup(o, mesh)
+    with np.load(FIX_C1) as z:
+        for k in range(steps):
+            o.step()
+            assert digest(o) == str(z[f"{name}/B/digests"][k]), f"C1 step {k}"
+            np.testing.assert_array_equal(info_vec(o), z[f"{name}/B/info"][k], err_msg=f"C1 step {k}")
