@@ -189,7 +189,7 @@ EXPORTED = [
     "cfd_get_step_info", "cfd_set_stop_state", "cfd_num_cells", "cfd_num_faces", "cfd_state_save", "cfd_state_load", "cfd_synchronize",
     "cfd_group_state_save", "cfd_profile_enable", "cfd_profile_reset",
     "cfd_profile_smoother", "cfd_graph_enable", "cfd_graph_stats", "cfd_amg_levels", "cfd_step_algorithmic_bytes", "cfd_smoother_layout_bytes", "cfd_step_layout_bytes", "cfd_debug_buffer",
-    "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_reference_reductions", "cfd_debug_amg_info",
+    "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_reference_semantics", "cfd_debug_amg_info",
     "cfd_dist_unique_id", "cfd_solver_create_dist", "cfd_solver_create_dist_host", "cfd_group_create",
     "cfd_group_step",
     "cfd_dist_info", "cfd_dist_plan", "cfd_debug_rccl_selftest", "cfd_debug_comm_watchdog", "cfd_dist_comm_stats",

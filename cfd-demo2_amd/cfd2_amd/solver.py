@@ -68,7 +68,7 @@ def _bind():
     L.cfd_debug_buffer_len.restype = C.c_size_t
     L.cfd_debug_buffer.argtypes = [_vp, C.c_int32, C.POINTER(C.c_float), C.c_size_t]
     L.cfd_debug_prepare_assemble.argtypes = [_vp, C.c_int32]
-    L.cfd_debug_reference_reductions.argtypes = [_vp, C.c_int32]
+    L.cfd_debug_reference_semantics.argtypes = [_vp, C.c_int32]
     L.cfd_debug_amg_info.argtypes = [_vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]
     u8p = C.POINTER(C.c_uint8)
     u32p = C.POINTER(C.c_uint32)
@@ -365,10 +365,11 @@ class GpuSolver:
     def debug_prepare_assemble(self, assemble=True):
         self._call("cfd_debug_prepare_assemble", 1 if assemble else 0)
 
-    def debug_reference_reductions(self, on=True):
-        """Test mode: the reference's own reduction order instead of the
-        canonical tree (cfd_debug_reference_reductions; one GPU)."""
-        self._call("cfd_debug_reference_reductions", 1 if on else 0)
+    def debug_reference_semantics(self, flags):
+        """Test mode: the reference's own semantics (oracle flag bits 1 / 4 /
+        8) instead of the canonical resolutions (cfd_debug_reference_semantics;
+        one GPU)."""
+        self._call("cfd_debug_reference_semantics", int(flags))
 
     def comm_stats(self, reset=False) -> dict:
         """Transport of this handle (RCCL: ncclCommCount / ncclCommUserRank),

@@ -2070,6 +2070,24 @@ __global__ void __launch_bounds__(kBlock) k_amg_smooth(const uint8_t* len, const
   Lk.w = w;
   *reinterpret_cast<float4*>(x_out + i0) = smooth4<D16, MODE, PRO, NT>(Lk, x, b, i0, xc);
 }
+// The reference's IN-PLACE smooth_op (amg.wgsl:24-50) under one legal
+// schedule (test mode, Solver::ref_inplace; oracle kSemInplaceSmoother): the
+// 64-row workgroups one after another, every row of a workgroup reading x
+// before any of them writes -- so rows of earlier workgroups are read new.
+// One block walks the row blocks in order; its 16 threads take 4 rows each
+// (smooth4: the same operations as k_amg_smooth).
+template <bool D16, int MODE>
+__global__ void __launch_bounds__(16) k_amg_smooth_ordered(AmgLevelDev L, float* x, const float* __restrict__ b) {
+  for (uint32_t b0 = 0; b0 < L.n; b0 += 64) {
+    const uint32_t i0 = b0 + 4 * threadIdx.x;
+    float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (i0 < L.n) o = smooth4<D16, MODE>(L, x, b, i0);
+    __syncthreads();  // the workgroup's reads complete
+    if (i0 < L.n) *reinterpret_cast<float4*>(x + i0) = o;
+    __syncthreads();  // visible to the next workgroup's reads
+  }
+}
+
 // the leading arguments of k_amg_smooth from a level image
 #define CFD_AMG_HEAD(L) \
   (L).len, (L).val, ((L).use16 ? (const void*)(L).col16 : (const void*)(L).col32), (L).r0, (L).r1, (L).r2, (L).r3, \
@@ -3206,6 +3224,12 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
                           (const float*)nullptr);
   else
     hipLaunchKernelGGL(fn, dim3(nb), dim3(kBlock), 0, s, CFD_AMG_HEAD(L), x, b, x_out, L, (const float*)nullptr);
+}
+void launch_amg_smooth_ordered(const AmgLevelDev& L, float* x, const float* b, hipStream_t s) {
+  if (L.n == 0) return;
+  auto fn = L.use16 ? (L.full ? k_amg_smooth_ordered<true, 1> : k_amg_smooth_ordered<true, 0>)
+                    : (L.full ? k_amg_smooth_ordered<false, 1> : k_amg_smooth_ordered<false, 0>);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(16), 0, s, L, x, b);
 }
 void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b, float* x_out,
                                hipStream_t s) {

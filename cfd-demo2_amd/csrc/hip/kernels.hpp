@@ -397,6 +397,9 @@ void launch_amg_smooth(const AmgLevelDev& L, const float* x, const float* b, flo
 // only read (single-GPU / replicated levels: every column an owned row)
 void launch_amg_smooth_prolong(const AmgLevelDev& L, const float* x, const float* xc, const float* b,
                                float* x_out, hipStream_t s);
+// test mode (reference semantics): the reference's in-place smoother with its
+// 64-row workgroups run in order (rows of a workgroup read before any writes)
+void launch_amg_smooth_ordered(const AmgLevelDev& L, float* x, const float* b, hipStream_t s);
 // pre-smoother of a level whose x is identically +0 (bit-identical to launch_amg_smooth then)
 void launch_amg_smooth_zero(const AmgLevelDev& L, const float* b, float* x_out, hipStream_t s);
 void launch_amg_residual(const AmgLevelDev& L, const float* x, const float* b, float* r,

@@ -294,9 +294,9 @@ cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble) {
   return guard([&] { s->s->debug_prepare_assemble(assemble != 0); });
 }
 
-cfd_status cfd_debug_reference_reductions(cfd_solver* s, int32_t on) {
+cfd_status cfd_debug_reference_semantics(cfd_solver* s, int32_t flags) {
   CHECK_S(s);
-  return guard([&] { s->s->set_reference_reductions(on != 0); });
+  return guard([&] { s->s->set_reference_semantics(flags); });
 }
 
 // ---------------------------------------------------------------- multi-GPU

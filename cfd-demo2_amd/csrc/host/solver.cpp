@@ -1431,6 +1431,10 @@ void Solver::v_cycle() {
   const int L = (int)levels.size();
   levels[0].x = p_sol;
   levels[0].b = temp_p;
+  if (ref_inplace || ref_clamp) {
+    v_cycle_reference();
+    return;
+  }
   const int D = dist() ? amg_g : 0;
   // the tail needs level >= 1 (level 0's x/b are bound per call) and is off
   // while the level-0 smoother is being timed on a one-level hierarchy
@@ -1646,15 +1650,52 @@ void Solver::precondition(int j, float* z) {
   });
 }
 
-void Solver::set_reference_reductions(bool on) {
-  if (on && dist()) throw std::invalid_argument("reference reduction order: one GPU only");
-  if (on && !ref_part) {
+void Solver::set_reference_semantics(int flags) {
+  if (flags & ~(1 | 4 | 8))
+    throw std::invalid_argument("reference semantics on the GPU: flags 1 (in-place smoother), 4 (reduction "
+                                "order), 8 (restrict clamp) only");
+  if (flags && dist()) throw std::invalid_argument("reference semantics: one GPU only");
+  if ((flags & 4) && !ref_part) {
     ref_ng = (uint32_t)((3 * (uint64_t)N + 63) / 64);
     ref_part = arena.alloc<float>((size_t)(m1 + 1) * ref_ng + 1);
     ref_norm = arena.alloc<float>((size_t)ref_ng + 1);
   }
-  drop_graphs();  // captured iterations hold the other order's launches
-  ref_red = on;
+  drop_graphs();  // captured iterations hold the other semantics' launches
+  ref_red = (flags & 4) != 0;
+  ref_inplace = (flags & 1) != 0;
+  ref_clamp = (flags & 8) != 0;
+}
+
+// amg.rs:666-770 dispatch by dispatch (test mode, flags 1 / 8): pre-smooth,
+// residual + restriction (+ the clamped rows' store onto the last coarse
+// entry), the coarse x cleared, 10 coarsest sweeps, prolongation +
+// post-smooth -- no fused forms, no tail kernel.  In place (flag 1) the
+// smoother runs its workgroups in order; else out-of-place Jacobi.
+void Solver::v_cycle_reference() {
+  const int L = (int)levels.size();
+  auto smooth = [&](int i) {
+    AmgGpuLevel& Lv = levels[i];
+    if (ref_inplace) {
+      launch_amg_smooth_ordered(Lv.dev, Lv.x, Lv.b, stream);
+    } else {
+      launch_amg_smooth(Lv.dev, Lv.x, Lv.b, Lv.xt, stream);
+      std::swap(Lv.x, Lv.xt);
+    }
+  };
+  for (int i = 0; i + 1 < L; ++i) {
+    AmgGpuLevel &F = levels[i], &C = levels[i + 1];
+    smooth(i);
+    launch_amg_residual(F.dev, F.x, F.b, F.r, stream);
+    launch_amg_restrict(F.dev, F.r, C.b, C.x, 0, 0, 0, stream);  // coarse b = R r, coarse x = 0
+    const uint32_t nc = C.dev.n;
+    if (ref_clamp && nc % 64 != 0) CFD_HIP(hipMemsetAsync(C.b + nc - 1, 0, sizeof(float), stream));
+  }
+  for (int s = 0; s < 10; ++s) smooth(L - 1);
+  for (int i = L - 2; i >= 0; --i) {
+    launch_amg_prolong(levels[i].dev, levels[i].x, levels[i + 1].x, stream);
+    smooth(i);
+  }
+  if (levels[0].x != p_sol) throw std::logic_error("AMG level-0 ping-pong parity (reference semantics)");
 }
 
 void Solver::norm_launch(const float* v, int mode, int slot) {

@@ -321,15 +321,22 @@ struct Solver {
   uint32_t pstride = 0;          // unit partials per vector (nunits rounded up to 4: 16-byte loads)
   float* partial = nullptr;      // [(m+1) * pstride] chunk partials (256 cells each)
   float* partial_n = nullptr;    // [nchunks]
-  // reference reduction order (test mode, cfd_debug_reference_reductions): the
-  // reference's 64-DOF group partials and finishing orders instead of the
-  // canonical tree, one GPU only -- the bits of the reference's own kernels
-  // (tests/test_gpu_wgsl_pin.py)
+  // reference semantics (test mode, cfd_debug_reference_semantics; the
+  // oracle's kSem* bits, one GPU only -- the bits of the reference's own
+  // kernels under a legal schedule, tests/test_gpu_wgsl_pin.py):
+  // ref_red (4) the reference's 64-DOF group partials and finishing orders
+  // instead of the canonical tree; ref_inplace (1) the in-place AMG smoother,
+  // 64-row workgroups in order; ref_clamp (8) restrict_residual's
+  // out-of-bounds rows under wgpu's Restrict policy (the last coarse rhs
+  // entry zeroed when n_c % 64 != 0).  1 / 8 run v_cycle_reference().
   bool ref_red = false;
+  bool ref_inplace = false;
+  bool ref_clamp = false;
+  void v_cycle_reference();
   uint32_t ref_ng = 0;           // ceil(3N / 64) groups
   float* ref_part = nullptr;     // [(m+1) * ref_ng] CGS dot group partials
   float* ref_norm = nullptr;     // [ref_ng] norm group partials
-  void set_reference_reductions(bool on);
+  void set_reference_semantics(int flags);
   void evolution_reference(double tot[5]);
   RedSrc ref_src(const float* part, int order) const {
     RedSrc r;

@@ -337,15 +337,20 @@ size_t cfd_debug_buffer_len(const cfd_solver* s, int32_t id);
 /* Runs only prepare_coupled (+ coupled_assembly_merged when assemble != 0) on
  * the current state without rotating the ring (kernel-level parity).        */
 cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble);
-/* Test mode: on != 0 replaces the canonical reduction tree by the reference's
- * own reduction order -- 64-DOF workgroup trees, then reduce_final's serial
- * sum (norms, gmres_ops.wgsl:241-293) or reduce_dots_cgs's strided lanes +
- * tree (CGS, gmres_cgs.wgsl:86-120), and check_evolution's serial f64 loops
- * (coupled_solver.rs:504-545) on the host.  With it the step gives the bits of
- * the reference's own WGSL kernels executed with the whole dispatch resident
- * (tests/test_gpu_wgsl_pin.py).  One GPU only (CFD_ERR_INVALID on a
- * distributed handle); slower (serial finishing sums); drops captured graphs. */
-cfd_status cfd_debug_reference_reductions(cfd_solver* s, int32_t on);
+/* Test mode: the reference's own semantics under a legal schedule instead of
+ * the canonical resolutions, with the oracle's flag bits
+ * (oracle_set_semantics): 4 the reference's reduction order -- 64-DOF
+ * workgroup trees, then reduce_final's serial sum (norms, gmres_ops.wgsl:
+ * 241-293) or reduce_dots_cgs's strided lanes + tree (CGS, gmres_cgs.wgsl:
+ * 86-120), and check_evolution's serial f64 loops (coupled_solver.rs:504-545)
+ * on the host; 1 the in-place AMG smoother (amg.wgsl:24-50) with its 64-row
+ * workgroups run in order; 8 restrict_residual's out-of-bounds rows
+ * (amg.rs:707-719) under wgpu's Restrict policy.  Flags 4 give the bits of the
+ * reference's WGSL kernels run with the whole dispatch resident, 13 those with
+ * the V-cycle's workgroups in order (tests/test_gpu_wgsl_pin.py).  Flag 2 (racy
+ * prepare reads) is oracle-only: CFD_ERR_INVALID, as on a distributed handle.
+ * Slow (serial sums / workgroups); drops captured graphs; 0 = canonical.    */
+cfd_status cfd_debug_reference_semantics(cfd_solver* s, int32_t flags);
 
 /* ------------------------------------------------------------------------ */
 /* Multi-GPU (the reference is single-GPU).  The mesh is split

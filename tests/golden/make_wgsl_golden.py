@@ -20,6 +20,7 @@ B on a random state, every output buffer (no reduction inside: equal to the
 oracle's canonical mode, flags 0).
 
 Run:  python -m tests.golden.make_wgsl_golden        (≈ 20 min)
+      python -m tests.golden.make_wgsl_golden --only=C   (one mode, the rest kept)
       python -m tests.golden.make_wgsl_golden --c1   (BASELINE configs[1]: wgsl_ref_c1.npz)
 """
 import hashlib
@@ -77,25 +78,32 @@ def cases():
         return bench_voronoi_channel()
     out = []
     for pc, tag in ((1, "amg"), (0, "jacobi")):
-        out.append((f"amg_test_{tag}", backwards_step, lambda s, m, pc=pc: setup_amg_test(s, m, pc), {}, 5, "AB"))
+        out.append((f"amg_test_{tag}", backwards_step, lambda s, m, pc=pc: setup_amg_test(s, m, pc), {}, 5,
+                    "ABC" if pc else "AB"))
     for sc, ts in ((0, 0), (1, 0), (2, 0), (0, 1)):
         out.append((f"schemes_s{sc}t{ts}", backwards_step,
                     lambda s, m, sc=sc, ts=ts: setup_schemes_test(s, m, sc, ts), {}, 2, "AB"))
     fixed = dict(convergence_lag=0, fixed_outer=3, fixed_inner=10)
     for pc, tag in ((1, "amg"), (0, "jacobi")):
-        out.append((f"fixed_{tag}", backwards_step, lambda s, m, pc=pc: setup_amg_test(s, m, pc), fixed, 3, "AB"))
-    out.append(("c0_voronoi", c0_mesh, c0_setup, dict(convergence_lag=0, fixed_outer=2, fixed_inner=8), 2, "B"))
+        out.append((f"fixed_{tag}", backwards_step, lambda s, m, pc=pc: setup_amg_test(s, m, pc), fixed, 3,
+                    "ABC" if pc else "AB"))
+    out.append(("c0_voronoi", c0_mesh, c0_setup, dict(convergence_lag=0, fixed_outer=2, fixed_inner=8), 2, "BC"))
     return out
 
 
-MODES = {"A": ("workgroups", "restrict", 15), "B": ("dispatch", "zero", 4)}
+# mode: (schedule, bounds, oracle flags, the V-cycle's own (schedule, bounds) or None)
+#   C: B for every dispatch but the V-cycle's, which run as in A -- the
+#      reference's in-place smoother and clamped restriction rows, the rest
+#      resident (oracle flags 13; the HIP path's reference-semantics mode 13)
+MODES = {"A": ("workgroups", "restrict", 15, None), "B": ("dispatch", "zero", 4, None),
+         "C": ("dispatch", "zero", 13, ("workgroups", "restrict"))}
 
 
 def run_wgsl(name, mk, setup, kw, steps, mode):
     from tests.wgsl_ref import WgslRefSolver
-    sched, bounds, _ = MODES[mode]
+    sched, bounds, _, amg = MODES[mode]
     mesh = mk()
-    s = WgslRefSolver(mesh, schedule=sched, bounds=bounds, **kw)
+    s = WgslRefSolver(mesh, schedule=sched, bounds=bounds, amg=amg, **kw)
     setup(s, mesh)
     res = {}
     digs, infos = [], []
@@ -175,24 +183,35 @@ def main_c1():
     np.savez_compressed(os.path.join(HERE, "wgsl_ref_c1.npz"), **{f"{name}/B/{k}": v for k, v in res.items()})
 
 
-def main():
+def main(only=None):
+    """only: regenerate just these modes, keeping the file's other arrays"""
     from tests import wgsl_ref
     if not wgsl_ref.available():
         raise SystemExit("the reference (/root/reference) is not present: fixtures cannot be regenerated here")
     out = {}
+    path = os.path.join(HERE, "wgsl_ref.npz")
+    if only and os.path.exists(path):
+        with np.load(path) as z:
+            out = {k: z[k] for k in z.files}
     for name, mk, setup, kw, steps, modes in cases():
         for mode in modes:
+            if only and mode not in only:
+                continue
             t = time.time()
             res = run_wgsl(name, mk, setup, kw, steps, mode)
             for k, v in res.items():
                 out[f"{name}/{mode}/{k}"] = v
             print(f"{name} {mode}: {time.time() - t:.1f} s, info {res['info'][-1].tolist()}", flush=True)
-    for sc, ts in ((0, 0), (1, 0), (2, 0), (0, 1)):
-        for k, v in kernel_case(sc, ts).items():
-            out[f"kernels_s{sc}t{ts}/{k}"] = v
-    np.savez_compressed(os.path.join(HERE, "wgsl_ref.npz"), **out)
-    print("wrote", os.path.join(HERE, "wgsl_ref.npz"), len(out), "arrays")
+    if not only:
+        for sc, ts in ((0, 0), (1, 0), (2, 0), (0, 1)):
+            for k, v in kernel_case(sc, ts).items():
+                out[f"kernels_s{sc}t{ts}/{k}"] = v
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
 
 
 if __name__ == "__main__":
-    main_c1() if "--c1" in sys.argv else main()
+    if "--c1" in sys.argv:
+        main_c1()
+    else:
+        main(only=[a[len("--only="):] for a in sys.argv if a.startswith("--only=")] or None)

@@ -8,7 +8,7 @@ k_assemble through the C ABI must give the same bits in every output buffer
 (fluxes, gradients, d_p, the coupled CSR values in the reference's order, rhs,
 the scalar pressure matrix, the diagonal inverses).  No oracle in between.
 
-Whole steps: with cfd_debug_reference_reductions the HIP path sums like the
+Whole steps: with cfd_debug_reference_semantics(4) the HIP path sums like the
 reference (64-DOF workgroup trees, serial / strided finishing sums, serial
 f64 check_evolution) and must then give, step by step, the bits of the
 reference's shaders under schedule B -- again with no oracle in between."""
@@ -56,32 +56,68 @@ def test_hip_kernels_equal_reference_shaders(scheme, time_scheme):
             assert np.array_equal(v, ref), f"{key} {k}: max diff {np.abs(v - ref).max()}"
 
 
-def _b_cases():
+def _gpu_cases():
+    """(case, mode) of the fixture the GPU can run: B (flags 4) and C (flags 13)"""
     from tests.golden.make_wgsl_golden import cases
-    return [c for c in cases() if "B" in c[5]]
+    return [(c[0], m) for c in cases() for m in c[5] if m in "BC"]
 
 
-@pytest.mark.parametrize("name", [c[0] for c in _b_cases()])
-def test_hip_reference_order_equals_reference_kernels(name):
-    """Whole steps: the HIP path with the reference's reduction order
-    (cfd_debug_reference_reductions) == the reference's eight shaders run
-    with the whole dispatch resident (fixture schedule B), bit for bit at
-    every step -- fields (SHA-256 of the f32 bytes), FGMRES iteration counts,
-    outer residuals, the linear residual and the stop counters -- on the
-    reference's own tests (amg_test, coupled_schemes), the fixed 3 x 10
+@pytest.mark.parametrize("name,mode", _gpu_cases())
+def test_hip_reference_semantics_equal_reference_kernels(name, mode):
+    """Whole steps: the HIP path in the reference-semantics test mode
+    (cfd_debug_reference_semantics with the mode's oracle flags: 4 -- the
+    reference's reduction order; 13 -- also the in-place AMG smoother with
+    its workgroups in order and restrict_residual's clamped rows) == the
+    reference's eight shaders run under the mode's schedule (fixture B: the
+    whole dispatch resident; C: the V-cycle's workgroups in order), bit for
+    bit at every step -- fields (SHA-256 of the f32 bytes), FGMRES iteration
+    counts, outer residuals, the linear residual and the stop counters -- on
+    the reference's own tests (amg_test, coupled_schemes), the fixed 3 x 10
     schedule and the 10 k-cell Voronoi channel (BASELINE configs[0])."""
     from cfd2_amd import default_config
-    from tests.golden.make_wgsl_golden import digest, info_vec
-    _, mk, setup, kw, steps, _ = [c for c in _b_cases() if c[0] == name][0]
+    from tests.golden.make_wgsl_golden import MODES, cases, digest, info_vec
+    _, mk, setup, kw, steps, _ = [c for c in cases() if c[0] == name][0]
     mesh = mk()
     g = GpuSolver(mesh, config=default_config(**kw))
-    g.debug_reference_reductions(True)
+    g.debug_reference_semantics(MODES[mode][2])
     setup(g, mesh)
     with np.load(FIX) as z:
         for k in range(steps):
             g.step()
-            assert digest(g) == str(z[f"{name}/B/digests"][k]), f"{name} step {k}: fields differ from the reference"
-            np.testing.assert_array_equal(info_vec(g), z[f"{name}/B/info"][k], err_msg=f"{name} step {k}")
+            assert digest(g) == str(z[f"{name}/{mode}/digests"][k]), f"{name}/{mode} step {k}: fields differ"
+            np.testing.assert_array_equal(info_vec(g), z[f"{name}/{mode}/info"][k], err_msg=f"{name}/{mode} step {k}")
+
+
+@pytest.mark.parametrize("flags", [1, 8, 9, 12, 13])
+def test_hip_reference_semantics_equal_oracle(flags):
+    """every combination the GPU offers == the oracle with the same flags
+    (amg_test setup, AMG, 2 steps of 2 x 5)"""
+    from cfd2_amd import default_config
+    from tests.golden.make_wgsl_golden import digest, info_vec
+    from tests.meshes import backwards_step
+    from tests.oracle_py import OracleSolver
+    from tests.test_oracle import setup_amg_test
+    mesh = backwards_step()
+    kw = dict(convergence_lag=0, fixed_outer=2, fixed_inner=5)
+    g = GpuSolver(mesh, config=default_config(**kw))
+    o = OracleSolver(mesh, config=default_config(**kw))
+    g.debug_reference_semantics(flags)
+    o.set_semantics(flags)
+    for s in (g, o):
+        setup_amg_test(s, mesh, 1)
+    for k in range(2):
+        for s in (g, o):
+            s.step()
+        assert digest(g) == digest(o), (flags, k)
+        np.testing.assert_array_equal(info_vec(g), info_vec(o))
+
+
+def test_reference_semantics_refuses_what_the_gpu_lacks():
+    from tests.meshes import backwards_step
+    g = GpuSolver(backwards_step())
+    for bad in (2, 16, 15):
+        with pytest.raises(Exception):
+            g.debug_reference_semantics(bad)
 
 
 def test_reference_order_switches_back_to_canonical():
@@ -94,8 +130,8 @@ def test_reference_order_switches_back_to_canonical():
     o = OracleSolver(mesh)
     for s in (g, o):
         setup_amg_test(s, mesh, 1)
-    g.debug_reference_reductions(True)
-    g.debug_reference_reductions(False)
+    g.debug_reference_semantics(13)
+    g.debug_reference_semantics(0)
     for s in (g, o):
         s.step()
     assert np.array_equal(g.get_p(), o.get_p()) and np.array_equal(g.get_u(), o.get_u())
@@ -111,7 +147,7 @@ def test_hip_reference_order_equals_reference_kernels_c1():
     name, mk, setup, kw, steps = C1
     mesh = mk()
     g = GpuSolver(mesh, config=default_config(**kw))
-    g.debug_reference_reductions(True)
+    g.debug_reference_semantics(4)
     setup(g, mesh)
     with np.load(os.path.join(os.path.dirname(__file__), "golden", "wgsl_ref_c1.npz")) as z:
         for k in range(steps):

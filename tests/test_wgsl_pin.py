@@ -134,7 +134,7 @@ from tests import wgsl_ref  # noqa: E402
 
 
 @pytest.mark.skipif(not wgsl_ref.available(), reason="/root/reference is present only in the build container")
-@pytest.mark.parametrize("mode", ["A", "B"])
+@pytest.mark.parametrize("mode", ["A", "B", "C"])
 def test_live_reference_kernels(mode):
     """re-runs the reference shaders now (1 step of 2 Picard x 4 FGMRES, AMG,
     amg_test setup) against the oracle in the matching semantics"""
@@ -142,8 +142,8 @@ def test_live_reference_kernels(mode):
     from tests.test_oracle import setup_amg_test
     mesh = backwards_step()
     kw = dict(convergence_lag=0, fixed_outer=2, fixed_inner=4)
-    sched, bounds, flags = MODES[mode]
-    r = wgsl_ref.WgslRefSolver(mesh, schedule=sched, bounds=bounds, **kw)
+    sched, bounds, flags, amg = MODES[mode]
+    r = wgsl_ref.WgslRefSolver(mesh, schedule=sched, bounds=bounds, amg=amg, **kw)
     o = OracleSolver(mesh, config=default_config(**kw))
     o.set_semantics(flags)
     for s in (r, o):

@@ -86,13 +86,18 @@ class WgslRefSolver(refpy.RefSolver):
     """refpy.RefSolver's surface; step() runs the reference's WGSL."""
 
     def __init__(self, mesh, fixed_outer=0, fixed_inner=0, convergence_lag=1, schedule="workgroups",
-                 bounds="restrict"):
+                 bounds="restrict", amg=None):
         """schedule / bounds: oracle/wgsl/wgsl_exec.py Dispatcher.dispatch --
         ("workgroups", "restrict") is the schedule of oracle flags 15,
         ("dispatch", "zero") the one of oracle flags 4 (reference reduction
-        order, every other resolution canonical)."""
+        order, every other resolution canonical).  amg: (schedule, bounds) of
+        the V-cycle's dispatches alone (every dispatch may run under its own
+        schedule): ("workgroups", "restrict") with the rest ("dispatch",
+        "zero") is oracle flags 13 (in-place smoother, restrict clamp,
+        reference reductions; prepare's reads the snapshot)."""
         super().__init__(mesh, fixed_outer=fixed_outer, fixed_inner=fixed_inner, convergence_lag=convergence_lag)
         self.schedule, self.bounds = schedule, bounds
+        self.amg_sched = amg or (schedule, bounds)
         M = self.M
         N, nf = M.N, len(M.area)
         self.N = N
@@ -193,7 +198,10 @@ class WgslRefSolver(refpy.RefSolver):
 
     # ------------------------------------------------------------ plumbing
     def _run(self, D, entry, bindings, groups):
-        D.dispatch(entry, bindings, groups, schedule=self.schedule, bounds=self.bounds)
+        if D is _SHADERS.get("amg"):
+            D.dispatch(entry, bindings, groups, schedule=self.amg_sched[0], bounds=self.amg_sched[1])
+        else:
+            D.dispatch(entry, bindings, groups, schedule=self.schedule, bounds=self.bounds)
 
     def _write_constants(self):
         c = self.c
