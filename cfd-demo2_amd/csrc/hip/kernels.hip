@@ -373,10 +373,11 @@ constexpr int kRedFinalThreads = CFD_RED_FINAL_THREADS;
 // ---------------------------------------------------------------------------
 // prepare_coupled.wgsl:63-348 — Rhie-Chow face flux, d_p, Green-Gauss grads.
 // Snapshot semantics: reads st (pre-kernel), writes d_p/grad_p to dp_out/gp_out.
-__global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
-  const uint32_t i = row_id();
+// prepare_cell: cell i's face fluxes (stored) and its new d_p, grad_p, grad_u,
+// grad_v (returned; k_prepare stores them, k_prepare_ordered after a barrier)
+__device__ __forceinline__ void prepare_cell(const PrepareArgs& a, uint32_t i, float& dp_new, float2& gp_new,
+                                             float2& gu_new, float2& gv_new) {
   const uint32_t N = a.N;
-  if (i >= N) return;
   const cfd_constants c = a.c;
   const FaceSlots fs = a.fs;
   const float vol = a.vol[i];
@@ -484,10 +485,51 @@ __global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
     gvx += vfv * nx * area;
     gvy += vfv * ny * area;
   }
-  a.dp_out[i] = (fabsf(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
-  a.gp_out[i] = make_float2(gpx / vol, gpy / vol);
-  a.grad_u[i] = make_float2(gux / vol, guy / vol);
-  a.grad_v[i] = make_float2(gvx / vol, gvy / vol);
+  dp_new = (fabsf(diag_coeff) > 1e-20f) ? vol / diag_coeff : 0.0f;
+  gp_new = make_float2(gpx / vol, gpy / vol);
+  gu_new = make_float2(gux / vol, guy / vol);
+  gv_new = make_float2(gvx / vol, gvy / vol);
+}
+__global__ void __launch_bounds__(kBlock) k_prepare(PrepareArgs a) {
+  const uint32_t i = row_id();
+  if (i >= a.N) return;
+  float dp;
+  float2 gp, gu, gv;
+  prepare_cell(a, i, dp, gp, gu, gv);
+  a.dp_out[i] = dp;
+  a.gp_out[i] = gp;
+  a.grad_u[i] = gu;
+  a.grad_v[i] = gv;
+}
+// The reference's RACY prepare (prepare_coupled.wgsl:140-143 vs :328-337)
+// under one legal schedule (test mode, Solver::ref_racy; oracle
+// kSemRacyPrepare): the 64-cell workgroups one after another, d_p / grad_p
+// written in place (dp_out == st.dp, gp_out == st.gp), every cell of a
+// workgroup reading before any writes -- later workgroups read the new values.
+__global__ void __launch_bounds__(64) k_prepare_ordered(PrepareArgs a) {
+  for (uint32_t b0 = 0; b0 < a.N; b0 += 64) {
+    const uint32_t i = b0 + threadIdx.x;
+    float dp = 0.0f;
+    float2 gp = make_float2(0.0f, 0.0f), gu = gp, gv = gp;
+    if (i < a.N) prepare_cell(a, i, dp, gp, gu, gv);
+    __syncthreads();  // the workgroup's reads complete
+    if (i < a.N) {
+      a.dp_out[i] = dp;
+      a.gp_out[i] = gp;
+      a.grad_u[i] = gu;
+      a.grad_v[i] = gv;
+    }
+    __syncthreads();  // visible to the next workgroup
+  }
+}
+// the assembly reads fluxes[face] as the OWNER stored it (coupled_assembly_
+// merged.wgsl:153): a non-owner slot takes -(owner's flux) -- the same bits as
+// its own computation under snapshot reads, not under the racy ones
+__global__ void __launch_bounds__(kBlock) k_flux_mirror(float* flux_s, const int32_t* mirror, uint32_t S) {
+  const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S) return;
+  const int32_t m = mirror[e];
+  if (m >= 0) flux_s[e] = -flux_s[m];  // owner slots (m < 0) are only read
 }
 
 // coupled_assembly_merged.wgsl:70-463
@@ -3054,6 +3096,11 @@ __global__ void k_max_combine(const uint32_t* __restrict__ gathered, int R, uint
 // ------------------------------- launchers ----------------------------------
 void launch_prepare(const PrepareArgs& a, hipStream_t s) {
   if (a.N) hipLaunchKernelGGL(k_prepare, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);
+}
+void launch_prepare_ordered(const PrepareArgs& a, const int32_t* mirror, uint32_t slots, hipStream_t s) {
+  if (!a.N) return;
+  hipLaunchKernelGGL(k_prepare_ordered, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_flux_mirror, dim3((slots + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a.flux_s, mirror, slots);
 }
 void launch_assemble(const AssembleArgs& a, hipStream_t s) {
   if (a.N) hipLaunchKernelGGL(k_assemble, dim3(grid_for(a.N)), dim3(kBlock), 0, s, a);

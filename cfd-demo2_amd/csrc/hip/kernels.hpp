@@ -317,6 +317,11 @@ struct TailBlobLevel {
 
 // ---------------- launch wrappers (kernels.hip) ----------------
 void launch_prepare(const PrepareArgs& a, hipStream_t s);
+// test mode (reference semantics): the reference's racy prepare with its 64-cell
+// workgroups in order, d_p / grad_p in place (a.dp_out / a.gp_out = a.st's),
+// then every non-owner face slot e takes -flux_s[mirror[e]] (mirror[e] < 0:
+// owner or boundary slot, kept)
+void launch_prepare_ordered(const PrepareArgs& a, const int32_t* mirror, uint32_t slots, hipStream_t s);
 void launch_assemble(const AssembleArgs& a, hipStream_t s);
 // writes per-block max bit patterns to blockmax[2*nb] and the final pair to maxbits[0..1]
 // (and to host_out[0..1], a device view of pinned host memory, when non-null)

@@ -514,6 +514,13 @@ void Solver::prepare() {
   a.flux_s = flux_s;
   a.grad_u = grad_u;
   a.grad_v = grad_v;
+  if (ref_racy) {  // test mode: in place, workgroups in order, the owners' fluxes
+    a.dp_out = S().dp;
+    a.gp_out = S().gp;
+    launch_prepare_ordered(a, d_flux_mirror, (uint32_t)((size_t)topo.wf * N), stream);
+    check_launch("prepare (reference semantics)");
+    return;
+  }
   launch_prepare(a, stream);
   check_launch("prepare");
   // commit d_p / grad_p (snapshot semantics): swap the scratch into the slot
@@ -1651,10 +1658,26 @@ void Solver::precondition(int j, float* z) {
 }
 
 void Solver::set_reference_semantics(int flags) {
-  if (flags & ~(1 | 4 | 8))
-    throw std::invalid_argument("reference semantics on the GPU: flags 1 (in-place smoother), 4 (reduction "
-                                "order), 8 (restrict clamp) only");
+  if (flags & ~(1 | 2 | 4 | 8))
+    throw std::invalid_argument("reference semantics on the GPU: flags 1 (in-place smoother), 2 (racy prepare), "
+                                "4 (reduction order), 8 (restrict clamp) only");
   if (flags && dist()) throw std::invalid_argument("reference semantics: one GPU only");
+  if ((flags & 2) && !d_flux_mirror) {  // each non-owner face slot -> the owner's slot of that face
+    const size_t S = (size_t)topo.wf * N;
+    std::vector<int64_t> owner_slot(topo.fs_face.empty() ? 0 : *std::max_element(topo.fs_face.begin(),
+                                                                                    topo.fs_face.end()) + 1,
+                                    -1);
+    for (size_t e = 0; e < S; ++e)
+      if (topo.fs_face[e] != 0xFFFFFFFFu && (topo.fs_meta[e] & kMetaOwner)) owner_slot[topo.fs_face[e]] = (int64_t)e;
+    std::vector<int32_t> mirror(S, -1);
+    for (size_t e = 0; e < S; ++e)
+      if (topo.fs_face[e] != 0xFFFFFFFFu && topo.fs_other[e] != kNoCell && !(topo.fs_meta[e] & kMetaOwner)) {
+        const int64_t o = owner_slot[topo.fs_face[e]];
+        if (o < 0) throw std::logic_error("reference semantics: a face without its owner's slot");
+        mirror[e] = (int32_t)o;
+      }
+    d_flux_mirror = arena.upload(mirror, stream);
+  }
   if ((flags & 4) && !ref_part) {
     ref_ng = (uint32_t)((3 * (uint64_t)N + 63) / 64);
     ref_part = arena.alloc<float>((size_t)(m1 + 1) * ref_ng + 1);
@@ -1664,6 +1687,7 @@ void Solver::set_reference_semantics(int flags) {
   ref_red = (flags & 4) != 0;
   ref_inplace = (flags & 1) != 0;
   ref_clamp = (flags & 8) != 0;
+  ref_racy = (flags & 2) != 0;
 }
 
 // amg.rs:666-770 dispatch by dispatch (test mode, flags 1 / 8): pre-smooth,

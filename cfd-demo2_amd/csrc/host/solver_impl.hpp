@@ -325,6 +325,7 @@ struct Solver {
   // oracle's kSem* bits, one GPU only -- the bits of the reference's own
   // kernels under a legal schedule, tests/test_gpu_wgsl_pin.py):
   // ref_red (4) the reference's 64-DOF group partials and finishing orders
+  // (ref_racy, flag 2, below)
   // instead of the canonical tree; ref_inplace (1) the in-place AMG smoother,
   // 64-row workgroups in order; ref_clamp (8) restrict_residual's
   // out-of-bounds rows under wgpu's Restrict policy (the last coarse rhs
@@ -332,6 +333,10 @@ struct Solver {
   bool ref_red = false;
   bool ref_inplace = false;
   bool ref_clamp = false;
+  // ref_racy (2): the racy prepare, 64-cell workgroups in order, in place;
+  // d_flux_mirror[e]: the owner's slot of non-owner face slot e (else -1)
+  bool ref_racy = false;
+  int32_t* d_flux_mirror = nullptr;
   void v_cycle_reference();
   uint32_t ref_ng = 0;           // ceil(3N / 64) groups
   float* ref_part = nullptr;     // [(m+1) * ref_ng] CGS dot group partials

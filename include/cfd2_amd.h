@@ -344,12 +344,16 @@ cfd_status cfd_debug_prepare_assemble(cfd_solver* s, int32_t assemble);
  * 241-293) or reduce_dots_cgs's strided lanes + tree (CGS, gmres_cgs.wgsl:
  * 86-120), and check_evolution's serial f64 loops (coupled_solver.rs:504-545)
  * on the host; 1 the in-place AMG smoother (amg.wgsl:24-50) with its 64-row
- * workgroups run in order; 8 restrict_residual's out-of-bounds rows
- * (amg.rs:707-719) under wgpu's Restrict policy.  Flags 4 give the bits of the
- * reference's WGSL kernels run with the whole dispatch resident, 13 those with
- * the V-cycle's workgroups in order (tests/test_gpu_wgsl_pin.py).  Flag 2 (racy
- * prepare reads) is oracle-only: CFD_ERR_INVALID, as on a distributed handle.
- * Slow (serial sums / workgroups); drops captured graphs; 0 = canonical.    */
+ * workgroups run in order; 2 prepare_coupled's racy neighbour reads
+ * (prepare_coupled.wgsl:140-143 vs :328-337), its 64-cell workgroups in order,
+ * the assembly reading each face's flux as its owner stored it; 8
+ * restrict_residual's out-of-bounds rows (amg.rs:707-719) under wgpu's
+ * Restrict policy.  Flags 4 give the bits of the reference's WGSL kernels run
+ * with the whole dispatch resident, 13 those with the V-cycle's workgroups in
+ * order, 15 those with every dispatch's workgroups in order
+ * (tests/test_gpu_wgsl_pin.py).  Other bits, or a distributed handle:
+ * CFD_ERR_INVALID.  Slow (serial sums / workgroups); drops captured graphs;
+ * 0 = canonical.                                                            */
 cfd_status cfd_debug_reference_semantics(cfd_solver* s, int32_t flags);
 
 /* ------------------------------------------------------------------------ */

@@ -57,9 +57,9 @@ def test_hip_kernels_equal_reference_shaders(scheme, time_scheme):
 
 
 def _gpu_cases():
-    """(case, mode) of the fixture the GPU can run: B (flags 4) and C (flags 13)"""
+    """(case, mode) of the fixture: A (flags 15), B (flags 4), C (flags 13)"""
     from tests.golden.make_wgsl_golden import cases
-    return [(c[0], m) for c in cases() for m in c[5] if m in "BC"]
+    return [(c[0], m) for c in cases() for m in c[5]]
 
 
 @pytest.mark.parametrize("name,mode", _gpu_cases())
@@ -67,9 +67,11 @@ def test_hip_reference_semantics_equal_reference_kernels(name, mode):
     """Whole steps: the HIP path in the reference-semantics test mode
     (cfd_debug_reference_semantics with the mode's oracle flags: 4 -- the
     reference's reduction order; 13 -- also the in-place AMG smoother with
-    its workgroups in order and restrict_residual's clamped rows) == the
-    reference's eight shaders run under the mode's schedule (fixture B: the
-    whole dispatch resident; C: the V-cycle's workgroups in order), bit for
+    its workgroups in order and restrict_residual's clamped rows; 15 -- also
+    prepare's racy reads with its workgroups in order) == the reference's
+    eight shaders run under the mode's schedule (fixture B: the whole
+    dispatch resident; C: the V-cycle's workgroups in order; A: every
+    dispatch's workgroups in order), bit for
     bit at every step -- fields (SHA-256 of the f32 bytes), FGMRES iteration
     counts, outer residuals, the linear residual and the stop counters -- on
     the reference's own tests (amg_test, coupled_schemes), the fixed 3 x 10
@@ -88,7 +90,7 @@ def test_hip_reference_semantics_equal_reference_kernels(name, mode):
             np.testing.assert_array_equal(info_vec(g), z[f"{name}/{mode}/info"][k], err_msg=f"{name}/{mode} step {k}")
 
 
-@pytest.mark.parametrize("flags", [1, 8, 9, 12, 13])
+@pytest.mark.parametrize("flags", [1, 2, 3, 6, 8, 9, 12, 13, 15])
 def test_hip_reference_semantics_equal_oracle(flags):
     """every combination the GPU offers == the oracle with the same flags
     (amg_test setup, AMG, 2 steps of 2 x 5)"""
@@ -115,7 +117,7 @@ def test_hip_reference_semantics_equal_oracle(flags):
 def test_reference_semantics_refuses_what_the_gpu_lacks():
     from tests.meshes import backwards_step
     g = GpuSolver(backwards_step())
-    for bad in (2, 16, 15):
+    for bad in (16, 17, 32, 31):
         with pytest.raises(Exception):
             g.debug_reference_semantics(bad)
 
