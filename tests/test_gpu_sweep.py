@@ -70,7 +70,11 @@ def _case(seed):
     # round 6: every candidate AMG level pair in one launch, the tail off (so
     # that these small meshes have candidate pairs)
     pairs = rng.random() < 0.3
-    return kind, mesh, cfg, phys, nranks, useed, graph, pairs
+    # round 6: the reference-semantics test mode (one GPU; the oracle with the
+    # same flags): its reduction order, the in-place smoother / racy prepare
+    # with ordered workgroups, the clamped restrict rows
+    refsem = rng.choice([4, 13, 15, 1, 2, 8]) if rng.random() < 0.25 else 0
+    return kind, mesh, cfg, phys, nranks, useed, graph, pairs, refsem
 
 
 def _setup(s, mesh, phys, useed):
@@ -94,7 +98,7 @@ def _setup(s, mesh, phys, useed):
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
-    kind, mesh, cfg, phys, nranks, useed, graph, pairs = _case(seed)
+    kind, mesh, cfg, phys, nranks, useed, graph, pairs, refsem = _case(seed)
     # ranks own whole reduction segments (>= 256 cells): small meshes take fewer ranks
     nranks = min(nranks, max_ranks(mesh.num_cells()))
     monkeypatch.setenv("CFD_AMG_REPLICATE_ROWS", "200")  # distributed coarse levels on these small meshes
@@ -106,9 +110,15 @@ def test_random_case_parity(seed, monkeypatch):
     if nranks == 1 and graph:
         g.graph_enable(True)
     o = OracleSolver(mesh, config=default_config(**cfg), nranks=nranks)
+    if nranks > 1:
+        refsem = 0
+    if refsem:
+        g.debug_reference_semantics(refsem)
+        o.set_semantics(refsem)
     for s in (g, o):
         _setup(s, mesh, phys, useed)
-    ctx = f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}, graph={graph}, pairs={pairs}"
+    ctx = (f"seed {seed}: {kind} {mesh.num_cells()} cells, R={nranks}, {cfg}, {phys}, graph={graph}, pairs={pairs}, "
+           f"reference semantics {refsem}")
     for k in range(3):
         g.step()
         o.step()
