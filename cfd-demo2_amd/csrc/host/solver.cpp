@@ -1664,9 +1664,10 @@ void Solver::set_reference_semantics(int flags) {
   if (flags && dist()) throw std::invalid_argument("reference semantics: one GPU only");
   if ((flags & 2) && !d_flux_mirror) {  // each non-owner face slot -> the owner's slot of that face
     const size_t S = (size_t)topo.wf * N;
-    std::vector<int64_t> owner_slot(topo.fs_face.empty() ? 0 : *std::max_element(topo.fs_face.begin(),
-                                                                                    topo.fs_face.end()) + 1,
-                                    -1);
+    size_t nfaces = 0;  // unused slots hold 0xFFFFFFFF: not a face
+    for (size_t e = 0; e < S; ++e)
+      if (topo.fs_face[e] != 0xFFFFFFFFu) nfaces = std::max(nfaces, (size_t)topo.fs_face[e] + 1);
+    std::vector<int64_t> owner_slot(nfaces, -1);
     for (size_t e = 0; e < S; ++e)
       if (topo.fs_face[e] != 0xFFFFFFFFu && (topo.fs_meta[e] & kMetaOwner)) owner_slot[topo.fs_face[e]] = (int64_t)e;
     std::vector<int32_t> mirror(S, -1);
