@@ -7,15 +7,20 @@ against restatements of them (VERDICT r05 "Missing 1": parity unpinned).
 Nothing under cfd-demo2_amd/ imports this; bench.py and the GPU tests do not
 either.
 
-Execution model (one of the schedules the WGSL memory model allows, and the
-one the oracle's reference-semantics mode describes, oracle.cpp kSem*):
-  * workgroups run one after another in dispatch order (x fastest);
-  * the invocations of a workgroup run in lockstep, statement by statement,
-    as one 64-wide wavefront does: every lane evaluates a statement's
-    expressions (its loads) before any lane's store of that statement, and a
-    lane that leaves a loop early waits, masked, for the others;
-  * out-of-bounds indices are clamped to the last element (wgpu's default
-    `Restrict` bounds-check policy); when several lanes store to one address in
+Execution model -- two of the schedules the WGSL memory model allows, chosen
+per dispatch (Dispatcher.dispatch), and the ones the oracle's
+reference-semantics modes describe (oracle.cpp kSem*):
+  * schedule "workgroups": workgroups one after another in dispatch order (x
+    fastest), the invocations of a workgroup in lockstep, statement by
+    statement, as one 64-wide wavefront runs them: every lane evaluates a
+    statement's expressions (its loads) before any lane's store of that
+    statement, and a lane that leaves a loop early waits, masked, for the
+    others;
+  * schedule "dispatch": every workgroup resident and the whole dispatch in
+    that lockstep (all loads of a statement before any store);
+  * bounds "restrict": out-of-bounds indices clamp to the last element (wgpu's
+    `Restrict` policy); "zero": naga's ReadZeroSkipWrite (out-of-bounds loads
+    read 0, stores are dropped); when several lanes store to one address in
     one statement the highest lane's value remains.
 Arithmetic: f32 in IEEE single precision (numpy float32, round to nearest,
 no contraction into FMA), u32 / i32 wrapping, integer division by zero = the
