@@ -184,17 +184,18 @@ class WgslRefSolver(refpy.RefSolver):
         self._state_mem(1).u[:] = s
         self._state_mem(2).u[:] = s
 
-    def _fields(self, which):
+    def _fields(self):
+        """the current FluidState buffer as [N, 8] f32 (u, v, p, d_p, grad_p, grad_component)"""
         return self._state_mem(0).f.reshape(-1, 8)
 
     def get_u(self):
-        return self._fields(0)[:, 0:2].astype(np.float64)
+        return self._fields()[:, 0:2].astype(np.float64)
 
     def get_p(self):
-        return self._fields(0)[:, 2].astype(np.float64)
+        return self._fields()[:, 2].astype(np.float64)
 
     def get_d_p(self):
-        return self._fields(0)[:, 3].astype(np.float64)
+        return self._fields()[:, 3].astype(np.float64)
 
     # ------------------------------------------------------------ plumbing
     def _run(self, D, entry, bindings, groups):
