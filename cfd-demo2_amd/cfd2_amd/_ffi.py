@@ -186,7 +186,7 @@ EXPORTED = [
     "cfd_set_alpha_u", "cfd_set_density", "cfd_set_scheme", "cfd_set_time_scheme",
     "cfd_set_inlet_velocity", "cfd_set_ramp_time", "cfd_set_precond_type", "cfd_update_constants",
     "cfd_initialize_history", "cfd_step", "cfd_get_u", "cfd_get_p", "cfd_get_d_p",
-    "cfd_get_step_info", "cfd_set_stop_state", "cfd_num_cells", "cfd_num_faces", "cfd_state_save", "cfd_state_load", "cfd_synchronize",
+    "cfd_get_step_info", "cfd_set_stop_state", "cfd_set_n_outer_correctors", "cfd_num_cells", "cfd_num_faces", "cfd_state_save", "cfd_state_load", "cfd_synchronize",
     "cfd_group_state_save", "cfd_profile_enable", "cfd_profile_reset",
     "cfd_profile_smoother", "cfd_graph_enable", "cfd_graph_stats", "cfd_amg_levels", "cfd_step_algorithmic_bytes", "cfd_smoother_layout_bytes", "cfd_step_layout_bytes", "cfd_debug_buffer",
     "cfd_debug_buffer_len", "cfd_debug_prepare_assemble", "cfd_debug_reference_semantics", "cfd_debug_amg_info",

@@ -47,6 +47,7 @@ def _bind():
         getattr(L, n).argtypes = [_vp]
     L.cfd_get_step_info.argtypes = [_vp, C.POINTER(_ffi.StepInfo)]
     L.cfd_set_stop_state.argtypes = [_vp, C.c_int32, C.c_uint32, C.c_uint32]
+    L.cfd_set_n_outer_correctors.argtypes = [_vp, C.c_int32]
     L.cfd_num_cells.argtypes = [_vp]
     L.cfd_num_cells.restype = C.c_uint32
     L.cfd_num_faces.argtypes = [_vp]
@@ -112,6 +113,7 @@ class GpuSolver:
         # the library copies what it needs at creation: no reference to the mesh is kept
         cfg = config if config is not None else _ffi.default_config(**cfg_overrides)
         self._cfg = cfg
+        self._n_outer = int(cfg.n_outer_correctors)
         if _handle is None:
             view = mesh.view()
             h = _vp()
@@ -301,6 +303,15 @@ class GpuSolver:
     def steady_state_count(self, v): self._set_stop_field(steady_state_count=int(v))
     @property
     def outer_iterations(self) -> int: return int(self.step_info().outer_iterations)
+
+    # n_outer_correctors: a public field as well (structs.rs:238), read by every
+    # step (coupled_solver.rs:111); its initial value comes from the config
+    @property
+    def n_outer_correctors(self) -> int: return int(self._n_outer)
+    @n_outer_correctors.setter
+    def n_outer_correctors(self, v):
+        self._call("cfd_set_n_outer_correctors", int(v))
+        self._n_outer = int(v)
 
     # -- instrumentation --------------------------------------------------------
     def profile_enable(self, on=True): self._call("cfd_profile_enable", 1 if on else 0)
@@ -506,6 +517,12 @@ class GpuGroup:
     def degenerate_count(self): return self.ranks[0].degenerate_count
     @property
     def steady_state_count(self): return self.ranks[0].steady_state_count
+    @property
+    def n_outer_correctors(self): return self.ranks[0].n_outer_correctors
+    @n_outer_correctors.setter
+    def n_outer_correctors(self, v):
+        for r in self.ranks:
+            r.n_outer_correctors = v
 
 
 def dist_plan(mesh, nranks: int, rank: int) -> dict:

@@ -190,6 +190,12 @@ cfd_status cfd_set_stop_state(cfd_solver* s, int32_t should_stop, uint32_t degen
   s->s->info.steady_state_count = steady_state_count;
   return CFD_OK;
 }
+cfd_status cfd_set_n_outer_correctors(cfd_solver* s, int32_t n) {
+  CHECK_S(s);
+  if (n < 0) return set_error(CFD_ERR_INVALID, "n_outer_correctors < 0");
+  s->s->cfg.n_outer_correctors = n;  // read by every step (Solver::step)
+  return CFD_OK;
+}
 cfd_status cfd_state_save(cfd_solver* s, const char* path) {
   CHECK_S(s);
   if (!path) return set_error(CFD_ERR_INVALID, "null path");

@@ -231,6 +231,11 @@ cfd_status cfd_get_step_info(const cfd_solver* s, cfd_step_info* out);
  * with the same values (the counters are global).                          */
 cfd_status cfd_set_stop_state(cfd_solver* s, int32_t should_stop, uint32_t degenerate_count,
                               uint32_t steady_state_count);
+/* The reference's public field n_outer_correctors (structs.rs:238, 20 from
+ * init/mod.rs:144), read by every step_coupled (coupled_solver.rs:111: at
+ * least 10 Picard iterations) -- caller-writable between steps like the stop
+ * state; cfd_config.n_outer_correctors is its initial value.  n >= 0.       */
+cfd_status cfd_set_n_outer_correctors(cfd_solver* s, int32_t n);
 uint32_t cfd_num_cells(const cfd_solver* s);
 uint32_t cfd_num_faces(const cfd_solver* s);
 

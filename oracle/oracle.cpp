@@ -1676,6 +1676,11 @@ int oracle_set_stop_state(oracle_solver* s, int should_stop, uint32_t degenerate
   return 0;
 }
 
+int oracle_set_n_outer_correctors(oracle_solver* s, int n) {
+  s->cfg.n_outer_correctors = n;
+  return 0;
+}
+
 size_t oracle_debug_buffer_len(const oracle_solver* s, int id) {
   const size_t N = s->N;
   switch (id) {

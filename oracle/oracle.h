@@ -55,6 +55,7 @@ int oracle_get_d_p(oracle_solver* s, double* dp);
 int oracle_get_step_info(const oracle_solver* s, cfd_step_info* out);
 int oracle_set_stop_state(oracle_solver* s, int should_stop, uint32_t degenerate_count,
                           uint32_t steady_state_count);
+int oracle_set_n_outer_correctors(oracle_solver* s, int n);
 /* same buffer ids as cfd_debug_buffer */
 size_t oracle_debug_buffer_len(const oracle_solver* s, int id);
 int oracle_debug_buffer(oracle_solver* s, int id, float* out, size_t count);

@@ -63,8 +63,19 @@ int main(int argc, char** argv) {
     return 1;
   }
   CHECK(cfd_set_stop_state(s, 0, 0, 0));
+  /* n_outer_correctors is a public field too (structs.rs:238): 12 Picard
+   * iterations at most from the next step on; a negative count is refused */
+  CHECK(cfd_set_n_outer_correctors(s, 12));
+  if (cfd_set_n_outer_correctors(s, -1) != CFD_ERR_INVALID) {
+    fprintf(stderr, "negative n_outer_correctors accepted\n");
+    return 1;
+  }
   CHECK(cfd_step(s));
   CHECK(cfd_get_step_info(s, &info));
+  if (info.outer_iterations > 12) {
+    fprintf(stderr, "n_outer_correctors = 12 not applied: %u outer iterations\n", info.outer_iterations);
+    return 1;
+  }
   if (info.should_stop != 0) { /* the flow still evolves: no stop */
     fprintf(stderr, "should_stop set again on an evolving flow\n");
     return 1;

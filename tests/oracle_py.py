@@ -45,6 +45,7 @@ def olib():
         L.oracle_step.argtypes = [vp]
         L.oracle_get_step_info.argtypes = [vp, C.POINTER(_ffi.StepInfo)]
         L.oracle_set_stop_state.argtypes = [vp, C.c_int, C.c_uint32, C.c_uint32]
+        L.oracle_set_n_outer_correctors.argtypes = [vp, C.c_int]
         L.oracle_debug_buffer_len.argtypes = [vp, C.c_int]
         L.oracle_debug_buffer_len.restype = C.c_size_t
         L.oracle_debug_buffer.argtypes = [vp, C.c_int, C.POINTER(C.c_float), C.c_size_t]
@@ -173,6 +174,13 @@ class OracleSolver:
                    steady_state_count=i.steady_state_count)
         cur.update(kw)
         self.set_stop_state(**cur)
+
+    @property
+    def n_outer_correctors(self): return int(self._cfg.n_outer_correctors)
+    @n_outer_correctors.setter
+    def n_outer_correctors(self, v):
+        self._cfg.n_outer_correctors = int(v)
+        olib().oracle_set_n_outer_correctors(self._h, int(v))
 
     @property
     def should_stop(self): return bool(self.step_info().should_stop)

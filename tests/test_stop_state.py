@@ -21,8 +21,9 @@ import numpy as np
 import pytest
 
 from cfd2_amd import GpuSolver, default_config
-from tests.meshes import channel_obstacle
+from tests.meshes import backwards_step, channel_obstacle
 from tests.oracle_py import OracleSolver
+from tests.test_oracle import setup_amg_test
 
 
 def _frozen_setup(s, mesh):
@@ -143,3 +144,35 @@ def test_zero_flow_stop_gpu():
     g.step()
     assert _info(g) == (0, 0, 0)
     g.close()
+
+
+def test_n_outer_correctors_writable_oracle_cpu():
+    """structs.rs:238: a public field, read by every step (coupled_solver.rs:111,
+    at least 10): amg_test reaches the 20-iteration cap; written to 12 the next
+    step stops at 12; written to 5 it still runs 10 (the max with 10)."""
+    mesh = backwards_step()
+    o = OracleSolver(mesh)
+    setup_amg_test(o, mesh, 1)
+    o.step()
+    assert o.step_info().outer_iterations == 20
+    o.n_outer_correctors = 12
+    o.step()
+    assert o.step_info().outer_iterations == 12
+    o.n_outer_correctors = 5
+    o.step()
+    assert o.step_info().outer_iterations == 10
+
+
+@pytest.mark.gpu
+def test_n_outer_correctors_gpu_matches_oracle():
+    mesh = backwards_step()
+    g, o = GpuSolver(mesh), OracleSolver(mesh)
+    for s in (g, o):
+        setup_amg_test(s, mesh, 1)
+    for k, n in enumerate((20, 12, 5, 25)):
+        for s in (g, o):
+            s.n_outer_correctors = n
+            s.step()
+        assert g.step_info().outer_iterations == o.step_info().outer_iterations, (k, n)
+        assert np.array_equal(g.get_u(), o.get_u()) and np.array_equal(g.get_p(), o.get_p()), (k, n)
+    assert g.n_outer_correctors == 25
