@@ -87,7 +87,7 @@ def cases():
     for pc, tag in ((1, "amg"), (0, "jacobi")):
         out.append((f"fixed_{tag}", backwards_step, lambda s, m, pc=pc: setup_amg_test(s, m, pc), fixed, 3,
                     "ABC" if pc else "AB"))
-    out.append(("c0_voronoi", c0_mesh, c0_setup, dict(convergence_lag=0, fixed_outer=2, fixed_inner=8), 2, "BC"))
+    out.append(("c0_voronoi", c0_mesh, c0_setup, dict(convergence_lag=0, fixed_outer=2, fixed_inner=8), 2, "ABC"))
     return out
 
 
