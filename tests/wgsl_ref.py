@@ -199,6 +199,10 @@ class WgslRefSolver(refpy.RefSolver):
 
     # ------------------------------------------------------------ plumbing
     def _run(self, D, entry, bindings, groups):
+        # wgpu refuses a dispatch dimension above 65,535 workgroups (the
+        # reference's mesh-size ceiling): so does this driver
+        if max(groups) > 65535:
+            raise ValueError(f"{entry}: {groups} workgroups exceed wgpu's 65,535 per dimension")
         if D is _SHADERS.get("amg"):
             D.dispatch(entry, bindings, groups, schedule=self.amg_sched[0], bounds=self.amg_sched[1])
         else:
