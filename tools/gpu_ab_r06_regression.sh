@@ -6,6 +6,8 @@
 #   nokpre  base without kernarg preload
 #   nohead  base with the smoother's leading-argument change reverted
 #   nt64    base with CFD_NT=111 (the level-1 residual nontemporal too)
+#   phead   base with the Schur prediction's first-needed fields and grid size
+#           as leading (preloaded) arguments (/tmp patch, tools/gpu_ab_phead.sh)
 # Usage: bash tools/gpu_ab_r06_regression.sh [variants...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -19,7 +21,7 @@ for k in $(seq 1 $ROUNDS); do
     bench=$R/bench.py; lib=$R/cfd-demo2_amd/cfd2_amd/_lib/libcfd2_amd.so; extra=""
     case $v in
       r04) bench=$R/abtrees/r04/bench.py; lib=$R/abtrees/r04/cfd-demo2_amd/cfd2_amd/_lib/libcfd2_amd.so ;;
-      nokpre|nohead) lib=$R/cfd-demo2_amd/cfd2_amd/_lib/ab/libcfd2_amd_$v.so ;;
+      nokpre|nohead|phead) lib=$R/cfd-demo2_amd/cfd2_amd/_lib/ab/libcfd2_amd_$v.so ;;
       nt64) extra="CFD_NT=111" ;;
     esac
     env $extra CFD2_AMD_LIB=$lib timeout -k 10 300 python $bench --config $CFG --steps ${STEPS:-10} --no-cpu-baseline \
