@@ -96,7 +96,10 @@ def _setup(s, mesh, phys, useed):
     s.update_constants()
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
+_SEED0 = int(os.environ.get("CFD_SWEEP_SEED0", "0"))  # fresh cases: CFD_SWEEP_SEED0=1000
+
+
+@pytest.mark.parametrize("seed", range(_SEED0, _SEED0 + int(os.environ.get("CFD_SWEEP_CASES", "32"))))  # wider: CFD_SWEEP_CASES=N
 def test_random_case_parity(seed, monkeypatch):
     kind, mesh, cfg, phys, nranks, useed, graph, pairs, refsem = _case(seed)
     # ranks own whole reduction segments (>= 256 cells): small meshes take fewer ranks
